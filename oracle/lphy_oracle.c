@@ -1,0 +1,618 @@
+/* TEST INFRASTRUCTURE ONLY — CPU oracle for the LoRa PHY demodulation path.
+ *
+ * A plain-C restatement of the reference algorithm (file:line citations on
+ * every function).  It calls the same glibc libm routines the reference does
+ * (sincosf, atan2f, cabsf, log10f, cosf), so on the same host it reproduces
+ * the reference bit for bit; tests/test_oracle.py checks that against
+ * oracle/_ref (the reference compiled from its own sources) and against the
+ * committed fixtures in tests/golden/.
+ *
+ * Not part of the product: nothing under lora-sdr-...-clean_amd/ links it.
+ * Build: oracle/Makefile (-O2 -ffp-contract=off, no -march).
+ */
+#define _GNU_SOURCE
+#include "lphy_oracle.h"
+
+#include <complex.h>
+#include <errno.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#define ORC_PI 3.14159265358979323846f /* phy.hpp:20, as float */
+#define ORC_MAX_N 4096
+
+typedef struct { float re, im; } cpx;
+
+static inline cpx cmul(cpx a, cpx b) {
+    /* GCC's inline complex<float> product (finite operands) */
+    cpx r;
+    r.re = a.re * b.re - a.im * b.im;
+    r.im = a.re * b.im + a.im * b.re;
+    return r;
+}
+static inline cpx cadd(cpx a, cpx b) { cpx r = {a.re + b.re, a.im + b.im}; return r; }
+static inline cpx csub(cpx a, cpx b) { cpx r = {a.re - b.re, a.im - b.im}; return r; }
+static inline cpx cscale(cpx a, float s) { cpx r = {a.re * s, a.im * s}; return r; }
+
+/* ---------------------------------------------------------------------- */
+/* ChirpGenerator.hpp:24-51                                                 */
+/* ---------------------------------------------------------------------- */
+int orc_genchirp(float* out, int N, int osr, int NN, float f0, int down,
+                 float ampl, float* phase, float bw_scale) {
+    const float fmin = -ORC_PI * bw_scale / (float)osr;
+    const float fmax = ORC_PI * bw_scale / (float)osr;
+    const float fstep = (2.0f * ORC_PI * bw_scale) / (float)(N * osr * osr);
+    float f = fmin + f0;
+    float ph = *phase;
+    int i;
+    for (i = 0; i < NN; ++i) {
+        f += fstep;
+        if (f > fmax) f -= (fmax - fmin);
+        if (down) ph -= f; else ph += f;
+        float s, c;
+        sincosf(ph, &s, &c);
+        out[2 * i] = ampl * c;
+        out[2 * i + 1] = ampl * s;
+    }
+    /* final wrap: unqualified floor() on a float resolves to ::floor(double)
+     * in the reference's template, so the wrap is evaluated in double */
+    double w = floor((double)(ph / (2.0f * ORC_PI))) * 2 * ORC_PI;
+    ph = (float)((double)ph - w);
+    *phase = ph;
+    return i;
+}
+
+/* ---------------------------------------------------------------------- */
+/* kissfft.hh:71-185 — iterative form of KISS's recursive mixed-radix DIT.  */
+/* Stage l (radix p, remainder m, stride fs = p_0..p_{l-1}) combines blocks  */
+/* of p*m outputs; stages run innermost first.  The leaf permutation puts   */
+/* input sum(q_l*fs_l) at output sum(q_l*m_l).  Butterflies are KISS's.     */
+/* ---------------------------------------------------------------------- */
+typedef struct {
+    int n, stages;
+    int radix[32], rem[32], fs[32];
+    cpx tw[ORC_MAX_N];
+} orc_plan;
+
+static void orc_plan_init(orc_plan* P, int nfft) {
+    P->n = nfft;
+    const float phinc = (-2.0f * acosf(-1.0f)) / (float)nfft; /* kissfft.hh:26 */
+    for (int i = 0; i < nfft; ++i) {
+        float s, c;
+        sincosf((float)i * phinc, &s, &c);
+        P->tw[i].re = c;
+        P->tw[i].im = s;
+    }
+    int n = nfft, p = 4, st = 0; /* kissfft.hh:78-98 */
+    do {
+        while (n % p) {
+            if (p == 4) p = 2;
+            else if (p == 2) p = 3;
+            else p += 2;
+            if (p * p > n) p = n;
+        }
+        n /= p;
+        P->radix[st] = p;
+        P->rem[st] = n;
+        ++st;
+    } while (n > 1);
+    P->stages = st;
+    int f = 1;
+    for (int l = 0; l < st; ++l) { P->fs[l] = f; f *= P->radix[l]; }
+}
+
+static void orc_fft_plan(const orc_plan* P, const cpx* in, cpx* out) {
+    const int N = P->n, L = P->stages;
+    /* leaf permutation */
+    for (int j = 0; j < N; ++j) {
+        int rest = j, pos = 0, idx = 0;
+        /* digits q_l of the output position, most significant = stage 0 */
+        for (int l = 0; l < L; ++l) {
+            int q = rest / P->rem[l];
+            rest -= q * P->rem[l];
+            pos += q * P->rem[l];
+            idx += q * P->fs[l];
+        }
+        out[pos] = in[idx];
+    }
+    for (int l = L - 1; l >= 0; --l) {
+        const int p = P->radix[l], m = P->rem[l], fs = P->fs[l];
+        for (int b = 0; b < N; b += p * m) {
+            cpx* F = out + b;
+            if (p == 2) { /* kissfft.hh:155-162 */
+                for (int k = 0; k < m; ++k) {
+                    cpx t = cmul(F[m + k], P->tw[k * fs]);
+                    F[m + k] = csub(F[k], t);
+                    F[k] = cadd(F[k], t);
+                }
+            } else { /* p == 4, forward; kissfft.hh:164-185 */
+                for (int k = 0; k < m; ++k) {
+                    cpx s0 = cmul(F[k + m], P->tw[k * fs]);
+                    cpx s1 = cmul(F[k + 2 * m], P->tw[k * fs * 2]);
+                    cpx s2 = cmul(F[k + 3 * m], P->tw[k * fs * 3]);
+                    cpx s5 = csub(F[k], s1);
+                    cpx a0 = cadd(F[k], s1);
+                    cpx s3 = cadd(s0, s2);
+                    cpx s4 = csub(s0, s2);
+                    cpx r4 = {s4.im * 1.0f, -s4.re * 1.0f};
+                    F[k + 2 * m] = csub(a0, s3);
+                    F[k] = cadd(a0, s3);
+                    F[k + m] = cadd(s5, r4);
+                    F[k + 3 * m] = csub(s5, r4);
+                }
+            }
+        }
+    }
+}
+
+void orc_fft(const float* in, float* out, int nfft) {
+    orc_plan* P = (orc_plan*)malloc(sizeof(orc_plan));
+    orc_plan_init(P, nfft);
+    orc_fft_plan(P, (const cpx*)in, (cpx*)out);
+    free(P);
+}
+
+/* ---------------------------------------------------------------------- */
+/* LoRaDetector.hpp:39-74                                                   */
+/* ---------------------------------------------------------------------- */
+static size_t orc_detect_plan(const orc_plan* P, const cpx* in, cpx* out,
+                              float* power, float* power_avg, float* findex) {
+    const int N = P->n;
+    const float power_scale = (float)(20.0 * log10((double)N)); /* :27 */
+    orc_fft_plan(P, in, out);
+    size_t max_index = 0;
+    float max_value = 0.0f;
+    double total = 0.0;
+    for (int i = 0; i < N; ++i) {
+        float mag2 = out[i].re * out[i].re + out[i].im * out[i].im;
+        total += mag2;
+        if (mag2 > max_value) { max_index = (size_t)i; max_value = mag2; }
+    }
+    const float noise = sqrtf((float)(total - (double)max_value));
+    const float fundamental = sqrtf(max_value);
+    *power_avg = 20.0f * log10f(noise) - power_scale;
+    *power = 20.0f * log10f(fundamental) - power_scale;
+    cpx lb = out[max_index > 0 ? max_index - 1 : (size_t)N - 1];
+    cpx rb = out[max_index < (size_t)N - 1 ? max_index + 1 : 0];
+    float left = cabsf(lb.re + I * lb.im);
+    float right = cabsf(rb.re + I * rb.im);
+    const double demon = (2.0 * (double)fundamental) - (double)right - (double)left;
+    if (demon == 0.0) *findex = 0.0f;
+    else *findex = (float)(0.5 * (double)(right - left) / demon);
+    return max_index;
+}
+
+size_t orc_detect(const float* fft_in, float* fft_out, int N, float* power,
+                  float* power_avg, float* findex) {
+    orc_plan* P = (orc_plan*)malloc(sizeof(orc_plan));
+    orc_plan_init(P, N);
+    size_t r = orc_detect_plan(P, (const cpx*)fft_in, (cpx*)fft_out, power,
+                               power_avg, findex);
+    free(P);
+    return r;
+}
+
+/* ---------------------------------------------------------------------- */
+/* Codes: LoRaCodes.hpp:69-105, 229-281; LoRaEncoder.cpp; LoRaDecoder.cpp   */
+/* ---------------------------------------------------------------------- */
+uint8_t orc_encode_hamming84(uint8_t x) {
+    unsigned d0 = x & 1, d1 = (x >> 1) & 1, d2 = (x >> 2) & 1, d3 = (x >> 3) & 1;
+    unsigned b = x & 0xf;
+    b |= (d0 ^ d1 ^ d2) << 4;
+    b |= (d1 ^ d2 ^ d3) << 5;
+    b |= (d0 ^ d1 ^ d3) << 6;
+    b |= (d0 ^ d2 ^ d3) << 7;
+    return (uint8_t)b;
+}
+
+uint8_t orc_decode_hamming84(uint8_t b) {
+    unsigned bit[8];
+    for (int i = 0; i < 8; ++i) bit[i] = (b >> i) & 1;
+    unsigned p0 = bit[0] ^ bit[1] ^ bit[2] ^ bit[4];
+    unsigned p1 = bit[1] ^ bit[2] ^ bit[3] ^ bit[5];
+    unsigned p2 = bit[0] ^ bit[1] ^ bit[3] ^ bit[6];
+    unsigned p3 = bit[0] ^ bit[2] ^ bit[3] ^ bit[7];
+    unsigned syn = p0 | (p1 << 1) | (p2 << 2) | (p3 << 3);
+    switch (syn) {
+        case 0xD: return (b ^ 1) & 0xf;
+        case 0x7: return (b ^ 2) & 0xf;
+        case 0xB: return (b ^ 4) & 0xf;
+        case 0xE: return (b ^ 8) & 0xf;
+        default: return b & 0xf; /* 0,1,2,4,8 and uncorrectable */
+    }
+}
+
+static uint16_t crc16sx(uint16_t crc, uint16_t poly) {
+    for (int i = 0; i < 8; ++i)
+        crc = (crc & 0x8000) ? (uint16_t)((crc << 1) ^ poly) : (uint16_t)(crc << 1);
+    return crc;
+}
+static uint8_t xsum8(uint8_t t) {
+    t ^= t >> 4; t ^= t >> 2; t ^= t >> 1;
+    return t & 1;
+}
+uint16_t orc_sx1272_checksum(const uint8_t* data, int len) {
+    uint16_t res = 0, crc = 0;
+    uint8_t v = 0xff;
+    for (int i = 0; i < len; ++i) {
+        crc = crc16sx(res, 0x1021);
+        v = (uint8_t)(xsum8(v & 0xB8) | (v << 1));
+        res = crc ^ data[i];
+    }
+    res ^= v;
+    v = (uint8_t)(xsum8(v & 0xB8) | (v << 1));
+    res ^= (uint16_t)(v << 8);
+    return res;
+}
+
+size_t orc_lora_encode(const uint8_t* bytes, size_t n, uint16_t* out) {
+    size_t k = 0;
+    for (size_t i = 0; i < n; ++i) {
+        out[k++] = orc_encode_hamming84(bytes[i] >> 4);
+        out[k++] = orc_encode_hamming84(bytes[i] & 0x0f);
+    }
+    return k;
+}
+
+ssize_t orc_lora_decode(const uint16_t* syms, size_t n, uint8_t* out) {
+    if (n % 2) return -EINVAL;
+    size_t k = 0;
+    for (size_t i = 0; i + 1 < n; i += 2) {
+        uint8_t hi = orc_decode_hamming84((uint8_t)syms[i]) & 0x0f;
+        uint8_t lo = orc_decode_hamming84((uint8_t)syms[i + 1]) & 0x0f;
+        out[k++] = (uint8_t)((hi << 4) | lo);
+    }
+    return (ssize_t)k;
+}
+
+/* phy.cpp:245-261 */
+ssize_t orc_decode(const uint16_t* syms, size_t n, uint8_t* out, size_t cap,
+                   uint8_t* crc_out) {
+    if (!syms || !out) return -EINVAL;
+    ssize_t produced = orc_lora_decode(syms, n, out);
+    if (produced < 0) return produced;
+    if ((size_t)produced > cap) return -ERANGE;
+    if (produced >= 4) {
+        uint16_t provided = (uint16_t)(out[produced - 2] | (out[produced - 1] << 8));
+        uint16_t calc = orc_sx1272_checksum(out + 2, (int)(produced - 4));
+        if (crc_out) *crc_out = provided == calc;
+    } else if (crc_out) {
+        *crc_out = 0;
+    }
+    return produced;
+}
+
+/* ---------------------------------------------------------------------- */
+/* LoRaMod.cpp:8-43                                                         */
+/* ---------------------------------------------------------------------- */
+size_t orc_lora_modulate(const uint16_t* syms, size_t n, float* out,
+                         unsigned sf, unsigned osr, unsigned bw_hz,
+                         float ampl, uint8_t sync) {
+    const size_t N = (size_t)1 << sf;
+    const size_t step = N * osr;
+    const float bws = (float)bw_hz / 125000.0f;
+    float phase = 0.0f;
+    if (ampl > 1.0f) ampl = 1.0f;
+    if (ampl < -1.0f) ampl = -1.0f;
+    unsigned shift = sf > 4 ? sf - 4 : 0;
+    const uint16_t sw[2] = {(uint16_t)((sync >> 4) << shift),
+                            (uint16_t)((sync & 0x0f) << shift)};
+    for (size_t s = 0; s < n + 2; ++s) {
+        uint16_t v = s < 2 ? sw[s] : syms[s - 2];
+        const float f0 = (2.0f * ORC_PI * (float)v * bws) / ((float)N * (float)osr);
+        orc_genchirp(out + 2 * s * step, (int)N, (int)osr, (int)step, f0, 0,
+                     ampl, &phase, bws);
+    }
+    return (n + 2) * step;
+}
+
+/* ---------------------------------------------------------------------- */
+/* Offset estimate shared by both demodulators.                             */
+/* LoRaDemod.cpp:80-136 (tie_low=1) and phy.cpp:81-148 (tie_low=0).         */
+/* ---------------------------------------------------------------------- */
+typedef struct { float cfo, time_offset; } orc_metrics;
+
+static void hann_window(float* w, size_t N) {
+    /* LoRaDemod.cpp:17-21 / phy.cpp:37-42 */
+    for (size_t i = 0; i < N; ++i)
+        w[i] = 0.5f - 0.5f * cosf(2.0f * ORC_PI * (float)i / ((float)N - 1.0f));
+}
+
+static orc_metrics estimate(const orc_plan* P, const cpx* samples,
+                            size_t est_syms, unsigned osr, const float* win,
+                            int tie_low, cpx* fin, cpx* fout) {
+    const size_t N = (size_t)P->n, step = N * osr;
+    float sum_index = 0.0f, phase_diff = 0.0f, prev_phase = 0.0f;
+    int have_prev = 0;
+    unsigned sum_t = 0;
+    for (size_t s = 0; s < est_syms; ++s) {
+        const cpx* sym = samples + s * step;
+        float best_p = -1e30f, best_f = 0.0f;
+        size_t best_idx = 0;
+        unsigned best_t = 0;
+        cpx best_bin = {0.0f, 0.0f};
+        for (unsigned t = 0; t < osr; ++t) {
+            for (size_t i = 0; i < N; ++i) {
+                cpx v = sym[t + i * osr];
+                if (win) v = cscale(v, win[i]);
+                fin[i] = v;
+            }
+            float p, pav, fi;
+            size_t idx = orc_detect_plan(P, fin, fout, &p, &pav, &fi);
+            if (p > best_p || (tie_low && p == best_p && idx < best_idx)) {
+                best_p = p; best_idx = idx; best_f = fi; best_t = t;
+                best_bin = fout[idx];
+            }
+        }
+        sum_t += best_t;
+        sum_index += (float)best_idx + best_f;
+        float phase = atan2f(best_bin.im, best_bin.re);
+        if (have_prev) {
+            float d = phase - prev_phase;
+            while (d > ORC_PI) d -= 2.0f * ORC_PI;
+            while (d < -ORC_PI) d += 2.0f * ORC_PI;
+            phase_diff += d;
+        }
+        prev_phase = phase;
+        have_prev = 1;
+    }
+    orc_metrics m;
+    float avg_index = sum_index / (float)est_syms;
+    float cfo_coarse = avg_index / (float)N;
+    float cfo_fine = 0.0f;
+    if (est_syms > 1)
+        cfo_fine = (phase_diff / (float)(est_syms - 1)) / (2.0f * ORC_PI * (float)N);
+    m.cfo = cfo_coarse + cfo_fine;
+    float frac = avg_index - floorf(avg_index + 0.5f);
+    float avg_t = (float)sum_t / (float)est_syms;
+    m.time_offset = avg_t - frac * (float)N * (float)osr;
+    return m;
+}
+
+/* x86-64 cvttss2si semantics for (int)roundf(x): out of range / NaN -> INT_MIN */
+static int round_to_int(float x) {
+    float r = roundf(x);
+    if (!(r >= -2147483648.0f && r < 2147483648.0f)) return (int)0x80000000u;
+    return (int)r;
+}
+
+static size_t shifted_base(size_t s, size_t step, int t_off, size_t count) {
+    /* LoRaDemod.cpp:144-151 / phy.cpp:209-216 */
+    size_t base = s * step;
+    if (t_off > 0) {
+        if (base + (size_t)t_off + step <= count) base += (size_t)t_off;
+    } else if (t_off < 0) {
+        size_t off = (size_t)(-(int64_t)t_off);
+        if (t_off == (int)0x80000000u) off = (size_t)(int64_t)t_off; /* -INT_MIN wraps */
+        if (off <= base) base -= off;
+    }
+    return base;
+}
+
+/* ---------------------------------------------------------------------- */
+/* LoRaDemod.cpp:50-197                                                     */
+/* ---------------------------------------------------------------------- */
+ssize_t orc_lora_demodulate(unsigned sf, int hann, const float* samples_f,
+                            size_t count, uint16_t* out, unsigned osr,
+                            uint8_t* out_sync, size_t scratch_len,
+                            float* metrics_out) {
+    const cpx* samples = (const cpx*)samples_f;
+    const size_t N = (size_t)1 << sf, step = N * osr;
+    const size_t total = count / step;
+    const int have_sync = total >= 2;
+    orc_plan* P = (orc_plan*)malloc(sizeof(orc_plan));
+    orc_plan_init(P, (int)N);
+    float* win = NULL;
+    float winbuf[ORC_MAX_N];
+    if (hann) { hann_window(winbuf, N); win = winbuf; }
+
+    float max_amp = 0.0f;
+    for (size_t i = 0; i < count; ++i) {
+        float r = fabsf(samples[i].re), im = fabsf(samples[i].im);
+        float m = (r < im) ? im : r; /* std::max(r, im) */
+        if (m > max_amp) max_amp = m;
+    }
+    const cpx* x = samples;
+    cpx* scratch = NULL;
+    if (max_amp > 1.0f) {
+        if (scratch_len < count) { free(P); return -ERANGE; }
+        scratch = (cpx*)malloc(count * sizeof(cpx));
+        float scale = 1.0f / max_amp;
+        for (size_t i = 0; i < count; ++i) scratch[i] = cscale(samples[i], scale);
+        x = scratch;
+    }
+
+    cpx fin[ORC_MAX_N], fout[ORC_MAX_N];
+    const size_t est_syms = total < 2 ? total : 2;
+    orc_metrics m = estimate(P, x, est_syms, osr, win, 1, fin, fout);
+    if (metrics_out) { metrics_out[0] = m.cfo; metrics_out[1] = m.time_offset; }
+
+    const int t_off = round_to_int(m.time_offset);
+    const float rate = -2.0f * ORC_PI * m.cfo / (float)N;
+    uint16_t sw0 = 0, sw1 = 0;
+    size_t k = 0;
+    for (size_t s = 0; s < total; ++s) {
+        const cpx* sym = x + shifted_base(s, step, t_off, count);
+        const float start = rate * ((float)(s * N) + (float)t_off / (float)osr);
+        for (size_t i = 0; i < N; ++i) {
+            float ph = start + rate * (float)i;
+            float sn, cs;
+            sincosf(ph, &sn, &cs);
+            cpx rot = {cs, sn};
+            cpx v = cmul(sym[i * osr], rot);
+            if (win) v = cscale(v, win[i]);
+            fin[i] = v;
+        }
+        float p, pav, fi;
+        size_t idx = orc_detect_plan(P, fin, fout, &p, &pav, &fi);
+        if (have_sync) {
+            if (s == 0) sw0 = (uint16_t)idx;
+            else if (s == 1) sw1 = (uint16_t)idx;
+            else out[k++] = (uint16_t)idx;
+        } else {
+            out[k++] = (uint16_t)idx;
+        }
+    }
+    if (out_sync) {
+        if (have_sync) {
+            unsigned sfb = 0;
+            for (size_t t = N; t > 1; t >>= 1) ++sfb;
+            unsigned shift = sfb > 4 ? sfb - 4 : 0;
+            uint8_t hi = (uint8_t)(sw0 >> shift) & 0x0f;
+            uint8_t lo = (uint8_t)(sw1 >> shift) & 0x0f;
+            *out_sync = (uint8_t)((hi << 4) | lo);
+        } else {
+            *out_sync = 0;
+        }
+    }
+    free(scratch);
+    free(P);
+    return have_sync ? (ssize_t)k : (ssize_t)total;
+}
+
+/* ---------------------------------------------------------------------- */
+/* phy.cpp:81-148                                                           */
+/* ---------------------------------------------------------------------- */
+void orc_estimate_offsets(unsigned sf, unsigned osr, int hann,
+                          const float* iq, size_t count, float* metrics_out) {
+    const size_t N = (size_t)1 << sf;
+    if (!osr) osr = 1;
+    const size_t syms = count / (N * osr);
+    if (!iq || count == 0 || syms == 0) return;
+    orc_plan* P = (orc_plan*)malloc(sizeof(orc_plan));
+    orc_plan_init(P, (int)N);
+    float winbuf[ORC_MAX_N];
+    if (hann) hann_window(winbuf, N);
+    cpx fin[ORC_MAX_N], fout[ORC_MAX_N];
+    orc_metrics m = estimate(P, (const cpx*)iq, syms, osr,
+                             hann ? winbuf : NULL, 0, fin, fout);
+    metrics_out[0] = m.cfo;
+    metrics_out[1] = m.time_offset;
+    free(P);
+}
+
+/* ---------------------------------------------------------------------- */
+/* phy.cpp:182-243                                                          */
+/* ---------------------------------------------------------------------- */
+ssize_t orc_demodulate(unsigned sf, unsigned bw_hz, unsigned osr, int hann,
+                       const float* iq_f, size_t count, uint16_t* syms,
+                       size_t cap, float* metrics_out, uint8_t sync_in,
+                       uint8_t* sync_out) {
+    if (sync_out) *sync_out = sync_in;
+    if (!iq_f || !syms) return -EINVAL;
+    if (!osr) osr = 1;
+    const cpx* iq = (const cpx*)iq_f;
+    const size_t N = (size_t)1 << sf, step = N * osr;
+    if (count % step != 0) return -EINVAL;
+    const size_t total = count / step;
+    if (total < 2) return -ERANGE;
+    if (total - 2 > cap) return -ERANGE;
+
+    orc_plan* P = (orc_plan*)malloc(sizeof(orc_plan));
+    orc_plan_init(P, (int)N);
+    float winbuf[ORC_MAX_N];
+    const float* win = NULL;
+    if (hann) { hann_window(winbuf, N); win = winbuf; }
+    cpx fin[ORC_MAX_N], fout[ORC_MAX_N];
+    orc_metrics m = estimate(P, iq, 2, osr, win, 0, fin, fout);
+    if (metrics_out) { metrics_out[0] = m.cfo; metrics_out[1] = m.time_offset; }
+
+    float down[2 * ORC_MAX_N];
+    float tmp = 0.0f;
+    orc_genchirp(down, (int)N, 1, (int)N, 0.0f, 1, 1.0f, &tmp,
+                 (float)bw_hz / 125000.0f);
+    const int t_off = round_to_int(m.time_offset);
+    const float rate = -2.0f * ORC_PI * m.cfo / (float)N;
+    uint16_t sw0 = 0, sw1 = 0;
+    for (size_t s = 0; s < total; ++s) {
+        const cpx* sym = iq + shifted_base(s, step, t_off, count);
+        const float start = rate * ((float)(s * N) + (float)t_off / (float)osr);
+        for (size_t i = 0; i < N; ++i) {
+            float ph = start + rate * (float)i;
+            float sn, cs;
+            sincosf(ph, &sn, &cs);
+            cpx rot = {cs, sn};
+            cpx d = {down[2 * i], down[2 * i + 1]};
+            cpx v = cmul(cmul(sym[i * osr], d), rot);
+            if (win) v = cscale(v, win[i]);
+            fin[i] = v;
+        }
+        float p, pav, fi;
+        size_t idx = orc_detect_plan(P, fin, fout, &p, &pav, &fi);
+        if (s == 0) sw0 = (uint16_t)idx;
+        else if (s == 1) sw1 = (uint16_t)idx;
+        else syms[s - 2] = (uint16_t)idx;
+    }
+    unsigned shift = sf > 4 ? sf - 4 : 0;
+    if (sync_out)
+        *sync_out = (uint8_t)((((sw0 >> shift) & 0x0f) << 4) | ((sw1 >> shift) & 0x0f));
+    free(P);
+    return (ssize_t)(total - 2);
+}
+
+/* ---------------------------------------------------------------------- */
+/* CPU timing harness (bench.py cpu_baseline, kind "port")                  */
+/* ---------------------------------------------------------------------- */
+typedef struct {
+    int mode; unsigned sf, bw_hz; const float* iq; size_t f0, f1, fs;
+    uint8_t* bytes;
+} orc_job;
+
+static void* orc_worker(void* arg) {
+    orc_job* j = (orc_job*)arg;
+    const size_t N = (size_t)1 << j->sf, nsym = j->fs / N;
+    const size_t ndata = nsym >= 2 ? nsym - 2 : 0;
+    uint16_t* syms = (uint16_t*)malloc((nsym + 2) * sizeof(uint16_t));
+    float* dech = (float*)malloc(j->fs * 2 * sizeof(float));
+    float down[2 * ORC_MAX_N], tmp = 0.0f;
+    orc_genchirp(down, (int)N, 1, (int)N, 0.0f, 1, 1.0f, &tmp,
+                 (float)j->bw_hz / 125000.0f);
+    for (size_t f = j->f0; f < j->f1; ++f) {
+        const float* x = j->iq + 2 * f * j->fs;
+        uint8_t* b = j->bytes + f * (ndata / 2);
+        if (j->mode == 1) {
+            for (size_t i = 0; i < j->fs; ++i) {
+                cpx a = {x[2 * i], x[2 * i + 1]};
+                cpx d = {down[2 * (i % N)], down[2 * (i % N) + 1]};
+                cpx r = cmul(a, d);
+                dech[2 * i] = r.re; dech[2 * i + 1] = r.im;
+            }
+            orc_lora_demodulate(j->sf, 0, dech, j->fs, syms, 1, NULL, j->fs, NULL);
+            orc_lora_decode(syms, ndata & ~(size_t)1, b);
+        } else {
+            orc_demodulate(j->sf, j->bw_hz, 1, 0, x, j->fs, syms, nsym, NULL,
+                           0x12, NULL);
+            orc_decode(syms, ndata & ~(size_t)1, b, ndata / 2, NULL);
+        }
+    }
+    free(syms);
+    free(dech);
+    return NULL;
+}
+
+double orc_bench(int mode, unsigned sf, unsigned bw_hz, const float* iq,
+                 size_t frames, size_t frame_samples, uint8_t* bytes_out,
+                 int threads) {
+    if (threads < 1) threads = 1;
+    pthread_t th[256];
+    orc_job jobs[256];
+    if (threads > 256) threads = 256;
+    size_t per = (frames + (size_t)threads - 1) / (size_t)threads;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    int started = 0;
+    for (int t = 0; t < threads; ++t) {
+        size_t a = (size_t)t * per, b = a + per < frames ? a + per : frames;
+        if (a >= b) break;
+        orc_job jb = {mode, sf, bw_hz, iq, a, b, frame_samples, bytes_out};
+        jobs[t] = jb;
+        pthread_create(&th[t], NULL, orc_worker, &jobs[t]);
+        ++started;
+    }
+    for (int t = 0; t < started; ++t) pthread_join(th[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

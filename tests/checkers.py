@@ -1,0 +1,292 @@
+"""ctypes bindings for the two CPU checkers (TEST INFRASTRUCTURE ONLY).
+
+* ``Oracle``    -> oracle/_build/liblphy_oracle.so  (our C restatement)
+* ``Reference`` -> oracle/_ref/libloraref.so        (the reference itself,
+                   compiled from /root/reference's own sources by
+                   oracle/Makefile; absent on boxes where it was never built)
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module.  The product never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+ORACLE_SO = ROOT / "oracle" / "_build" / "liblphy_oracle.so"
+REF_SO = ROOT / "oracle" / "_ref" / "libloraref.so"
+
+_f32p = C.POINTER(C.c_float)
+_u16p = C.POINTER(C.c_uint16)
+_u8p = C.POINTER(C.c_uint8)
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t) if a is not None else None
+
+
+def _cf(iq: np.ndarray) -> np.ndarray:
+    """complex64 / interleaved float32 -> contiguous float32 view."""
+    iq = np.ascontiguousarray(iq)
+    if iq.dtype == np.complex64:
+        return iq.view(np.float32)
+    assert iq.dtype == np.float32
+    return iq
+
+
+def build_oracle() -> None:
+    import subprocess
+    subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "oracle"], check=True)
+
+
+class Oracle:
+    def __init__(self, path: Path = ORACLE_SO):
+        if not path.exists():
+            build_oracle()
+        L = self.lib = C.CDLL(str(path))
+        L.orc_genchirp.argtypes = [_f32p, C.c_int, C.c_int, C.c_int, C.c_float,
+                                   C.c_int, C.c_float, _f32p, C.c_float]
+        L.orc_fft.argtypes = [_f32p, _f32p, C.c_int]
+        L.orc_detect.argtypes = [_f32p, _f32p, C.c_int, _f32p, _f32p, _f32p]
+        L.orc_detect.restype = C.c_size_t
+        L.orc_lora_modulate.argtypes = [_u16p, C.c_size_t, _f32p, C.c_uint, C.c_uint,
+                                        C.c_uint, C.c_float, C.c_uint8]
+        L.orc_lora_modulate.restype = C.c_size_t
+        L.orc_lora_encode.argtypes = [_u8p, C.c_size_t, _u16p]
+        L.orc_lora_encode.restype = C.c_size_t
+        L.orc_lora_decode.argtypes = [_u16p, C.c_size_t, _u8p]
+        L.orc_lora_decode.restype = C.c_ssize_t
+        L.orc_sx1272_checksum.argtypes = [_u8p, C.c_int]
+        L.orc_sx1272_checksum.restype = C.c_uint16
+        L.orc_decode_hamming84.argtypes = [C.c_uint8]
+        L.orc_decode_hamming84.restype = C.c_uint8
+        L.orc_encode_hamming84.argtypes = [C.c_uint8]
+        L.orc_encode_hamming84.restype = C.c_uint8
+        L.orc_lora_demodulate.argtypes = [C.c_uint, C.c_int, _f32p, C.c_size_t, _u16p,
+                                          C.c_uint, _u8p, C.c_size_t, _f32p]
+        L.orc_lora_demodulate.restype = C.c_ssize_t
+        L.orc_demodulate.argtypes = [C.c_uint, C.c_uint, C.c_uint, C.c_int, _f32p,
+                                     C.c_size_t, _u16p, C.c_size_t, _f32p, C.c_uint8, _u8p]
+        L.orc_demodulate.restype = C.c_ssize_t
+        L.orc_estimate_offsets.argtypes = [C.c_uint, C.c_uint, C.c_int, _f32p,
+                                           C.c_size_t, _f32p]
+        L.orc_decode.argtypes = [_u16p, C.c_size_t, _u8p, C.c_size_t, _u8p]
+        L.orc_decode.restype = C.c_ssize_t
+        L.orc_bench.argtypes = [C.c_int, C.c_uint, C.c_uint, _f32p, C.c_size_t,
+                                C.c_size_t, _u8p, C.c_int]
+        L.orc_bench.restype = C.c_double
+
+    # --- producers -----------------------------------------------------
+    def genchirp(self, N, osr, NN, f0, down, ampl, phase, bw_scale):
+        out = np.zeros(2 * NN, np.float32)
+        ph = np.array([phase], np.float32)
+        self.lib.orc_genchirp(_p(out, _f32p), N, osr, NN, f0, int(down), ampl,
+                              _p(ph, _f32p), bw_scale)
+        return out.view(np.complex64), float(ph[0])
+
+    def modulate(self, syms, sf, osr=1, bw_hz=125000, ampl=1.0, sync=0x12):
+        syms = np.ascontiguousarray(syms, np.uint16)
+        n = len(syms)
+        out = np.zeros(2 * (n + 2) * (1 << sf) * osr, np.float32)
+        self.lib.orc_lora_modulate(_p(syms, _u16p), n, _p(out, _f32p), sf, osr,
+                                   bw_hz, ampl, sync)
+        return out.view(np.complex64)
+
+    def encode(self, payload):
+        payload = np.ascontiguousarray(np.frombuffer(bytes(payload), np.uint8))
+        out = np.zeros(2 * len(payload), np.uint16)
+        self.lib.orc_lora_encode(_p(payload, _u8p), len(payload), _p(out, _u16p))
+        return out
+
+    def dechirp(self, iq, sf, bw_hz=125000):
+        N = 1 << sf
+        down, _ = self.genchirp(N, 1, N, 0.0, True, 1.0, 0.0, bw_hz / 125000.0)
+        x = np.asarray(iq, np.complex64).reshape(-1, N)
+        # complex64 * complex64 in numpy = (ac-bd, ad+bc) in float32
+        return (x * down[None, :]).reshape(-1).astype(np.complex64)
+
+    # --- consumers -----------------------------------------------------
+    def fft(self, x):
+        x = _cf(np.asarray(x, np.complex64))
+        out = np.zeros_like(x)
+        self.lib.orc_fft(_p(x, _f32p), _p(out, _f32p), len(x) // 2)
+        return out.view(np.complex64)
+
+    def lora_demodulate(self, samples, sf, osr=1, hann=False, scratch=True):
+        x = _cf(samples)
+        count = len(x) // 2
+        total = count // ((1 << sf) * osr)
+        out = np.zeros(max(total, 1), np.uint16)
+        sync = np.zeros(1, np.uint8)
+        met = np.zeros(2, np.float32)
+        r = self.lib.orc_lora_demodulate(sf, int(hann), _p(x, _f32p), count,
+                                         _p(out, _u16p), osr, _p(sync, _u8p),
+                                         count if scratch else 0, _p(met, _f32p))
+        return r, out[: max(r, 0)], int(sync[0]), met
+
+    def demodulate(self, iq, sf, bw_hz=125000, osr=1, hann=False, cap=None, sync=0x12):
+        x = _cf(iq)
+        count = len(x) // 2
+        total = count // ((1 << sf) * osr)
+        cap = max(total - 2, 0) if cap is None else cap
+        syms = np.zeros(max(cap, 1), np.uint16)
+        met = np.zeros(2, np.float32)
+        so = np.zeros(1, np.uint8)
+        r = self.lib.orc_demodulate(sf, bw_hz, osr, int(hann), _p(x, _f32p), count,
+                                    _p(syms, _u16p), cap, _p(met, _f32p), sync,
+                                    _p(so, _u8p))
+        return r, syms[: max(r, 0)], int(so[0]), met
+
+    def decode(self, syms, cap=None):
+        syms = np.ascontiguousarray(syms, np.uint16)
+        cap = len(syms) // 2 if cap is None else cap
+        out = np.zeros(max(len(syms) // 2, 1), np.uint8)
+        crc = np.zeros(1, np.uint8)
+        r = self.lib.orc_decode(_p(syms, _u16p), len(syms), _p(out, _u8p), cap,
+                                _p(crc, _u8p))
+        return r, out[: max(r, 0)], int(crc[0])
+
+    def lora_decode(self, syms):
+        syms = np.ascontiguousarray(syms, np.uint16)
+        out = np.zeros(max(len(syms) // 2, 1), np.uint8)
+        r = self.lib.orc_lora_decode(_p(syms, _u16p), len(syms), _p(out, _u8p))
+        return r, out[: max(r, 0)]
+
+    def checksum(self, data):
+        d = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8))
+        return self.lib.orc_sx1272_checksum(_p(d, _u8p), len(d))
+
+    def bench(self, mode, sf, iq, frames, frame_samples, threads, bw_hz=125000):
+        x = _cf(iq)
+        ndata = frame_samples // (1 << sf) - 2
+        out = np.zeros(frames * (ndata // 2), np.uint8)
+        t = self.lib.orc_bench(mode, sf, bw_hz, _p(x, _f32p), frames, frame_samples,
+                               _p(out, _u8p), threads)
+        return t, out
+
+
+class Reference:
+    """The reference library (oracle/_ref), when it has been built."""
+
+    def __init__(self, path: Path = REF_SO):
+        if not path.exists():
+            raise FileNotFoundError(path)
+        L = self.lib = C.CDLL(str(path))
+        for n in ("ref_sizeof_workspace", "ref_sizeof_demod_workspace",
+                  "ref_sizeof_params", "ref_sizeof_metrics"):
+            getattr(L, n).restype = C.c_size_t
+        L.ref_fft.argtypes = [_f32p, _f32p, C.c_int]
+        L.ref_detect.argtypes = [_f32p, _f32p, C.c_int, _f32p, _f32p, _f32p]
+        L.ref_detect.restype = C.c_size_t
+        L.ref_genchirp.argtypes = [_f32p, C.c_int, C.c_int, C.c_int, C.c_float,
+                                   C.c_int, C.c_float, _f32p, C.c_float]
+        L.ref_lora_modulate.argtypes = [_u16p, C.c_size_t, _f32p, C.c_uint, C.c_uint,
+                                        C.c_uint, C.c_float, C.c_uint8]
+        L.ref_lora_modulate.restype = C.c_size_t
+        L.ref_lora_encode.argtypes = [_u8p, C.c_size_t, _u16p, C.c_uint]
+        L.ref_lora_encode.restype = C.c_size_t
+        L.ref_lora_decode.argtypes = [_u16p, C.c_size_t, _u8p]
+        L.ref_lora_decode.restype = C.c_ssize_t
+        L.ref_sx1272_checksum.argtypes = [_u8p, C.c_int]
+        L.ref_sx1272_checksum.restype = C.c_uint16
+        L.ref_decode_hamming84.argtypes = [C.c_uint8]
+        L.ref_decode_hamming84.restype = C.c_uint8
+        L.ref_lora_demodulate.argtypes = [C.c_uint, C.c_int, _f32p, C.c_size_t, _u16p,
+                                          C.c_uint, _u8p, C.c_int, _f32p]
+        L.ref_lora_demodulate.restype = C.c_ssize_t
+        L.ref_demodulate.argtypes = [C.c_uint, C.c_uint, C.c_uint, C.c_int, C.c_uint8,
+                                     _f32p, C.c_size_t, _u16p, C.c_size_t, _f32p, _u8p]
+        L.ref_demodulate.restype = C.c_ssize_t
+        L.ref_estimate_offsets.argtypes = [C.c_uint, C.c_uint, C.c_uint, C.c_int,
+                                           _f32p, C.c_size_t, _f32p]
+        L.ref_decode.argtypes = [C.c_uint, _u16p, C.c_size_t, _u8p, C.c_size_t, _u8p]
+        L.ref_decode.restype = C.c_ssize_t
+        for n in ("ref_bench_modeA", "ref_bench_modeB"):
+            getattr(L, n).argtypes = [C.c_uint, C.c_uint, _f32p, C.c_size_t,
+                                      C.c_size_t, _u8p, C.c_int]
+            getattr(L, n).restype = C.c_double
+
+    def fft(self, x):
+        x = _cf(np.asarray(x, np.complex64))
+        out = np.zeros_like(x)
+        self.lib.ref_fft(_p(x, _f32p), _p(out, _f32p), len(x) // 2)
+        return out.view(np.complex64)
+
+    def detect(self, x):
+        x = _cf(np.asarray(x, np.complex64))
+        out = np.zeros_like(x)
+        p, pa, fi = (np.zeros(1, np.float32) for _ in range(3))
+        idx = self.lib.ref_detect(_p(x, _f32p), _p(out, _f32p), len(x) // 2,
+                                  _p(p, _f32p), _p(pa, _f32p), _p(fi, _f32p))
+        return idx, float(p[0]), float(pa[0]), float(fi[0]), out.view(np.complex64)
+
+    def genchirp(self, N, osr, NN, f0, down, ampl, phase, bw_scale):
+        out = np.zeros(2 * NN, np.float32)
+        ph = np.array([phase], np.float32)
+        self.lib.ref_genchirp(_p(out, _f32p), N, osr, NN, f0, int(down), ampl,
+                              _p(ph, _f32p), bw_scale)
+        return out.view(np.complex64), float(ph[0])
+
+    def modulate(self, syms, sf, osr=1, bw_hz=125000, ampl=1.0, sync=0x12):
+        syms = np.ascontiguousarray(syms, np.uint16)
+        n = len(syms)
+        out = np.zeros(2 * (n + 2) * (1 << sf) * osr, np.float32)
+        self.lib.ref_lora_modulate(_p(syms, _u16p), n, _p(out, _f32p), sf, osr,
+                                   bw_hz, ampl, sync)
+        return out.view(np.complex64)
+
+    def encode(self, payload, sf=7):
+        payload = np.ascontiguousarray(np.frombuffer(bytes(payload), np.uint8))
+        out = np.zeros(2 * len(payload), np.uint16)
+        self.lib.ref_lora_encode(_p(payload, _u8p), len(payload), _p(out, _u16p), sf)
+        return out
+
+    def lora_demodulate(self, samples, sf, osr=1, hann=False, scratch=True):
+        x = _cf(samples)
+        count = len(x) // 2
+        total = count // ((1 << sf) * osr)
+        out = np.zeros(max(total, 1), np.uint16)
+        sync = np.zeros(1, np.uint8)
+        met = np.zeros(2, np.float32)
+        r = self.lib.ref_lora_demodulate(sf, int(hann), _p(x, _f32p), count,
+                                         _p(out, _u16p), osr, _p(sync, _u8p),
+                                         int(scratch), _p(met, _f32p))
+        return r, out[: max(r, 0)], int(sync[0]), met
+
+    def demodulate(self, iq, sf, bw_hz=125000, osr=1, hann=False, cap=None, sync=0x12):
+        x = _cf(iq)
+        count = len(x) // 2
+        total = count // ((1 << sf) * osr)
+        cap = max(total - 2, 0) if cap is None else cap
+        syms = np.zeros(max(cap, 1), np.uint16)
+        met = np.zeros(2, np.float32)
+        so = np.zeros(1, np.uint8)
+        r = self.lib.ref_demodulate(sf, bw_hz, osr, int(hann), sync, _p(x, _f32p),
+                                    count, _p(syms, _u16p), cap, _p(met, _f32p),
+                                    _p(so, _u8p))
+        return r, syms[: max(r, 0)], int(so[0]), met
+
+    def decode(self, syms, cap=None):
+        syms = np.ascontiguousarray(syms, np.uint16)
+        cap = len(syms) // 2 if cap is None else cap
+        out = np.zeros(max(len(syms) // 2, 1), np.uint8)
+        crc = np.zeros(1, np.uint8)
+        r = self.lib.ref_decode(7, _p(syms, _u16p), len(syms), _p(out, _u8p), cap,
+                                _p(crc, _u8p))
+        return r, out[: max(r, 0)], int(crc[0])
+
+    def bench(self, mode, sf, iq, frames, frame_samples, threads, bw_hz=125000):
+        x = _cf(iq)
+        ndata = frame_samples // (1 << sf) - 2
+        out = np.zeros(frames * (ndata // 2), np.uint8)
+        fn = self.lib.ref_bench_modeB if mode == 1 else self.lib.ref_bench_modeA
+        t = fn(sf, bw_hz, _p(x, _f32p), frames, frame_samples, _p(out, _u8p), threads)
+        return t, out
+
+
+def reference_available() -> bool:
+    return REF_SO.exists()
