@@ -1,0 +1,287 @@
+#!/usr/bin/env python3
+"""Throughput bench for the MI355X LoRa demodulation path (BASELINE.json).
+
+Workload (BASELINE.json configs[1], "C1"): SF7 BW125, 65,536 synthetic frames
+per GPU, each a 32-byte random payload -> lora_encode -> lora_modulate
+(66 symbols: 2 sync + 64 data, 8,448 complex float32 samples = 67.6 KB).
+The IQ is generated on the device (bit-exact lora_modulate kernel) and stays
+resident in HBM; the timed step is one pass of the hot path over the batch:
+
+    fused dechirp -> lora_demodulate (max-abs normalise, offset estimate,
+    per-symbol rotate + KISS-identical FFT + argmax) -> lora_decode + CRC
+
+(LPHY_MODE_DECHIRP_LORA_DEMODULATE + LPHY_F_DECODE through the C ABI), plus,
+for N > 1 ranks, an all_gather of the decoded payloads (RCCL over xGMI).
+`value` = data symbols demodulated by all ranks / max-over-ranks time.
+
+Also reported: the high-level lora_phy::demodulate path (mode A), the
+dominant kernel's roofline fraction (HIP events on the launch stream), and
+the reference CPU path timed on this host's cores (rank 0, N = 1).
+
+Run: python bench.py [--gpus N --steps K --warmup W --sf 7 --frames F]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent
+PKG = ROOT / "lora-sdr-lightweight-standalone-library-clean_amd"
+sys.path.insert(0, str(PKG))
+sys.path.insert(0, str(ROOT / "tests"))
+
+import lphy  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+PAYLOAD = 32                  # bytes per frame (performance_test.cpp:67)
+DATA_SYMS = 2 * PAYLOAD       # 64 data symbols
+TOTAL_SYMS = DATA_SYMS + 2    # + 2 sync symbols
+DEFAULT_FRAMES = {7: 65536, 8: 32768, 9: 16384, 10: 8192, 11: 4096, 12: 4096}
+
+
+def bytes_per_data_symbol(N: int) -> float:
+    """IQ read (sync share included) + u16 symbol + 1/2 byte."""
+    return 8.0 * N * TOTAL_SYMS / DATA_SYMS + 2.0 + 0.5
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--sf", type=int, default=7)
+    ap.add_argument("--bw", type=int, default=125000)
+    ap.add_argument("--frames", type=int, default=0, help="frames per GPU (0 = config default)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-mode-a", action="store_true")
+    ap.add_argument("--sweep", action="store_true", help="also time SF8..SF12 (extra field)")
+    return ap.parse_args()
+
+
+class Workload:
+    """One SF configuration resident on this rank's GPU."""
+
+    def __init__(self, sf: int, bw: int, frames: int, rank: int, dev: torch.device):
+        self.sf, self.N, self.bw, self.frames = sf, 1 << sf, bw, frames
+        self.fs = TOTAL_SYMS * self.N
+        self.dem = lphy.Demodulator(sf, bw, 1, lphy.WINDOW_NONE, device=dev.index)
+        rng = np.random.default_rng(0x5EED + 7919 * rank + sf)
+        self.payloads = rng.integers(0, 256, (frames, PAYLOAD), dtype=np.uint8)
+        syms = lphy.encode_payloads(self.payloads)
+        stream = torch.cuda.current_stream().cuda_stream
+        t_in = torch.from_numpy(syms.view(np.int16).reshape(-1).copy()).to(dev)
+        self.iq = torch.empty(frames * self.fs * 2, dtype=torch.float32, device=dev)
+        self.dem.modulate_batch(t_in, frames, DATA_SYMS, self.iq, 1.0, 0x12, stream)
+        del t_in
+        self.syms = torch.zeros(frames * DATA_SYMS, dtype=torch.int16, device=dev)
+        self.pay = torch.zeros(frames * PAYLOAD, dtype=torch.uint8, device=dev)
+        self.meta = torch.zeros(frames * 32, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+
+    def run(self, mode: int, flags: int = lphy.F_DECODE):
+        self.dem.demod_batch(self.iq, self.frames, self.fs, self.syms, self.meta, mode,
+                             flags, payload=self.pay,
+                             stream=torch.cuda.current_stream().cuda_stream)
+
+    def stage_times(self, mode: int, reps: int = 3):
+        """Average device time per launch of each stage (HIP events recorded
+        on the stream the kernels are launched on)."""
+        names = [("prologue", lphy.F_STAGE_PROLOGUE), ("symbols", lphy.F_STAGE_SYMBOLS),
+                 ("final", lphy.F_STAGE_FINAL)]
+        acc = {n: 0.0 for n, _ in names}
+        for _ in range(reps):
+            for n, fl in names:
+                a = torch.cuda.Event(enable_timing=True)
+                b = torch.cuda.Event(enable_timing=True)
+                a.record()
+                self.run(mode, lphy.F_DECODE | fl)
+                b.record()
+                torch.cuda.synchronize()
+                acc[n] += a.elapsed_time(b)
+        return {n: v / reps for n, v in acc.items()}
+
+    def check(self, mode: int) -> dict:
+        """Size-independent property over the whole batch (every payload
+        recovered, CRC field consistent) + bit-exact oracle comparison on a
+        sample of frames."""
+        torch.cuda.synchronize()
+        pay = self.pay.cpu().numpy().reshape(self.frames, PAYLOAD)
+        res = {"payloads_recovered": int((pay == self.payloads).all(axis=1).sum()),
+               "frames": self.frames}
+        try:
+            from checkers import Oracle
+            o = Oracle()
+            syms = self.syms.cpu().numpy().view(np.uint16).reshape(self.frames, DATA_SYMS)
+            idx = np.unique(np.linspace(0, self.frames - 1, 8).astype(int))
+            ok = 0
+            for f in idx:
+                x = self.iq[f * self.fs * 2:(f + 1) * self.fs * 2].cpu().numpy().view(np.complex64)
+                if mode == lphy.MODE_DEMODULATE:
+                    r, osyms, _, _ = o.demodulate(x, self.sf, bw_hz=self.bw)
+                else:
+                    r, osyms, _, _ = o.lora_demodulate(o.dechirp(x, self.sf, self.bw), self.sf)
+                ok += int(np.array_equal(osyms, syms[f]))
+            res["oracle_frames_bit_exact"] = f"{ok}/{len(idx)}"
+        except Exception as e:  # checker unavailable: say so, never fall back
+            res["oracle_frames_bit_exact"] = f"unavailable: {e}"
+        return res
+
+
+def timed(wl: Workload, mode: int, steps: int, warmup: int, world: int, gathered=None):
+    def step():
+        wl.run(mode)
+        if world > 1:
+            torch.distributed.all_gather_into_tensor(gathered, wl.pay)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=wl.iq.device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+def cpu_baseline(wl: Workload, seconds: float) -> dict:
+    """Reference CPU path (mode B: dechirp + lora_demodulate + lora_decode)
+    on this host, one workspace per thread, on a bounded sample."""
+    import checkers
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    if checkers.reference_available():
+        ck, kind = checkers.Reference(), "reference"
+    else:
+        ck, kind = checkers.Oracle(), "port"
+    nf = min(wl.frames, 2048)
+    x = wl.iq[: nf * wl.fs * 2].cpu().numpy().view(np.complex64)
+    done, el = 0, 0.0
+    while el < seconds:
+        t, out = ck.bench(1, wl.sf, x, nf, wl.fs, threads, wl.bw)
+        el += t
+        done += nf
+    ok = bool((out.reshape(nf, PAYLOAD) == wl.payloads[:nf]).all())
+    return {"value": done * DATA_SYMS / el, "unit": "data symbols/s", "cores": threads,
+            "kind": kind,
+            "sample": f"{done} SF{wl.sf} BW{wl.bw // 1000} frames ({nf}-frame batches, "
+                      f"{el:.1f} s), dechirp+lora_demodulate+lora_decode, payloads ok={ok}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=dev)
+    baseline = json.loads((ROOT / "BASELINE.json").read_text())
+
+    frames = args.frames or DEFAULT_FRAMES.get(args.sf, 4096)
+    wl = Workload(args.sf, args.bw, frames, rank, dev)
+    gathered = (torch.empty(world * frames * PAYLOAD, dtype=torch.uint8, device=dev)
+                if world > 1 else None)
+
+    mode_b = lphy.MODE_DECHIRP_LORA_DEMODULATE
+    dt = timed(wl, mode_b, args.steps, args.warmup, world, gathered)
+    ms = dt / args.steps * 1e3
+    data_syms = world * frames * DATA_SYMS
+    value = data_syms * args.steps / dt
+    check_b = wl.check(mode_b)
+    st = wl.stage_times(mode_b)
+
+    N = wl.N
+    # dominant kernel = per-symbol demod: reads every IQ sample once, writes
+    # one u16 per data symbol (sync bins go to the 32-B frame record)
+    sym_bytes = frames * (wl.fs * 8 + DATA_SYMS * 2)
+    achieved = sym_bytes / (st["symbols"] * 1e-3) / 1e9
+    step_gbps = frames * DATA_SYMS * bytes_per_data_symbol(N) / (ms * 1e-3) / 1e9
+
+    extra = {}
+    if not args.no_mode_a:
+        dta = timed(wl, lphy.MODE_DEMODULATE, max(3, args.steps // 2), 1, world, gathered)
+        extra["demodulate_mode_A"] = {
+            "value": data_syms * max(3, args.steps // 2) / dta, "unit": "data symbols/s",
+            "check": wl.check(lphy.MODE_DEMODULATE)}
+        wl.run(mode_b)  # leave mode-B results in place
+    if args.sweep:
+        sweep = {}
+        for sf in range(8, 13):
+            w2 = Workload(sf, args.bw, DEFAULT_FRAMES[sf] // 4, rank, dev)
+            d2 = timed(w2, mode_b, 3, 1, 1)
+            s2 = w2.stage_times(mode_b, 1)
+            sweep[f"SF{sf}"] = {"value": w2.frames * DATA_SYMS * 3 / d2,
+                                "frames": w2.frames,
+                                "symbols_kernel_frac_hbm": w2.frames * (w2.fs * 8 + DATA_SYMS * 2)
+                                / (s2["symbols"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                                "check": w2.check(mode_b)["payloads_recovered"]}
+            del w2
+            torch.cuda.empty_cache()
+        extra["sweep"] = sweep
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(wl, args.cpu_seconds)
+        except Exception as e:
+            cpu = {"value": None, "unit": "data symbols/s", "cores": 0, "kind": "port",
+                   "sample": f"failed: {e}"}
+
+    if rank == 0:
+        line = {
+            "metric": baseline["metric"],
+            "value": value,
+            "unit": "data symbols/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (device-generated lora_modulate IQ of random payloads)",
+            "config": {
+                "workload": f"SF{args.sf} BW{args.bw // 1000} CR4/5, {frames} frames/GPU x "
+                            f"{PAYLOAD} B payload ({TOTAL_SYMS} symbols), fused dechirp -> "
+                            "lora_demodulate -> lora_decode+CRC" +
+                            (", all_gather of payloads" if world > 1 else ""),
+                "sf": args.sf, "bw_hz": args.bw, "frames_per_gpu": frames,
+                "symbols_per_frame": TOTAL_SYMS, "parallelism": f"frames sharded x{world}",
+            },
+            "hbm_gbps_step": step_gbps,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                         "kernel": f"k_demod<{args.sf}>",
+                         "bytes_per_launch": sym_bytes,
+                         "avg_launch_ms": st["symbols"]},
+            "stage_ms": st,
+            "check": check_b,
+            "cpu_baseline": cpu,
+        }
+        line.update(extra)
+        print(json.dumps(line))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,163 @@
+/*
+ * lphy_hip.h — C ABI of the MI355X (gfx950) LoRa PHY demodulation layer.
+ *
+ * This is the drop-in boundary below the lora_phy:: C++ API
+ * (include/lora_phy/phy.hpp, implemented by liblora_phy_amd.so on top of
+ * these entry points).  Plain pointers and sizes only; device pointers are
+ * hipMalloc'd (or torch) memory, `stream` is a hipStream_t (NULL = default).
+ * Every function returns 0 or a negative errno, like the reference.
+ *
+ * Reference interfaces replaced (file:line under the reference tree):
+ *   lphy_hip_ctx_create    lora_phy::init            src/phy/phy.cpp:27-52
+ *                          lora_phy::lora_demod_init src/phy/LoRaDemod.cpp:11-33
+ *   lphy_hip_ctx_destroy   lora_phy::lora_demod_free src/phy/LoRaDemod.cpp:35-48
+ *   lphy_hip_demod_batch   mode LPHY_MODE_DEMODULATE:
+ *                            lora_phy::demodulate        src/phy/phy.cpp:182-243
+ *                            (+ estimate_offsets          src/phy/phy.cpp:81-148)
+ *                          mode LPHY_MODE_LORA_DEMODULATE:
+ *                            lora_phy::lora_demodulate   src/phy/LoRaDemod.cpp:50-197
+ *                          mode LPHY_MODE_DECHIRP_LORA_DEMODULATE:
+ *                            test-side dechirp (tests/e2e_chain_test.cpp:80-93)
+ *                            fused in front of lora_demodulate
+ *                          flag LPHY_F_DECODE adds, per frame:
+ *                            lora_phy::decode / lora_decode src/phy/phy.cpp:245-261,
+ *                            src/phy/LoRaDecoder.cpp:7-21
+ *   lphy_hip_decode_batch  lora_phy::decode / lora_decode on device symbols
+ *   lphy_hip_estimate_batch lora_phy::estimate_offsets src/phy/phy.cpp:81-148
+ *   lphy_hip_modulate_batch lora_phy::lora_modulate  src/phy/LoRaMod.cpp:8-43
+ *                            (producer; bit-exact, used for synthetic IQ)
+ *   lphy_hip_compensate    lora_phy::compensate_offsets src/phy/phy.cpp:150-180
+ *
+ * Batch layout in HBM:
+ *   IQ      interleaved float32 (I,Q) = std::complex<float>, frame f at
+ *           d_iq + 2*f*frame_samples floats.
+ *   symbols uint16, frame f at d_syms + f*lphy_hip_syms_per_frame(...)
+ *           (data symbols only when the frame has >= 2 symbols — the two
+ *           sync symbols go to lphy_frame_meta.sw0/sw1, as the reference
+ *           routes them to ws->sync_word / *out_sync).
+ *   bytes   uint8, frame f at d_bytes + f*(data_symbols/2) (LPHY_F_DECODE).
+ *   meta    one lphy_frame_meta per frame (also the kernels' hand-off
+ *           between the per-frame prologue and the per-symbol demodulator).
+ */
+#ifndef LPHY_HIP_H
+#define LPHY_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct lphy_hip_ctx lphy_hip_ctx;
+
+/* Per-frame results (32 bytes). */
+typedef struct lphy_frame_meta {
+    float cfo;          /* ws->metrics.cfo after the call                    */
+    float time_offset;  /* ws->metrics.time_offset                           */
+    float rate;         /* -2*pi*cfo/N: per-sample CFO rotation              */
+    float scale;        /* 1/max(|I|,|Q|) when normalised (modes 1,2), else 1 */
+    int32_t t_off;      /* (int)round(time_offset)                           */
+    int32_t status;     /* 0 | -ERANGE (needs scratch) | -EINVAL (odd count) */
+    uint16_t sw0, sw1;  /* argmax bins of the two sync symbols               */
+    uint8_t sync_word;  /* ((sw0>>(sf-4))&15)<<4 | ((sw1>>(sf-4))&15)        */
+    uint8_t crc_ok;     /* lora_phy::decode's metrics.crc_ok (LPHY_F_DECODE) */
+    uint8_t normalised; /* 1 when max(|I|,|Q|) > 1 forced the rescale        */
+    uint8_t have_sync;  /* frame had >= 2 symbols                            */
+} lphy_frame_meta;
+
+enum lphy_mode {
+    LPHY_MODE_DEMODULATE = 0,              /* lora_phy::demodulate (raw IQ)  */
+    LPHY_MODE_LORA_DEMODULATE = 1,         /* lora_demodulate (dechirped IQ) */
+    LPHY_MODE_DECHIRP_LORA_DEMODULATE = 2  /* raw IQ, dechirp fused, then 1  */
+};
+
+enum lphy_flags {
+    LPHY_F_DECODE = 1u,      /* also Hamming-decode + CRC each frame        */
+    LPHY_F_NO_SCRATCH = 2u,  /* modes 1/2: behave as lora_demodulate with no
+                                scratch buffer (-ERANGE when rescale needed) */
+    /* Stage selection (profiling / overlap): when any of these bits is set
+     * only the selected stages are launched; none set = all three. */
+    LPHY_F_STAGE_PROLOGUE = 4u,  /* per-frame max-abs + offset estimate   */
+    LPHY_F_STAGE_SYMBOLS = 8u,   /* per-symbol rotate + FFT + argmax      */
+    LPHY_F_STAGE_FINAL = 16u     /* per-frame sync word, decode, CRC      */
+};
+
+enum lphy_window { LPHY_WINDOW_NONE = 0, LPHY_WINDOW_HANN = 1 };
+
+/* Create a context for one (sf, bandwidth, osr, window) configuration on
+ * HIP device `device`.  Precomputes the KISS twiddles, the down-chirp and
+ * the window on the host with the same libm calls as the reference, and
+ * uploads them.  sf in [1,12]; bw_hz in {125000,250000,500000}.
+ * Returns 0, -EINVAL (bad arguments) or -ENODEV / -ENOMEM. */
+int lphy_hip_ctx_create(lphy_hip_ctx** out, int device, unsigned sf,
+                        unsigned bw_hz, unsigned osr, int window);
+void lphy_hip_ctx_destroy(lphy_hip_ctx* ctx);
+
+/* Symbols written per frame for a frame of `frame_samples` samples. */
+size_t lphy_hip_syms_per_frame(const lphy_hip_ctx* ctx, size_t frame_samples,
+                               int mode);
+
+/* Demodulate `frames` frames of device-resident IQ (asynchronous on
+ * `stream`).  d_bytes may be NULL unless LPHY_F_DECODE.  d_meta is
+ * required.  Returns 0 or -EINVAL/-ERANGE for shape errors (the per-frame
+ * conditions the reference reports through its return value are in
+ * lphy_frame_meta.status). */
+int lphy_hip_demod_batch(lphy_hip_ctx* ctx, const float* d_iq, size_t frames,
+                         size_t frame_samples, uint16_t* d_syms,
+                         uint8_t* d_bytes, lphy_frame_meta* d_meta, int mode,
+                         unsigned flags, void* stream);
+
+/* Hamming(8,4)sx decode + sx1272 CRC of device symbols: frame f holds
+ * syms_per_frame symbols at d_syms + f*syms_per_frame and yields
+ * syms_per_frame/2 bytes; meta[f].crc_ok / .status updated.  An odd
+ * syms_per_frame gives -EINVAL (LoRaDecoder.cpp:10). */
+int lphy_hip_decode_batch(lphy_hip_ctx* ctx, const uint16_t* d_syms,
+                          size_t frames, size_t syms_per_frame,
+                          uint8_t* d_bytes, lphy_frame_meta* d_meta,
+                          void* stream);
+
+/* estimate_offsets (phy.cpp:81-148) over the first `est_samples` samples of
+ * each frame: writes meta[f].cfo / .time_offset / .t_off / .rate. */
+int lphy_hip_estimate_batch(lphy_hip_ctx* ctx, const float* d_iq,
+                            size_t frames, size_t frame_samples,
+                            size_t est_samples, lphy_frame_meta* d_meta,
+                            void* stream);
+
+/* compensate_offsets (phy.cpp:150-180), in place on one device buffer. */
+int lphy_hip_compensate(lphy_hip_ctx* ctx, float* d_iq, size_t count,
+                        float cfo, float time_offset, void* stream);
+
+/* lora_modulate (LoRaMod.cpp:8-43) for `frames` frames of `nsyms` symbols
+ * each (d_syms + f*nsyms) into d_iq + 2*f*(nsyms+2)*N*osr floats; bit-exact
+ * with the reference.  Producer for synthetic input, not on the timed path. */
+int lphy_hip_modulate_batch(lphy_hip_ctx* ctx, const uint16_t* d_syms,
+                            size_t frames, size_t nsyms, float* d_iq,
+                            float amplitude, uint8_t sync, void* stream);
+
+/* Host-buffer convenience used by the C++ shim: uploads, runs
+ * lphy_hip_demod_batch, downloads; synchronous. */
+int lphy_hip_demod_host(lphy_hip_ctx* ctx, const float* h_iq, size_t frames,
+                        size_t frame_samples, uint16_t* h_syms,
+                        uint8_t* h_bytes, lphy_frame_meta* h_meta, int mode,
+                        unsigned flags);
+int lphy_hip_decode_host(lphy_hip_ctx* ctx, const uint16_t* h_syms,
+                         size_t count, uint8_t* h_bytes, lphy_frame_meta* h_meta);
+int lphy_hip_estimate_host(lphy_hip_ctx* ctx, const float* h_iq,
+                           size_t count, lphy_frame_meta* h_meta);
+int lphy_hip_compensate_host(lphy_hip_ctx* ctx, float* h_iq, size_t count,
+                             float cfo, float time_offset);
+int lphy_hip_modulate_host(lphy_hip_ctx* ctx, const uint16_t* h_syms,
+                           size_t nsyms, float* h_iq, float amplitude,
+                           uint8_t sync);
+
+/* Wait for all work queued on `stream`. */
+int lphy_hip_sync(void* stream);
+
+/* Version / build string (for tests that check the library loaded). */
+const char* lphy_hip_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LPHY_HIP_H */

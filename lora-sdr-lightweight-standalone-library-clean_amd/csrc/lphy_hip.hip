@@ -1,0 +1,978 @@
+// lphy_hip.hip — MI355X (gfx950) LoRa PHY demodulation kernels + C ABI.
+//
+// Hot path: per frame a prologue (whole-frame max|I|,|Q| for
+// lora_demodulate's normalisation, LoRaDemod.cpp:60-78, and the two-symbol
+// CFO/timing estimate, LoRaDemod.cpp:80-136 / phy.cpp:81-148), then per
+// symbol CFO rotation -> KISS-identical FFT -> |X|^2 argmax
+// (LoRaDemod.cpp:142-176 / phy.cpp:204-238), then per frame Hamming(8,4)
+// decode + sx1272 CRC (LoRaDecoder.cpp:7-21, phy.cpp:245-261).
+//
+// Kernels:
+//   k_prologue   one 256-thread workgroup per frame: max-abs reduction,
+//                estimate FFTs (tile machinery of lphy_fft.h), offsets.
+//   k_demod<SF>  256-thread tiles of T = 256/(N/16) symbols; each symbol is
+//                staged to LDS with coalesced float2 loads while the rotation
+//                (glibc-exact sincosf in FP64) is applied, transformed by
+//                LPS = N/16 lanes holding 16 complex each, and reduced by
+//                cross-lane argmax.  No MFMA: the path is HBM/VALU bound.
+//   k_finalize   one thread per frame: sync word, decode, CRC.
+//   k_modulate*  bit-exact lora_modulate (producer for synthetic IQ).
+//
+// All device arithmetic is built with -ffp-contract=off (see
+// __graft_entry__.build); every product/sum is evaluated in the reference's
+// operand order so that symbol indices, sync words and decoded bytes are
+// bit-identical to the reference's CPU path.
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/lphy_hip.h"
+#include "libm_exact.h"
+#include "lphy_fft.h"
+
+using namespace lphy;
+
+namespace {
+
+constexpr float kPi = 3.14159265358979323846f;  // lora_phy::PI (phy.hpp:20)
+
+// ---------------------------------------------------------------------------
+// Per-launch parameters
+// ---------------------------------------------------------------------------
+struct DemodArgs {
+    const float2* iq;        // frames * frame_samples
+    const float2* tw;        // N twiddles (KISS, forward)
+    const float2* down;      // N down-chirp samples (genChirp, down=true)
+    const float* win;        // N window coefficients or nullptr
+    uint16_t* syms;          // output symbols
+    lphy_frame_meta* meta;   // per-frame meta (prologue -> demod hand-off)
+    unsigned long long frames;
+    unsigned long long frame_samples;
+    unsigned long long total_syms;  // symbols per frame = frame_samples / step
+    unsigned long long out_per_frame;
+    int osr;
+    int mode;
+    int no_scratch;
+    int est_units;           // estimate units per frame (est_syms * osr)
+};
+
+// (int)std::round(x) as the x86-64 reference evaluates it: cvttss2si on the
+// rounded value, INT_MIN for NaN / out of range.
+__device__ __forceinline__ int round_to_int(float x) {
+    const float r = roundf(x);
+    if (!(r >= -2147483648.0f && r < 2147483648.0f)) return (int)0x80000000u;
+    return (int)r;
+}
+
+// Symbol base offset after the timing shift (LoRaDemod.cpp:144-151).
+__device__ __forceinline__ unsigned long long shifted_base(unsigned long long s,
+                                                           unsigned long long step, int t_off,
+                                                           unsigned long long count) {
+    unsigned long long base = s * step;
+    if (t_off > 0) {
+        if (base + (unsigned long long)t_off + step <= count) base += (unsigned long long)t_off;
+    } else if (t_off < 0) {
+        unsigned long long off = (t_off == (int)0x80000000u)
+                                     ? (unsigned long long)(long long)t_off
+                                     : (unsigned long long)(-(long long)t_off);
+        if (off <= base) base -= off;
+    }
+    return base;
+}
+
+// Input sample for the estimate (no rotation): raw (mode 0) or
+// [dechirped,] [normalised] (modes 1, 2).  idx is the absolute sample index
+// in the frame, i the index inside the symbol (window / mode-0 chirp).
+__device__ __forceinline__ float2 est_sample(const DemodArgs& A, const float2* fr,
+                                             unsigned long long idx, int i, int N,
+                                             const lphy_frame_meta& m) {
+    float2 x = fr[idx];
+    if (A.mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+        x = idx < A.total_syms * (unsigned long long)N ? cmul(x, A.down[idx & (N - 1)])
+                                                       : make_float2(0.0f, 0.0f);
+    if (A.mode != LPHY_MODE_DEMODULATE && m.normalised) x = cscale(x, m.scale);
+    if (A.win) x = cscale(x, A.win[i]);
+    return x;
+}
+
+// ---------------------------------------------------------------------------
+// Prologue: one workgroup per frame
+// ---------------------------------------------------------------------------
+struct UnitResult {
+    int idx;
+    int valid;   // p > best_p reachable (maxValue > 0)
+    float findex;
+    float phase;
+};
+
+template <int SF>
+__global__ __launch_bounds__(kTile) void k_prologue(DemodArgs A) {
+    using G = Geo<SF>;
+    constexpr int N = G::N;
+    __shared__ float2 lds[G::T * G::SSTRIDE];
+    __shared__ ArgMax red[kTile / 64];
+    __shared__ float wmax[kTile / 64];
+    __shared__ UnitResult units[G::T];
+    __shared__ float fold[4];   // sum_index, phase_diff, prev_phase, have_prev
+    __shared__ unsigned fold_t;
+    __shared__ lphy_frame_meta sm;
+
+    const unsigned long long f = blockIdx.x;
+    const int tid = threadIdx.x;
+    const float2* fr = A.iq + f * A.frame_samples;
+    const unsigned long long count = A.frame_samples;
+    const unsigned long long step = (unsigned long long)N * A.osr;
+
+    // --- whole-frame max(|I|,|Q|) (lora_demodulate only) -------------------
+    float mx = 0.0f;
+    if (A.mode != LPHY_MODE_DEMODULATE) {
+        const unsigned long long dech_end = A.total_syms * N;  // dechirped span
+        for (unsigned long long i = tid; i < count; i += kTile) {
+            float2 x = fr[i];
+            if (A.mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+                x = i < dech_end ? cmul(x, A.down[i & (N - 1)]) : make_float2(0.0f, 0.0f);
+            const float r = fabsf(x.x), im = fabsf(x.y);
+            const float m = (r < im) ? im : r;  // std::max(r, im)
+            if (m > mx) mx = m;
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const float o = __shfl_xor(mx, off, 64);
+            mx = o > mx ? o : mx;
+        }
+        if ((tid & 63) == 0) wmax[tid >> 6] = mx;
+        __syncthreads();
+        mx = wmax[0];
+#pragma unroll
+        for (int w = 1; w < kTile / 64; ++w) mx = wmax[w] > mx ? wmax[w] : mx;
+    }
+    if (tid == 0) {
+        lphy_frame_meta m{};
+        m.scale = 1.0f;
+        m.have_sync = A.total_syms >= 2;
+        if (A.mode != LPHY_MODE_DEMODULATE && mx > 1.0f) {
+            if (A.no_scratch) m.status = -ERANGE;
+            m.normalised = 1;
+            m.scale = 1.0f / mx;
+        }
+        sm = m;
+    }
+    __syncthreads();
+    if (sm.status != 0) {
+        if (tid == 0) A.meta[f] = sm;
+        return;  // whole workgroup leaves together (uniform condition)
+    }
+    const lphy_frame_meta m0 = sm;
+
+    // --- estimate: FFT + detect per (symbol, osr phase) unit, folded in
+    // symbol order exactly like the reference loop (LoRaDemod.cpp:80-140,
+    // phy.cpp:95-147) -------------------------------------------------------
+    if (tid == 0) {
+        fold[0] = 0.0f; fold[1] = 0.0f; fold[2] = 0.0f; fold[3] = 0.0f;
+        fold_t = 0;
+    }
+    const int sym_slot = tid / G::LPS;   // symbol slot within the tile
+    const int lam = tid % G::LPS;        // lane within the symbol
+    for (int u0 = 0; u0 < A.est_units; u0 += G::T) {
+        const int u = u0 + sym_slot;
+        const bool live = u < A.est_units;
+        const int s = live ? u / A.osr : 0, t = live ? u % A.osr : 0;
+        float2* sym = lds + sym_slot * G::SSTRIDE;
+        // stage natural-order samples sym[t + i*osr] (LoRaDemod.cpp:86-92)
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) {
+            const int i = lam + e * G::LPS;
+            float2 x = make_float2(0.0f, 0.0f);
+            if (live) x = est_sample(A, fr, (unsigned long long)s * step + t + (unsigned long long)i * A.osr, i, N, m0);
+            sym[G::lds(i)] = x;
+        }
+        __syncthreads();
+        float2 v[16];
+        int pos[16];
+        fft_tile<SF>(v, pos, sym, lam, A.tw);
+        // keep the bins for the interpolation and the phase
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) sym[G::lds(pos[e])] = v[e];
+        ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, pos), red);
+        __syncthreads();
+        if (live && lam == 0) {
+            // LoRaDetector.hpp:60-71
+            const int idx = best.i;
+            const float mv = best.v > 0.0f ? best.v : 0.0f;
+            const float fund = sqrtf(mv);
+            const float2 lb = sym[G::lds(idx > 0 ? idx - 1 : N - 1)];
+            const float2 rb = sym[G::lds(idx < N - 1 ? idx + 1 : 0)];
+            const float left = lphy_libm::cabsf_exact(lb.x, lb.y);
+            const float right = lphy_libm::cabsf_exact(rb.x, rb.y);
+            const double demon = (2.0 * (double)fund) - (double)right - (double)left;
+            const float fi = demon == 0.0 ? 0.0f : (float)(0.5 * (double)(right - left) / demon);
+            const float2 bin = sym[G::lds(idx)];
+            UnitResult r;
+            r.idx = idx;
+            r.valid = mv > 0.0f;  // osr == 1: p > -1e30 <=> maxValue > 0
+            r.findex = fi;
+            r.phase = lphy_libm::atan2f_exact(bin.y, bin.x);
+            units[sym_slot] = r;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const int nu = (A.est_units - u0) < G::T ? (A.est_units - u0) : G::T;
+            float sum_index = fold[0], phase_diff = fold[1], prev_phase = fold[2];
+            bool have_prev = fold[3] != 0.0f;
+            unsigned sum_t = fold_t;
+            for (int s0 = 0; s0 < nu; s0 += A.osr) {
+                int best_idx = 0, best_t = 0;
+                float best_f = 0.0f, best_phase = 0.0f;  // atan2(0, 0) of an unset bin
+                for (int t2 = 0; t2 < A.osr; ++t2) {
+                    const UnitResult& r = units[s0 + t2];
+                    if (r.valid) {
+                        best_idx = r.idx; best_f = r.findex; best_t = t2; best_phase = r.phase;
+                        break;
+                    }
+                }
+                sum_t += (unsigned)best_t;
+                sum_index += (float)best_idx + best_f;
+                if (have_prev) {
+                    float d = best_phase - prev_phase;
+                    while (d > kPi) d -= 2.0f * kPi;
+                    while (d < -kPi) d += 2.0f * kPi;
+                    phase_diff += d;
+                }
+                prev_phase = best_phase;
+                have_prev = true;
+            }
+            fold[0] = sum_index; fold[1] = phase_diff; fold[2] = prev_phase;
+            fold[3] = have_prev ? 1.0f : 0.0f;
+            fold_t = sum_t;
+        }
+        __syncthreads();
+    }
+
+    if (tid == 0) {
+        const int est_syms = A.est_units / A.osr;
+        const float sum_index = fold[0], phase_diff = fold[1];
+        const unsigned sum_t = fold_t;
+        lphy_frame_meta m = m0;
+        const float avg_index = sum_index / (float)est_syms;
+        const float cfo_coarse = avg_index / (float)N;
+        float cfo_fine = 0.0f;
+        if (est_syms > 1)
+            cfo_fine = (phase_diff / (float)(est_syms - 1)) / (2.0f * kPi * (float)N);
+        m.cfo = cfo_coarse + cfo_fine;
+        const float frac = avg_index - floorf(avg_index + 0.5f);
+        const float avg_t = (float)sum_t / (float)est_syms;
+        m.time_offset = avg_t - frac * (float)N * (float)A.osr;
+        m.t_off = round_to_int(m.time_offset);
+        m.rate = -2.0f * kPi * m.cfo / (float)N;
+        A.meta[f] = m;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Demodulation: 256-thread tiles of T symbols
+// ---------------------------------------------------------------------------
+template <int SF>
+__global__ __launch_bounds__(kTile) void k_demod(DemodArgs A) {
+    using G = Geo<SF>;
+    constexpr int N = G::N;
+    __shared__ float2 lds[G::T * G::SSTRIDE];
+    __shared__ ArgMax red[kTile / 64];
+
+    const int tid = threadIdx.x;
+    const int slot = tid / G::LPS, lam = tid % G::LPS;
+    const unsigned long long gsym = (unsigned long long)blockIdx.x * G::T + slot;
+    const bool live = gsym < A.frames * A.total_syms;
+    const unsigned long long f = live ? gsym / A.total_syms : 0;
+    const unsigned long long s = live ? gsym % A.total_syms : 0;
+    const lphy_frame_meta m = A.meta[f];
+    const bool ok = live && m.status == 0;
+    const unsigned long long step = (unsigned long long)N * A.osr;
+    const float2* fr = A.iq + f * A.frame_samples;
+    const unsigned long long base = shifted_base(s, step, m.t_off, A.frame_samples);
+    const float2* src = fr + base;
+    const unsigned long long dech_end = A.total_syms * N;  // whole symbols only
+    const float start = m.rate * ((float)(s * N) + (float)m.t_off / (float)A.osr);
+    float2* sym = lds + slot * G::SSTRIDE;
+
+    // stage: rotated samples in natural order (LoRaDemod.cpp:152-163,
+    // phy.cpp:217-229)
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) {
+        const int i = lam + e * G::LPS;
+        float2 x = make_float2(0.0f, 0.0f);
+        if (ok) {
+            x = src[(unsigned long long)i * A.osr];
+            if (A.mode == LPHY_MODE_DEMODULATE) {
+                x = cmul(x, A.down[i]);  // phy.cpp:219-220: down-chirp of the window
+            } else {
+                if (A.mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE) {
+                    // the external dechirp ran on the unshifted buffer
+                    // (e2e_chain_test.cpp:88-93): chirp index of the absolute sample
+                    const unsigned long long j = base + (unsigned long long)i;
+                    x = j < dech_end ? cmul(x, A.down[j & (N - 1)]) : make_float2(0.0f, 0.0f);
+                }
+                if (m.normalised) x = cscale(x, m.scale);
+            }
+            const float ph = start + m.rate * (float)i;
+            float sn, cs;
+            lphy_libm::sincosf_exact(ph, &sn, &cs);
+            x = cmul(x, make_float2(cs, sn));
+            if (A.win) x = cscale(x, A.win[i]);
+        }
+        sym[G::lds(i)] = x;
+    }
+    __syncthreads();
+    float2 v[16];
+    int pos[16];
+    fft_tile<SF>(v, pos, sym, lam, A.tw);
+    const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, pos), red);
+    if (ok && lam == 0) {
+        const uint16_t idx = (uint16_t)best.i;
+        if (m.have_sync && s < 2) {
+            if (s == 0) A.meta[f].sw0 = idx;
+            else A.meta[f].sw1 = idx;
+        } else {
+            const unsigned long long o = m.have_sync ? s - 2 : s;
+            A.syms[f * A.out_per_frame + o] = idx;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Per-frame finalisation: sync word, decode, CRC
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint8_t hamming84_decode(uint8_t b) {
+    // LoRaCodes.hpp:250-281 (decodeHamming84sx)
+    const unsigned b0 = b & 1, b1 = (b >> 1) & 1, b2 = (b >> 2) & 1, b3 = (b >> 3) & 1;
+    const unsigned b4 = (b >> 4) & 1, b5 = (b >> 5) & 1, b6 = (b >> 6) & 1, b7 = (b >> 7) & 1;
+    const unsigned syn = (b0 ^ b1 ^ b2 ^ b4) | ((b1 ^ b2 ^ b3 ^ b5) << 1) |
+                         ((b0 ^ b1 ^ b3 ^ b6) << 2) | ((b0 ^ b2 ^ b3 ^ b7) << 3);
+    switch (syn) {
+        case 0xD: return (b ^ 1) & 0xf;
+        case 0x7: return (b ^ 2) & 0xf;
+        case 0xB: return (b ^ 4) & 0xf;
+        case 0xE: return (b ^ 8) & 0xf;
+        default: return b & 0xf;
+    }
+}
+
+__device__ __forceinline__ uint16_t sx1272_checksum(const uint8_t* data, int len) {
+    // LoRaCodes.hpp:69-105
+    uint16_t res = 0;
+    uint8_t v = 0xff;
+    for (int i = 0; i < len; ++i) {
+        uint16_t crc = res;
+        for (int b = 0; b < 8; ++b) crc = (crc & 0x8000) ? (uint16_t)((crc << 1) ^ 0x1021) : (uint16_t)(crc << 1);
+        uint8_t t = v & 0xB8;
+        t ^= t >> 4; t ^= t >> 2; t ^= t >> 1;
+        v = (uint8_t)((t & 1) | (v << 1));
+        res = crc ^ data[i];
+    }
+    res ^= v;
+    uint8_t t = v & 0xB8;
+    t ^= t >> 4; t ^= t >> 2; t ^= t >> 1;
+    v = (uint8_t)((t & 1) | (v << 1));
+    res ^= (uint16_t)(v << 8);
+    return res;
+}
+
+struct FinalArgs {
+    const uint16_t* syms;
+    uint8_t* bytes;
+    lphy_frame_meta* meta;
+    unsigned long long frames;
+    unsigned long long nsyms;     // symbols per frame to decode
+    unsigned long long sym_stride;
+    int shift;                    // sf > 4 ? sf - 4 : 0
+    int decode;
+    int set_sync;
+};
+
+__global__ void k_finalize(FinalArgs A) {
+    const unsigned long long f = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= A.frames) return;
+    lphy_frame_meta m = A.meta[f];
+    if (m.status != 0) return;
+    if (A.set_sync && m.have_sync)
+        m.sync_word = (uint8_t)((((m.sw0 >> A.shift) & 0x0f) << 4) | ((m.sw1 >> A.shift) & 0x0f));
+    if (A.decode) {
+        if (A.nsyms & 1) {
+            m.status = -EINVAL;  // LoRaDecoder.cpp:10
+        } else {
+            const unsigned long long nb = A.nsyms / 2;
+            const uint16_t* s = A.syms + f * A.sym_stride;
+            uint8_t* out = A.bytes + f * nb;
+            for (unsigned long long k = 0; k < nb; ++k) {
+                const uint8_t hi = hamming84_decode((uint8_t)s[2 * k]) & 0x0f;
+                const uint8_t lo = hamming84_decode((uint8_t)s[2 * k + 1]) & 0x0f;
+                out[k] = (uint8_t)((hi << 4) | lo);
+            }
+            if (nb >= 4) {  // phy.cpp:252-259
+                const uint16_t provided = (uint16_t)(out[nb - 2] | (out[nb - 1] << 8));
+                m.crc_ok = provided == sx1272_checksum(out + 2, (int)(nb - 4));
+            } else {
+                m.crc_ok = 0;
+            }
+        }
+    }
+    A.meta[f] = m;
+}
+
+// ---------------------------------------------------------------------------
+// lora_modulate (LoRaMod.cpp:8-43 + ChirpGenerator.hpp:24-51), bit-exact.
+// Pass 1: one thread per frame walks the phase accumulator through every
+// symbol (no sincos) and records the phase at each symbol start.  Pass 2: one
+// thread per symbol regenerates its samples from that phase.
+// ---------------------------------------------------------------------------
+struct ModArgs {
+    const uint16_t* syms;
+    float2* iq;
+    float* phase0;           // frames * (nsyms + 2) phase at symbol start
+    unsigned long long frames, nsyms;
+    int N, osr;
+    float bws, ampl;
+    uint8_t sync;
+};
+
+__device__ __forceinline__ float mod_f0(const ModArgs& A, unsigned long long f, unsigned long long s) {
+    const int shift = 0;
+    (void)shift;
+    uint16_t v;
+    if (s < 2) {
+        int sf = 0;
+        while ((1 << sf) < A.N) ++sf;
+        const unsigned sh = sf > 4 ? sf - 4 : 0;
+        v = s == 0 ? (uint16_t)((A.sync >> 4) << sh) : (uint16_t)((A.sync & 0x0f) << sh);
+    } else {
+        v = A.syms[f * A.nsyms + (s - 2)];
+    }
+    return (2.0f * kPi * (float)v * A.bws) / ((float)A.N * (float)A.osr);
+}
+
+__global__ void k_mod_phase(ModArgs A) {
+    const unsigned long long f = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= A.frames) return;
+    const float fmin = -kPi * A.bws / (float)A.osr;
+    const float fmax = kPi * A.bws / (float)A.osr;
+    const float fstep = (2.0f * kPi * A.bws) / (float)(A.N * A.osr * A.osr);
+    const int step = A.N * A.osr;
+    float phase = 0.0f;
+    const unsigned long long ns = A.nsyms + 2;
+    for (unsigned long long s = 0; s < ns; ++s) {
+        A.phase0[f * ns + s] = phase;
+        float fr = fmin + mod_f0(A, f, s);
+        for (int i = 0; i < step; ++i) {
+            fr += fstep;
+            if (fr > fmax) fr -= (fmax - fmin);
+            phase += fr;
+        }
+        const double w = floor((double)(phase / (2.0f * kPi))) * 2 * (double)kPi;
+        phase = (float)((double)phase - w);
+    }
+}
+
+__global__ void k_mod_samples(ModArgs A) {
+    const unsigned long long g = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long ns = A.nsyms + 2;
+    if (g >= A.frames * ns) return;
+    const unsigned long long f = g / ns, s = g % ns;
+    const float fmin = -kPi * A.bws / (float)A.osr;
+    const float fmax = kPi * A.bws / (float)A.osr;
+    const float fstep = (2.0f * kPi * A.bws) / (float)(A.N * A.osr * A.osr);
+    const int step = A.N * A.osr;
+    float phase = A.phase0[g];
+    float fr = fmin + mod_f0(A, f, s);
+    float2* out = A.iq + (f * ns + s) * (unsigned long long)step;
+    for (int i = 0; i < step; ++i) {
+        fr += fstep;
+        if (fr > fmax) fr -= (fmax - fmin);
+        phase += fr;
+        float sn, cs;
+        lphy_libm::sincosf_exact(phase, &sn, &cs);
+        out[i] = make_float2(A.ampl * cs, A.ampl * sn);
+    }
+}
+
+// compensate_offsets (phy.cpp:150-180): rotation then integer time shift.
+__global__ void k_comp_rotate(float2* out, const float2* in, unsigned long long count,
+                              float rate) {
+    const unsigned long long n = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= count) return;
+    const float ph = rate * (float)n;
+    float sn, cs;
+    lphy_libm::sincosf_exact(ph, &sn, &cs);
+    out[n] = cmul(in[n], make_float2(cs, sn));
+}
+
+__global__ void k_comp_shift(float2* out, const float2* in, unsigned long long count,
+                             long long offset) {
+    const unsigned long long n = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= count) return;
+    const long long src = (long long)n - offset;
+    out[n] = (src >= 0 && src < (long long)count) ? in[src] : make_float2(0.0f, 0.0f);
+}
+
+}  // namespace
+
+// ===========================================================================
+// Host side
+// ===========================================================================
+struct lphy_hip_ctx {
+    int device = 0;
+    unsigned sf = 0, N = 0, bw_hz = 0, osr = 1;
+    int window = 0;
+    float2* d_tw = nullptr;
+    float2* d_down = nullptr;
+    float* d_win = nullptr;
+    // staging for the host convenience entry points
+    std::mutex mu;
+    void* d_stage = nullptr;
+    size_t stage_bytes = 0;
+};
+
+namespace {
+
+#define HIP_OK(x)                                                         \
+    do {                                                                  \
+        hipError_t e_ = (x);                                              \
+        if (e_ != hipSuccess) {                                           \
+            fprintf(stderr, "lphy_hip: %s failed: %s (%s:%d)\n", #x,      \
+                    hipGetErrorString(e_), __FILE__, __LINE__);           \
+            return -EIO;                                                  \
+        }                                                                 \
+    } while (0)
+
+// Host-side constant tables with the reference's own libm calls.
+void make_twiddles(std::vector<std::complex<float>>& tw, int nfft) {
+    // kissfft.hh:24-29: exp(i * (i*phinc)), phinc = -2*acos(-1)/nfft in float
+    tw.resize(nfft);
+    const float phinc = (-2 * std::acos((float)-1)) / nfft;
+    for (int i = 0; i < nfft; ++i) tw[i] = std::exp(std::complex<float>(0, i * phinc));
+}
+
+void make_downchirp(std::vector<std::complex<float>>& d, int N, float bw_scale) {
+    // genChirp(out, N, 1, N, 0, down=true, 1, phase=0, bw_scale)
+    // (ChirpGenerator.hpp:24-51)
+    d.resize(N);
+    const float fMin = -kPi * bw_scale / 1;
+    const float fMax = kPi * bw_scale / 1;
+    const float fStep = (2 * kPi * bw_scale) / (N * 1 * 1);
+    float f = fMin + 0.0f;
+    float phase = 0.0f;
+    for (int i = 0; i < N; ++i) {
+        f += fStep;
+        if (f > fMax) f -= (fMax - fMin);
+        phase -= f;
+        d[i] = std::polar(1.0f, phase);
+    }
+}
+
+void make_hann(std::vector<float>& w, int N) {
+    // LoRaDemod.cpp:17-21 / phy.cpp:37-42
+    w.resize(N);
+    for (int i = 0; i < N; ++i)
+        w[i] = 0.5f - 0.5f * std::cos(2.0f * kPi * static_cast<float>(i) /
+                                      (static_cast<float>(N) - 1.0f));
+}
+
+template <int SF>
+int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symbols) {
+    using G = Geo<SF>;
+    if (prologue)
+        hipLaunchKernelGGL(k_prologue<SF>, dim3((unsigned)A.frames), dim3(kTile), 0, st, A);
+    if (symbols) {
+        const unsigned long long nsym = A.frames * A.total_syms;
+        const unsigned long long tiles = (nsym + G::T - 1) / G::T;
+        if (tiles > 0x7fffffffULL) return -ERANGE;
+        if (tiles) hipLaunchKernelGGL(k_demod<SF>, dim3((unsigned)tiles), dim3(kTile), 0, st, A);
+    }
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int launch_demod(unsigned sf, const DemodArgs& A, hipStream_t st, bool pro, bool sym) {
+    switch (sf) {
+        case 1: return launch_demod_sf<1>(A, st, pro, sym);
+        case 2: return launch_demod_sf<2>(A, st, pro, sym);
+        case 3: return launch_demod_sf<3>(A, st, pro, sym);
+        case 4: return launch_demod_sf<4>(A, st, pro, sym);
+        case 5: return launch_demod_sf<5>(A, st, pro, sym);
+        case 6: return launch_demod_sf<6>(A, st, pro, sym);
+        case 7: return launch_demod_sf<7>(A, st, pro, sym);
+        case 8: return launch_demod_sf<8>(A, st, pro, sym);
+        case 9: return launch_demod_sf<9>(A, st, pro, sym);
+        case 10: return launch_demod_sf<10>(A, st, pro, sym);
+        case 11: return launch_demod_sf<11>(A, st, pro, sym);
+        case 12: return launch_demod_sf<12>(A, st, pro, sym);
+        default: return -EINVAL;
+    }
+}
+
+int ensure_stage(lphy_hip_ctx* c, size_t bytes) {
+    if (c->stage_bytes >= bytes) return 0;
+    if (c->d_stage) (void)hipFree(c->d_stage);
+    c->d_stage = nullptr;
+    c->stage_bytes = 0;
+    HIP_OK(hipMalloc(&c->d_stage, bytes));
+    c->stage_bytes = bytes;
+    return 0;
+}
+
+size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+}  // namespace
+
+extern "C" {
+
+const char* lphy_hip_version(void) { return "lphy_hip 0.1 gfx950"; }
+
+int lphy_hip_ctx_create(lphy_hip_ctx** out, int device, unsigned sf, unsigned bw_hz,
+                        unsigned osr, int window) {
+    if (!out) return -EINVAL;
+    *out = nullptr;
+    if (sf < 1 || sf > 12) return -EINVAL;
+    if (bw_hz != 125000 && bw_hz != 250000 && bw_hz != 500000) return -EINVAL;
+    if (osr == 0) osr = 1;
+    if (osr != 1) return -ENOTSUP;  // TODO(osr>1): p comparison needs log10f parity
+    if (window != LPHY_WINDOW_NONE && window != LPHY_WINDOW_HANN) return -EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return -ENODEV;
+    HIP_OK(hipSetDevice(device));
+    auto* c = new lphy_hip_ctx;
+    c->device = device;
+    c->sf = sf;
+    c->N = 1u << sf;
+    c->bw_hz = bw_hz;
+    c->osr = osr;
+    c->window = window;
+    std::vector<std::complex<float>> tw, down;
+    make_twiddles(tw, (int)c->N);
+    make_downchirp(down, (int)c->N, (float)bw_hz / 125000.0f);
+    if (hipMalloc(&c->d_tw, c->N * sizeof(float2)) != hipSuccess ||
+        hipMalloc(&c->d_down, c->N * sizeof(float2)) != hipSuccess) {
+        lphy_hip_ctx_destroy(c);
+        return -ENOMEM;
+    }
+    HIP_OK(hipMemcpy(c->d_tw, tw.data(), c->N * sizeof(float2), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(c->d_down, down.data(), c->N * sizeof(float2), hipMemcpyHostToDevice));
+    if (window == LPHY_WINDOW_HANN) {
+        std::vector<float> w;
+        make_hann(w, (int)c->N);
+        if (hipMalloc(&c->d_win, c->N * sizeof(float)) != hipSuccess) {
+            lphy_hip_ctx_destroy(c);
+            return -ENOMEM;
+        }
+        HIP_OK(hipMemcpy(c->d_win, w.data(), c->N * sizeof(float), hipMemcpyHostToDevice));
+    }
+    *out = c;
+    return 0;
+}
+
+void lphy_hip_ctx_destroy(lphy_hip_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->d_tw) (void)hipFree(c->d_tw);
+    if (c->d_down) (void)hipFree(c->d_down);
+    if (c->d_win) (void)hipFree(c->d_win);
+    if (c->d_stage) (void)hipFree(c->d_stage);
+    delete c;
+}
+
+size_t lphy_hip_syms_per_frame(const lphy_hip_ctx* c, size_t frame_samples, int mode) {
+    if (!c) return 0;
+    const size_t total = frame_samples / ((size_t)c->N * c->osr);
+    if (mode == LPHY_MODE_DEMODULATE) return total >= 2 ? total - 2 : 0;
+    return total >= 2 ? total - 2 : total;
+}
+
+int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
+                         size_t frame_samples, uint16_t* d_syms, uint8_t* d_bytes,
+                         lphy_frame_meta* d_meta, int mode, unsigned flags, void* stream) {
+    if (!c || !d_iq || !d_meta || !d_syms) return -EINVAL;
+    if (mode < 0 || mode > 2) return -EINVAL;
+    if ((flags & LPHY_F_DECODE) && !d_bytes) return -EINVAL;
+    if (frames == 0) return 0;
+    const size_t step = (size_t)c->N * c->osr;
+    const size_t total = frame_samples / step;
+    if (mode == LPHY_MODE_DEMODULATE) {
+        // phy.cpp:190-194
+        if (frame_samples % step != 0) return -EINVAL;
+        if (total < 2) return -ERANGE;
+    }
+    if (mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE && c->osr != 1) return -EINVAL;
+    HIP_OK(hipSetDevice(c->device));
+    hipStream_t st = (hipStream_t)stream;
+    DemodArgs A{};
+    A.iq = reinterpret_cast<const float2*>(d_iq);
+    A.tw = c->d_tw;
+    A.down = c->d_down;
+    A.win = c->window == LPHY_WINDOW_HANN ? c->d_win : nullptr;
+    A.syms = d_syms;
+    A.meta = d_meta;
+    A.frames = frames;
+    A.frame_samples = frame_samples;
+    A.total_syms = total;
+    A.out_per_frame = lphy_hip_syms_per_frame(c, frame_samples, mode);
+    A.osr = (int)c->osr;
+    A.mode = mode;
+    A.no_scratch = (flags & LPHY_F_NO_SCRATCH) ? 1 : 0;
+    const size_t est_syms = mode == LPHY_MODE_DEMODULATE ? 2 : (total < 2 ? total : 2);
+    A.est_units = (int)(est_syms * c->osr);
+    if (frames > 0x7fffffffULL) return -ERANGE;
+    const unsigned stages = flags & (LPHY_F_STAGE_PROLOGUE | LPHY_F_STAGE_SYMBOLS | LPHY_F_STAGE_FINAL);
+    const bool all = stages == 0;
+    int rc = launch_demod(c->sf, A, st, all || (stages & LPHY_F_STAGE_PROLOGUE),
+                          all || (stages & LPHY_F_STAGE_SYMBOLS));
+    if (rc) return rc;
+    if (!all && !(stages & LPHY_F_STAGE_FINAL)) return 0;
+    FinalArgs F{};
+    F.syms = d_syms;
+    F.bytes = d_bytes;
+    F.meta = d_meta;
+    F.frames = frames;
+    F.nsyms = A.out_per_frame;
+    F.sym_stride = A.out_per_frame;
+    F.shift = c->sf > 4 ? (int)c->sf - 4 : 0;
+    F.decode = (flags & LPHY_F_DECODE) ? 1 : 0;
+    F.set_sync = 1;
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)((frames + 255) / 256)), dim3(256), 0, st, F);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int lphy_hip_decode_batch(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames,
+                          size_t syms_per_frame, uint8_t* d_bytes, lphy_frame_meta* d_meta,
+                          void* stream) {
+    if (!c || !d_syms || !d_bytes || !d_meta) return -EINVAL;
+    if (syms_per_frame & 1) return -EINVAL;
+    if (frames == 0) return 0;
+    HIP_OK(hipSetDevice(c->device));
+    FinalArgs F{};
+    F.syms = d_syms;
+    F.bytes = d_bytes;
+    F.meta = d_meta;
+    F.frames = frames;
+    F.nsyms = syms_per_frame;
+    F.sym_stride = syms_per_frame;
+    F.shift = 0;
+    F.decode = 1;
+    F.set_sync = 0;
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)((frames + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, F);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int lphy_hip_estimate_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
+                            size_t frame_samples, size_t est_samples,
+                            lphy_frame_meta* d_meta, void* stream) {
+    if (!c || !d_iq || !d_meta) return -EINVAL;
+    const size_t step = (size_t)c->N * c->osr;
+    const size_t syms = est_samples / step;
+    if (syms == 0 || frames == 0) return 0;  // phy.cpp:87,91: nothing written
+    if (syms * c->osr > 0x7fffffffULL) return -ERANGE;
+    HIP_OK(hipSetDevice(c->device));
+    DemodArgs A{};
+    A.iq = reinterpret_cast<const float2*>(d_iq);
+    A.tw = c->d_tw;
+    A.down = c->d_down;
+    A.win = c->window == LPHY_WINDOW_HANN ? c->d_win : nullptr;
+    A.meta = d_meta;
+    A.frames = frames;
+    A.frame_samples = frame_samples;
+    A.total_syms = frame_samples / step;
+    A.osr = (int)c->osr;
+    A.mode = LPHY_MODE_DEMODULATE;
+    A.est_units = (int)(syms * c->osr);
+    hipStream_t st = (hipStream_t)stream;
+    switch (c->sf) {
+#define CASE(S) case S: hipLaunchKernelGGL(k_prologue<S>, dim3((unsigned)frames), dim3(kTile), 0, st, A); break;
+        CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6)
+        CASE(7) CASE(8) CASE(9) CASE(10) CASE(11) CASE(12)
+#undef CASE
+        default: return -EINVAL;
+    }
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int lphy_hip_compensate(lphy_hip_ctx* c, float* d_iq, size_t count, float cfo,
+                        float time_offset, void* stream) {
+    if (!c || !d_iq) return -EINVAL;
+    if (count == 0) return 0;
+    HIP_OK(hipSetDevice(c->device));
+    hipStream_t st = (hipStream_t)stream;
+    // phy.cpp:159-160
+    const float rate = -2.0f * kPi * cfo / (static_cast<float>(c->N) * static_cast<float>(c->osr));
+    float2* tmp = nullptr;
+    HIP_OK(hipMallocAsync((void**)&tmp, count * sizeof(float2), st));
+    const unsigned blocks = (unsigned)((count + 255) / 256);
+    float2* x = reinterpret_cast<float2*>(d_iq);
+    hipLaunchKernelGGL(k_comp_rotate, dim3(blocks), dim3(256), 0, st, tmp, x, (unsigned long long)count, rate);
+    const float r = std::round(time_offset);
+    long long off = (r >= -2147483648.0f && r < 2147483648.0f) ? (long long)(int)r : (long long)(int)0x80000000u;
+    if (off != 0 && (unsigned long long)(off > 0 ? off : -off) < count) {
+        hipLaunchKernelGGL(k_comp_shift, dim3(blocks), dim3(256), 0, st, x, tmp, (unsigned long long)count, off);
+    } else {
+        HIP_OK(hipMemcpyAsync(x, tmp, count * sizeof(float2), hipMemcpyDeviceToDevice, st));
+    }
+    HIP_OK(hipFreeAsync(tmp, st));
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int lphy_hip_modulate_batch(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames,
+                            size_t nsyms, float* d_iq, float amplitude, uint8_t sync,
+                            void* stream) {
+    if (!c || !d_iq || (nsyms && !d_syms)) return -EINVAL;
+    if (frames == 0) return 0;
+    HIP_OK(hipSetDevice(c->device));
+    hipStream_t st = (hipStream_t)stream;
+    ModArgs A{};
+    A.syms = d_syms;
+    A.iq = reinterpret_cast<float2*>(d_iq);
+    A.frames = frames;
+    A.nsyms = nsyms;
+    A.N = (int)c->N;
+    A.osr = (int)c->osr;
+    A.bws = (float)c->bw_hz / 125000.0f;
+    A.ampl = std::max(-1.0f, std::min(1.0f, amplitude));  // LoRaMod.cpp:18
+    A.sync = sync;
+    const size_t nph = frames * (nsyms + 2);
+    HIP_OK(hipMallocAsync((void**)&A.phase0, nph * sizeof(float), st));
+    hipLaunchKernelGGL(k_mod_phase, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, A);
+    hipLaunchKernelGGL(k_mod_samples, dim3((unsigned)((nph + 63) / 64)), dim3(64), 0, st, A);
+    HIP_OK(hipFreeAsync(A.phase0, st));
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int lphy_hip_sync(void* stream) {
+    HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+    return 0;
+}
+
+// ---- host-buffer convenience (synchronous) --------------------------------
+int lphy_hip_demod_host(lphy_hip_ctx* c, const float* h_iq, size_t frames,
+                        size_t frame_samples, uint16_t* h_syms, uint8_t* h_bytes,
+                        lphy_frame_meta* h_meta, int mode, unsigned flags) {
+    if (!c || !h_iq || !h_meta) return -EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    const size_t per = lphy_hip_syms_per_frame(c, frame_samples, mode);
+    const size_t iq_b = align_up(frames * frame_samples * sizeof(float2));
+    const size_t sym_b = align_up(std::max<size_t>(1, frames * per) * sizeof(uint16_t));
+    const size_t byte_b = align_up(std::max<size_t>(1, frames * (per / 2)));
+    const size_t meta_b = align_up(frames * sizeof(lphy_frame_meta));
+    int rc = ensure_stage(c, iq_b + sym_b + byte_b + meta_b);
+    if (rc) return rc;
+    char* base = (char*)c->d_stage;
+    float* d_iq = (float*)base;
+    uint16_t* d_syms = (uint16_t*)(base + iq_b);
+    uint8_t* d_bytes = (uint8_t*)(base + iq_b + sym_b);
+    lphy_frame_meta* d_meta = (lphy_frame_meta*)(base + iq_b + sym_b + byte_b);
+    HIP_OK(hipMemcpy(d_iq, h_iq, frames * frame_samples * sizeof(float2), hipMemcpyHostToDevice));
+    HIP_OK(hipMemset(d_meta, 0, frames * sizeof(lphy_frame_meta)));
+    rc = lphy_hip_demod_batch(c, d_iq, frames, frame_samples, d_syms,
+                              (flags & LPHY_F_DECODE) ? d_bytes : nullptr, d_meta, mode, flags,
+                              nullptr);
+    if (rc) return rc;
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(h_meta, d_meta, frames * sizeof(lphy_frame_meta), hipMemcpyDeviceToHost));
+    if (h_syms && per)
+        HIP_OK(hipMemcpy(h_syms, d_syms, frames * per * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    if (h_bytes && (flags & LPHY_F_DECODE) && per / 2)
+        HIP_OK(hipMemcpy(h_bytes, d_bytes, frames * (per / 2), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int lphy_hip_decode_host(lphy_hip_ctx* c, const uint16_t* h_syms, size_t count,
+                         uint8_t* h_bytes, lphy_frame_meta* h_meta) {
+    if (!c || !h_syms || !h_bytes || !h_meta) return -EINVAL;
+    if (count & 1) return -EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    const size_t sym_b = align_up(std::max<size_t>(1, count) * sizeof(uint16_t));
+    const size_t byte_b = align_up(std::max<size_t>(1, count / 2));
+    const size_t meta_b = align_up(sizeof(lphy_frame_meta));
+    int rc = ensure_stage(c, sym_b + byte_b + meta_b);
+    if (rc) return rc;
+    char* base = (char*)c->d_stage;
+    uint16_t* d_syms = (uint16_t*)base;
+    uint8_t* d_bytes = (uint8_t*)(base + sym_b);
+    lphy_frame_meta* d_meta = (lphy_frame_meta*)(base + sym_b + byte_b);
+    if (count) HIP_OK(hipMemcpy(d_syms, h_syms, count * sizeof(uint16_t), hipMemcpyHostToDevice));
+    HIP_OK(hipMemset(d_meta, 0, sizeof(lphy_frame_meta)));
+    rc = lphy_hip_decode_batch(c, d_syms, 1, count, d_bytes, d_meta, nullptr);
+    if (rc) return rc;
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(h_meta, d_meta, sizeof(lphy_frame_meta), hipMemcpyDeviceToHost));
+    if (count / 2) HIP_OK(hipMemcpy(h_bytes, d_bytes, count / 2, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int lphy_hip_estimate_host(lphy_hip_ctx* c, const float* h_iq, size_t count,
+                           lphy_frame_meta* h_meta) {
+    if (!c || !h_iq || !h_meta) return -EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    const size_t iq_b = align_up(std::max<size_t>(1, count) * sizeof(float2));
+    const size_t meta_b = align_up(sizeof(lphy_frame_meta));
+    int rc = ensure_stage(c, iq_b + meta_b);
+    if (rc) return rc;
+    char* base = (char*)c->d_stage;
+    float* d_iq = (float*)base;
+    lphy_frame_meta* d_meta = (lphy_frame_meta*)(base + iq_b);
+    HIP_OK(hipMemcpy(d_iq, h_iq, count * sizeof(float2), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_meta, h_meta, sizeof(lphy_frame_meta), hipMemcpyHostToDevice));
+    rc = lphy_hip_estimate_batch(c, d_iq, 1, count, count, d_meta, nullptr);
+    if (rc) return rc;
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(h_meta, d_meta, sizeof(lphy_frame_meta), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int lphy_hip_compensate_host(lphy_hip_ctx* c, float* h_iq, size_t count, float cfo,
+                             float time_offset) {
+    if (!c || !h_iq) return -EINVAL;
+    if (count == 0) return 0;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    int rc = ensure_stage(c, align_up(count * sizeof(float2)));
+    if (rc) return rc;
+    float* d = (float*)c->d_stage;
+    HIP_OK(hipMemcpy(d, h_iq, count * sizeof(float2), hipMemcpyHostToDevice));
+    rc = lphy_hip_compensate(c, d, count, cfo, time_offset, nullptr);
+    if (rc) return rc;
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(h_iq, d, count * sizeof(float2), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int lphy_hip_modulate_host(lphy_hip_ctx* c, const uint16_t* h_syms, size_t nsyms,
+                           float* h_iq, float amplitude, uint8_t sync) {
+    if (!c || !h_iq || (nsyms && !h_syms)) return -EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    const size_t samples = (nsyms + 2) * (size_t)c->N * c->osr;
+    const size_t sym_b = align_up(std::max<size_t>(1, nsyms) * sizeof(uint16_t));
+    int rc = ensure_stage(c, sym_b + align_up(samples * sizeof(float2)));
+    if (rc) return rc;
+    char* base = (char*)c->d_stage;
+    uint16_t* d_syms = (uint16_t*)base;
+    float* d_iq = (float*)(base + sym_b);
+    if (nsyms) HIP_OK(hipMemcpy(d_syms, h_syms, nsyms * sizeof(uint16_t), hipMemcpyHostToDevice));
+    rc = lphy_hip_modulate_batch(c, d_syms, 1, nsyms, d_iq, amplitude, sync, nullptr);
+    if (rc) return rc;
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(h_iq, d_iq, samples * sizeof(float2), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+}  // extern "C"

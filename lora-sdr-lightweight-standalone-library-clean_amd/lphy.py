@@ -1,0 +1,223 @@
+"""Python binding of the MI355X LoRa PHY C ABI (include/lphy_hip.h).
+
+Thin ctypes layer used by tests/, bench.py and __graft_entry__: it loads
+lib/liblphy_hip.so (built in-tree by the package Makefile) and exposes the
+batch entry points on device pointers (torch tensors) plus the host-buffer
+conveniences.  There is no fallback: when the library or a HIP device is
+missing, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import errno
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG = Path(__file__).resolve().parent
+LIB_DIR = PKG / "lib"
+HIP_SO = LIB_DIR / "liblphy_hip.so"
+SHIM_SO = LIB_DIR / "liblora_phy_amd.so"
+
+MODE_DEMODULATE = 0
+MODE_LORA_DEMODULATE = 1
+MODE_DECHIRP_LORA_DEMODULATE = 2
+F_DECODE = 1
+F_NO_SCRATCH = 2
+F_STAGE_PROLOGUE = 4
+F_STAGE_SYMBOLS = 8
+F_STAGE_FINAL = 16
+WINDOW_NONE = 0
+WINDOW_HANN = 1
+
+
+class FrameMeta(C.Structure):
+    _fields_ = [
+        ("cfo", C.c_float), ("time_offset", C.c_float), ("rate", C.c_float),
+        ("scale", C.c_float), ("t_off", C.c_int32), ("status", C.c_int32),
+        ("sw0", C.c_uint16), ("sw1", C.c_uint16), ("sync_word", C.c_uint8),
+        ("crc_ok", C.c_uint8), ("normalised", C.c_uint8), ("have_sync", C.c_uint8),
+    ]
+
+
+assert C.sizeof(FrameMeta) == 32
+
+META_DTYPE = np.dtype([
+    ("cfo", "<f4"), ("time_offset", "<f4"), ("rate", "<f4"), ("scale", "<f4"),
+    ("t_off", "<i4"), ("status", "<i4"), ("sw0", "<u2"), ("sw1", "<u2"),
+    ("sync_word", "u1"), ("crc_ok", "u1"), ("normalised", "u1"), ("have_sync", "u1"),
+])
+assert META_DTYPE.itemsize == 32
+
+_vp = C.c_void_p
+_sz = C.c_size_t
+
+EXPORTS = (
+    "lphy_hip_ctx_create", "lphy_hip_ctx_destroy", "lphy_hip_syms_per_frame",
+    "lphy_hip_demod_batch", "lphy_hip_decode_batch", "lphy_hip_estimate_batch",
+    "lphy_hip_compensate", "lphy_hip_modulate_batch", "lphy_hip_demod_host",
+    "lphy_hip_decode_host", "lphy_hip_estimate_host", "lphy_hip_compensate_host",
+    "lphy_hip_modulate_host", "lphy_hip_sync", "lphy_hip_version",
+)
+
+_LIB = None
+
+
+class LphyError(RuntimeError):
+    def __init__(self, rc: int, what: str):
+        name = errno.errorcode.get(-rc, str(rc))
+        super().__init__(f"{what} failed: -{name} ({rc})")
+        self.rc = rc
+
+
+def load(path: Path = HIP_SO) -> C.CDLL:
+    """Load liblphy_hip.so (raises if it was not built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not path.exists():
+        raise FileNotFoundError(f"{path} missing: build with __graft_entry__.build()")
+    L = C.CDLL(str(path))
+    L.lphy_hip_ctx_create.argtypes = [C.POINTER(_vp), C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_int]
+    L.lphy_hip_ctx_destroy.argtypes = [_vp]
+    L.lphy_hip_ctx_destroy.restype = None
+    L.lphy_hip_syms_per_frame.argtypes = [_vp, _sz, C.c_int]
+    L.lphy_hip_syms_per_frame.restype = _sz
+    L.lphy_hip_demod_batch.argtypes = [_vp, _vp, _sz, _sz, _vp, _vp, _vp, C.c_int, C.c_uint, _vp]
+    L.lphy_hip_decode_batch.argtypes = [_vp, _vp, _sz, _sz, _vp, _vp, _vp]
+    L.lphy_hip_estimate_batch.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _vp]
+    L.lphy_hip_compensate.argtypes = [_vp, _vp, _sz, C.c_float, C.c_float, _vp]
+    L.lphy_hip_modulate_batch.argtypes = [_vp, _vp, _sz, _sz, _vp, C.c_float, C.c_uint8, _vp]
+    L.lphy_hip_demod_host.argtypes = [_vp, _vp, _sz, _sz, _vp, _vp, _vp, C.c_int, C.c_uint]
+    L.lphy_hip_decode_host.argtypes = [_vp, _vp, _sz, _vp, _vp]
+    L.lphy_hip_estimate_host.argtypes = [_vp, _vp, _sz, _vp]
+    L.lphy_hip_compensate_host.argtypes = [_vp, _vp, _sz, C.c_float, C.c_float]
+    L.lphy_hip_modulate_host.argtypes = [_vp, _vp, _sz, _vp, C.c_float, C.c_uint8]
+    L.lphy_hip_sync.argtypes = [_vp]
+    L.lphy_hip_version.restype = C.c_char_p
+    _LIB = L
+    return L
+
+
+def _chk(rc: int, what: str) -> None:
+    if rc != 0:
+        raise LphyError(rc, what)
+
+
+def _ptr(a) -> int | None:
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()  # torch tensor
+
+
+class Demodulator:
+    """One (sf, bw, osr, window) configuration on one HIP device."""
+
+    def __init__(self, sf: int, bw_hz: int = 125000, osr: int = 1,
+                 window: int = WINDOW_NONE, device: int = 0):
+        self.lib = load()
+        self.sf, self.N, self.bw_hz, self.osr = sf, 1 << sf, bw_hz, osr
+        h = _vp()
+        _chk(self.lib.lphy_hip_ctx_create(C.byref(h), device, sf, bw_hz, osr, window),
+             "lphy_hip_ctx_create")
+        self.ctx = h
+
+    def close(self):
+        if self.ctx:
+            self.lib.lphy_hip_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def syms_per_frame(self, frame_samples: int, mode: int) -> int:
+        return self.lib.lphy_hip_syms_per_frame(self.ctx, frame_samples, mode)
+
+    # --- device batch API (torch tensors) --------------------------------
+    def demod_batch(self, iq, frames, frame_samples, syms, meta, mode, flags=0,
+                    payload=None, stream=None):
+        _chk(self.lib.lphy_hip_demod_batch(self.ctx, _ptr(iq), frames, frame_samples,
+                                           _ptr(syms), _ptr(payload), _ptr(meta), mode,
+                                           flags, stream),
+             "lphy_hip_demod_batch")
+
+    def modulate_batch(self, syms, frames, nsyms, iq, amplitude=1.0, sync=0x12, stream=None):
+        _chk(self.lib.lphy_hip_modulate_batch(self.ctx, _ptr(syms), frames, nsyms, _ptr(iq),
+                                              amplitude, sync, stream),
+             "lphy_hip_modulate_batch")
+
+    def decode_batch(self, syms, frames, syms_per_frame, payload, meta, stream=None):
+        _chk(self.lib.lphy_hip_decode_batch(self.ctx, _ptr(syms), frames, syms_per_frame,
+                                            _ptr(payload), _ptr(meta), stream),
+             "lphy_hip_decode_batch")
+
+    # --- host convenience ----------------------------------------------
+    def demod_host(self, iq: np.ndarray, frames: int, frame_samples: int, mode: int,
+                   flags: int = 0):
+        iq = np.ascontiguousarray(iq, np.complex64).reshape(-1)
+        assert iq.size == frames * frame_samples
+        per = self.syms_per_frame(frame_samples, mode)
+        syms = np.zeros(max(frames * per, 1), np.uint16)
+        payload = np.zeros(max(frames * (per // 2), 1), np.uint8)
+        meta = np.zeros(frames, META_DTYPE)
+        _chk(self.lib.lphy_hip_demod_host(self.ctx, iq.ctypes.data, frames, frame_samples,
+                                          syms.ctypes.data, payload.ctypes.data,
+                                          meta.ctypes.data, mode, flags),
+             "lphy_hip_demod_host")
+        return (syms[: frames * per].reshape(frames, per),
+                payload[: frames * (per // 2)].reshape(frames, per // 2), meta)
+
+    def decode_host(self, syms: np.ndarray):
+        syms = np.ascontiguousarray(syms, np.uint16)
+        out = np.zeros(max(len(syms) // 2, 1), np.uint8)
+        meta = np.zeros(1, META_DTYPE)
+        rc = self.lib.lphy_hip_decode_host(self.ctx, syms.ctypes.data, len(syms),
+                                           out.ctypes.data, meta.ctypes.data)
+        return rc, out[: len(syms) // 2], meta[0]
+
+    def estimate_host(self, iq: np.ndarray):
+        iq = np.ascontiguousarray(iq, np.complex64).reshape(-1)
+        meta = np.zeros(1, META_DTYPE)
+        _chk(self.lib.lphy_hip_estimate_host(self.ctx, iq.ctypes.data, iq.size,
+                                             meta.ctypes.data), "lphy_hip_estimate_host")
+        return meta[0]
+
+    def compensate_host(self, iq: np.ndarray, cfo: float, time_offset: float):
+        x = np.array(iq, np.complex64, copy=True).reshape(-1)
+        _chk(self.lib.lphy_hip_compensate_host(self.ctx, x.ctypes.data, x.size, cfo,
+                                               time_offset), "lphy_hip_compensate_host")
+        return x
+
+    def modulate_host(self, syms: np.ndarray, amplitude=1.0, sync=0x12):
+        syms = np.ascontiguousarray(syms, np.uint16)
+        out = np.zeros((len(syms) + 2) * self.N * self.osr, np.complex64)
+        _chk(self.lib.lphy_hip_modulate_host(self.ctx, syms.ctypes.data, len(syms),
+                                             out.ctypes.data, amplitude, sync),
+             "lphy_hip_modulate_host")
+        return out
+
+
+def hamming84_encode_table() -> np.ndarray:
+    """encodeHamming84sx (LoRaCodes.hpp:229-242) for nibbles 0..15 (producer)."""
+    t = np.zeros(16, np.uint16)
+    for x in range(16):
+        d = [(x >> i) & 1 for i in range(4)]
+        t[x] = (x | (d[0] ^ d[1] ^ d[2]) << 4 | (d[1] ^ d[2] ^ d[3]) << 5
+                | (d[0] ^ d[1] ^ d[3]) << 6 | (d[0] ^ d[2] ^ d[3]) << 7)
+    return t
+
+
+def encode_payloads(payloads: np.ndarray) -> np.ndarray:
+    """lora_encode for a [frames, bytes] uint8 array -> [frames, 2*bytes] uint16."""
+    t = hamming84_encode_table()
+    p = np.asarray(payloads, np.uint8)
+    out = np.empty(p.shape[:-1] + (2 * p.shape[-1],), np.uint16)
+    out[..., 0::2] = t[p >> 4]
+    out[..., 1::2] = t[p & 0x0F]
+    return out

@@ -285,6 +285,22 @@ ssize_t orc_decode(const uint16_t* syms, size_t n, uint8_t* out, size_t cap,
     return produced;
 }
 
+/* Test-side dechirp, tests/e2e_chain_test.cpp:80-93 */
+void orc_dechirp(const float* in, float* out, size_t count, unsigned sf,
+                 unsigned bw_hz) {
+    const size_t N = (size_t)1 << sf;
+    float down[2 * ORC_MAX_N], ph = 0.0f;
+    orc_genchirp(down, (int)N, 1, (int)N, 0.0f, 1, 1.0f, &ph, (float)bw_hz / 125000.0f);
+    for (size_t i = 0; i < 2 * count; ++i) out[i] = 0.0f;
+    for (size_t j = 0; j < (count / N) * N; ++j) {
+        cpx a = {in[2 * j], in[2 * j + 1]};
+        cpx d = {down[2 * (j % N)], down[2 * (j % N) + 1]};
+        cpx r = cmul(a, d);
+        out[2 * j] = r.re;
+        out[2 * j + 1] = r.im;
+    }
+}
+
 /* ---------------------------------------------------------------------- */
 /* LoRaMod.cpp:8-43                                                         */
 /* ---------------------------------------------------------------------- */

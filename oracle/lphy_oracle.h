@@ -37,6 +37,10 @@ size_t orc_lora_modulate(const uint16_t* syms, size_t n, float* out,
                          unsigned sf, unsigned osr, unsigned bw_hz,
                          float ampl, uint8_t sync);
 
+/* tests/e2e_chain_test.cpp:80-93 (whole symbols; tail zeroed) */
+void orc_dechirp(const float* in, float* out, size_t count, unsigned sf,
+                 unsigned bw_hz);
+
 /* LoRaEncoder.cpp:6-18 / LoRaDecoder.cpp:7-21 */
 size_t orc_lora_encode(const uint8_t* bytes, size_t n, uint16_t* out);
 ssize_t orc_lora_decode(const uint16_t* syms, size_t n, uint8_t* out);

@@ -63,6 +63,23 @@ int ref_genchirp(float* out, int N, int osr, int NN, float f0, int down,
     return r;
 }
 
+// Test-side dechirp exactly as tests/e2e_chain_test.cpp:80-93 writes it:
+// down = genChirp(N, down=true, phase 0); out[s*N+i] = in[s*N+i] * down[i]
+// for every whole symbol; samples past the last whole symbol stay zero.
+void ref_dechirp(const float* in, float* out, size_t count, unsigned sf,
+                 unsigned bw_hz) {
+    const size_t N = size_t(1) << sf;
+    std::vector<cf> down(N);
+    float phase = 0.0f;
+    genChirp(down.data(), int(N), 1, int(N), 0.0f, true, 1.0f, phase,
+             bw_scale(static_cast<bandwidth>(bw_hz)));
+    const cf* x = reinterpret_cast<const cf*>(in);
+    cf* y = reinterpret_cast<cf*>(out);
+    for (size_t i = 0; i < count; ++i) y[i] = cf(0.0f, 0.0f);
+    for (size_t s = 0; s < count / N; ++s)
+        for (size_t i = 0; i < N; ++i) y[s * N + i] = x[s * N + i] * down[i];
+}
+
 // LoRaMod.cpp:8-43
 size_t ref_lora_modulate(const uint16_t* syms, size_t n, float* out,
                          unsigned sf, unsigned osr, unsigned bw_hz,

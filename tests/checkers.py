@@ -51,6 +51,7 @@ class Oracle:
         L.orc_genchirp.argtypes = [_f32p, C.c_int, C.c_int, C.c_int, C.c_float,
                                    C.c_int, C.c_float, _f32p, C.c_float]
         L.orc_fft.argtypes = [_f32p, _f32p, C.c_int]
+        L.orc_dechirp.argtypes = [_f32p, _f32p, C.c_size_t, C.c_uint, C.c_uint]
         L.orc_detect.argtypes = [_f32p, _f32p, C.c_int, _f32p, _f32p, _f32p]
         L.orc_detect.restype = C.c_size_t
         L.orc_lora_modulate.argtypes = [_u16p, C.c_size_t, _f32p, C.c_uint, C.c_uint,
@@ -103,11 +104,10 @@ class Oracle:
         return out
 
     def dechirp(self, iq, sf, bw_hz=125000):
-        N = 1 << sf
-        down, _ = self.genchirp(N, 1, N, 0.0, True, 1.0, 0.0, bw_hz / 125000.0)
-        x = np.asarray(iq, np.complex64).reshape(-1, N)
-        # complex64 * complex64 in numpy = (ac-bd, ad+bc) in float32
-        return (x * down[None, :]).reshape(-1).astype(np.complex64)
+        x = _cf(np.asarray(iq, np.complex64))
+        out = np.zeros_like(x)
+        self.lib.orc_dechirp(_p(x, _f32p), _p(out, _f32p), len(x) // 2, sf, bw_hz)
+        return out.view(np.complex64)
 
     # --- consumers -----------------------------------------------------
     def fft(self, x):
@@ -180,6 +180,7 @@ class Reference:
                   "ref_sizeof_params", "ref_sizeof_metrics"):
             getattr(L, n).restype = C.c_size_t
         L.ref_fft.argtypes = [_f32p, _f32p, C.c_int]
+        L.ref_dechirp.argtypes = [_f32p, _f32p, C.c_size_t, C.c_uint, C.c_uint]
         L.ref_detect.argtypes = [_f32p, _f32p, C.c_int, _f32p, _f32p, _f32p]
         L.ref_detect.restype = C.c_size_t
         L.ref_genchirp.argtypes = [_f32p, C.c_int, C.c_int, C.c_int, C.c_float,
@@ -214,6 +215,12 @@ class Reference:
         x = _cf(np.asarray(x, np.complex64))
         out = np.zeros_like(x)
         self.lib.ref_fft(_p(x, _f32p), _p(out, _f32p), len(x) // 2)
+        return out.view(np.complex64)
+
+    def dechirp(self, iq, sf, bw_hz=125000):
+        x = _cf(np.asarray(iq, np.complex64))
+        out = np.zeros_like(x)
+        self.lib.ref_dechirp(_p(x, _f32p), _p(out, _f32p), len(x) // 2, sf, bw_hz)
         return out.view(np.complex64)
 
     def detect(self, x):

@@ -1,0 +1,37 @@
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+PKG = ROOT / "lora-sdr-lightweight-standalone-library-clean_amd"
+for p in (str(ROOT / "tests"), str(PKG), str(ROOT)):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) — run via gpurun")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from checkers import Oracle
+    return Oracle()
+
+
+@pytest.fixture(scope="session")
+def reference():
+    from checkers import Reference, reference_available
+    if not reference_available():
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    return Reference()
+
+
+@pytest.fixture(scope="session")
+def lphy():
+    import lphy as m
+    m.load()
+    return m
