@@ -119,54 +119,85 @@ LPHY_HD uint32_t inv_pio4(int i) {
     return t[i];
 }
 
-LPHY_HD void sincosf_exact(float y, float* sinp, float* cosp) {
-    const uint32_t T_PIO4 = 0x3f4;   // top12((float)pi/4)
-    const uint32_t T_2M12 = 0x398;   // top12(0x1p-12f)
-    const uint32_t T_120 = 0x42f;    // top12(120.0f)
-    const uint32_t T_INF = 0x7f8;    // top12(INFINITY)
-    const double hpi_inv = 0x1.45F306DC9C883p+23;  // 2^24 * 2/pi
-    const double hpi = 0x1.921FB54442D18p0;        // pi/2
+// Large |y| (>= 120) and Inf/NaN: glibc's Payne-Hanek path (reduce_large).
+LPHY_HD void sincosf_large(float y, float* sinp, float* cosp) {
+    const uint32_t T_INF = 0x7f8;                  // top12(INFINITY)
     const double pi63 = 0x1.921FB54442D18p-62;     // 2pi * 2^-64
-    double x = (double)y;
-    uint32_t t = top12(y);
-    if (t < T_PIO4) {
-        if (t < T_2M12) { *sinp = y; *cosp = 1.0f; return; }
-        sincos_poly(x, x * x, sincos_coef(0), 0, sinp, cosp);
+    if (top12(y) >= T_INF) {
+        float nanv = y - y;
+        *sinp = nanv; *cosp = nanv;
         return;
     }
-    if (t < T_120) {
-        double r = x * hpi_inv;
-        int n = ((int32_t)r + 0x800000) >> 24;
-        double xr = dfma(-(double)n, hpi, x);   // x - n*hpi, fused
-        double s = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;
-        sincos_poly(xr * s, xr * xr, sincos_coef((n & 2) ? 1 : 0), n, sinp,
-                    cosp);
-        return;
-    }
-    if (t < T_INF) {
-        uint32_t xi = f2u(y);
-        int sign = (int)(xi >> 31);
-        int idx = (int)((xi >> 26) & 15);
-        int shift = (int)((xi >> 23) & 7);
-        uint32_t m = (xi & 0xffffffu) | 0x800000u;
-        m <<= shift;
-        uint64_t res0 = (uint64_t)(uint32_t)(m * inv_pio4(idx));
-        uint64_t res1 = (uint64_t)m * inv_pio4(idx + 4);
-        uint64_t res2 = (uint64_t)m * inv_pio4(idx + 8);
-        res0 = (res2 >> 32) | (res0 << 32);
-        res0 += res1;
-        uint64_t nq = (res0 + (1ULL << 61)) >> 62;
-        res0 -= nq << 62;
-        double xr = (double)(int64_t)res0 * pi63;
-        int n = (int)nq;
-        int q = (n + sign) & 3;
-        double s = (q == 1 || q == 2) ? -1.0 : 1.0;
-        sincos_poly(xr * s, xr * xr, sincos_coef(((n + sign) & 2) ? 1 : 0), n,
-                    sinp, cosp);
-        return;
-    }
-    float nanv = y - y;
-    *sinp = nanv; *cosp = nanv;
+    uint32_t xi = f2u(y);
+    int sign = (int)(xi >> 31);
+    int idx = (int)((xi >> 26) & 15);
+    int shift = (int)((xi >> 23) & 7);
+    uint32_t m = (xi & 0xffffffu) | 0x800000u;
+    m <<= shift;
+    uint64_t res0 = (uint64_t)(uint32_t)(m * inv_pio4(idx));
+    uint64_t res1 = (uint64_t)m * inv_pio4(idx + 4);
+    uint64_t res2 = (uint64_t)m * inv_pio4(idx + 8);
+    res0 = (res2 >> 32) | (res0 << 32);
+    res0 += res1;
+    uint64_t nq = (res0 + (1ULL << 61)) >> 62;
+    res0 -= nq << 62;
+    double xr = (double)(int64_t)res0 * pi63;
+    int n = (int)nq;
+    int q = (n + sign) & 3;
+    double s = (q == 1 || q == 2) ? -1.0 : 1.0;
+    sincos_poly(xr * s, xr * xr, sincos_coef(((n + sign) & 2) ? 1 : 0), n, sinp, cosp);
+}
+
+// sincosf(y) exactly as glibc 2.35's FMA variant.  |y| < 120 (every CFO
+// rotation angle in practice) runs one straight-line path:
+//  * glibc's |y| < pi/4 branch is the n = 0 case of its fast reduction
+//    (n = 0, x - 0*hpi = x exactly), so it needs no branch of its own;
+//  * the second coefficient table is the first with the cos-polynomial
+//    coefficients negated, i.e. an exact negation of the cos result;
+//  * the quadrant sign s multiplies an odd polynomial: exact negation.
+// |y| < 2^-12 returns (y, 1) as glibc does; |y| >= 120 takes sincosf_large.
+// True when sincosf_fast is not valid for y (|y| >= 120, Inf, NaN).
+LPHY_HD bool sincosf_needs_large(float y) { return top12(y) >= 0x42f; }
+
+// The |y| < 120 path alone (result meaningless when sincosf_needs_large(y)).
+LPHY_HD void sincosf_fast(float y, float* sinp, float* cosp) {
+    const uint32_t T_2M12 = 0x398;   // top12(0x1p-12f)
+    const uint32_t t = top12(y);
+    const double S1 = -0x1.555545995a603p-3, S2 = 0x1.1107605230bc4p-7,
+                 S3 = -0x1.994eb3774cf24p-13;
+    const double C1 = -0x1.ffffffd0c621cp-2, C2 = 0x1.55553e1068f19p-5,
+                 C3 = -0x1.6c087e89a359dp-10, C4 = 0x1.99343027bf8c3p-16;
+    const double x = (double)y;
+    const double r = x * 0x1.45F306DC9C883p+23;            // x * 2^24 * 2/pi
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    const double xr = dfma(-(double)n, 0x1.921FB54442D18p0, x);  // x - n*pi/2
+    const double x2 = xr * xr;
+    // sin polynomial
+    const double x3 = x2 * xr;
+    const double s1 = dfma(x2, S3, S2);
+    const double s = dfma(x3, S1, xr);
+    const double x5 = x3 * x2;
+    float sv = (float)dfma(x5, s1, s);
+    // cos polynomial
+    const double x4 = x2 * x2;
+    const double c2 = dfma(x2, C4, C3);
+    const double c1 = dfma(x2, C1, 1.0);
+    const double x6 = x4 * x2;
+    const double c = dfma(x4, C2, c1);
+    float cv = (float)dfma(x6, c2, c);
+    const int q = n & 3;
+    if (q == 1 || q == 2) sv = -sv;   // quadrant sign of the odd polynomial
+    if (n & 2) cv = -cv;              // second coefficient table
+    const bool swap = (n & 1) != 0;
+    float so = swap ? cv : sv, co = swap ? sv : cv;
+    if (t < T_2M12) { so = y; co = 1.0f; }
+    *sinp = so;
+    *cosp = co;
+}
+
+LPHY_HD void sincosf_exact(float y, float* sinp, float* cosp) {
+    if (sincosf_needs_large(y)) { sincosf_large(y, sinp, cosp); return; }
+    sincosf_fast(y, sinp, cosp);
 }
 
 // ---------------------------------------------------------------------------

@@ -115,22 +115,43 @@ __device__ __forceinline__ int rev4(int high, int ndig) {
     return r;
 }
 
-// All butterflies of one pass on the lane's registers.  v[s*GS + a] is group
-// s, group-local index a; low[s] is the group's fixed low position part.
+// Position bookkeeping for pass (HI, LO), group slot s of lane lam:
+// group g = s*LPS + lam; fixed digits split into the part above the pass
+// (g / MH, weight SPAN) and below it (g % MH).
 template <int SF, int HI, int LO>
-__device__ __forceinline__ void pass_butterflies(float2 (&v)[16], const int (&low)[16],
+struct Group {
+    using G = Geo<SF>;
+    using P = PassGeo<SF, HI, LO>;
+    __device__ static __forceinline__ int g(int s, int lam) { return s * G::LPS + lam; }
+    __device__ static __forceinline__ int low(int s, int lam) { return g(s, lam) % P::MH; }
+    __device__ static __forceinline__ int high(int s, int lam) { return g(s, lam) / P::MH; }
+    __device__ static __forceinline__ int base(int s, int lam) {
+        return high(s, lam) * P::SPAN + low(s, lam);
+    }
+    // position of element e (= s*GS + a) of the lane
+    __device__ static __forceinline__ int pos(int e, int lam) {
+        return base(e / P::GS, lam) + (e % P::GS) * P::MH;
+    }
+};
+
+// All butterflies of one pass on the lane's registers.  v[s*GS + a] is group
+// s, group-local index a.
+template <int SF, int HI, int LO>
+__device__ __forceinline__ void pass_butterflies(float2 (&v)[16], int lam,
                                                  const float2* __restrict__ tw) {
     using G = Geo<SF>;
     using P = PassGeo<SF, HI, LO>;
+    using Gr = Group<SF, HI, LO>;
 #pragma unroll
     for (int l = HI; l >= LO; --l) {
         const int R = G::R(l), w = P::W(l), fs = G::FS(l);
 #pragma unroll
         for (int s = 0; s < P::SLOTS; ++s) {
+            const int low = Gr::low(s, lam);
 #pragma unroll
             for (int a = 0; a < P::GS; ++a) {
                 if (P::digit(a, l) != 0) continue;
-                const int k = low[s] + (a % w) * P::MH;
+                const int k = low + (a % w) * P::MH;
                 float2* x = &v[s * P::GS];
                 if (R == 2) {
                     const float2 t = cmul(x[a + w], tw[k * fs]);
@@ -155,77 +176,61 @@ __device__ __forceinline__ void pass_butterflies(float2 (&v)[16], const int (&lo
     }
 }
 
-// Group bookkeeping for pass (HI, LO) and lane lam of its symbol.
-template <int SF, int HI, int LO>
-__device__ __forceinline__ void pass_groups(int lam, int (&low)[16], int (&base)[16]) {
-    using G = Geo<SF>;
-    using P = PassGeo<SF, HI, LO>;
-#pragma unroll
-    for (int s = 0; s < P::SLOTS; ++s) {
-        const int g = s * G::LPS + lam;
-        const int hi_part = g / P::MH;
-        low[s] = g % P::MH;
-        base[s] = hi_part * P::SPAN + low[s];
-    }
-}
-
-// Pass p of the transform.  `sym` points at the symbol's LDS slot.
-//  FIRST: read inputs from the natural-order staging copy at index
-//         rev4(high) + vidx(a) (leaf permutation), barrier, compute, write
-//         positions.
-//  LAST:  leave results in registers (v, pos_of) for the detector.
+// Pass PI of the transform.  `sym` points at the symbol's LDS slot.
+//  first pass: read inputs from the natural-order staging copy at index
+//              rev4(high) + vidx(a) (KISS's leaf permutation), barrier,
+//              compute, write positions;
+//  last pass:  leave results in registers for the detector.
 template <int SF, int PI, bool LAST>
-__device__ __forceinline__ void run_pass(float2 (&v)[16], int (&pos_of)[16], float2* sym,
-                                         int lam, const float2* __restrict__ tw) {
+__device__ __forceinline__ void run_pass(float2 (&v)[16], float2* sym, int lam,
+                                         const float2* __restrict__ tw) {
     using G = Geo<SF>;
     constexpr Passes<SF> PS{};
     constexpr int HI = PS.hi[PI], LO = PS.lo[PI];
     using P = PassGeo<SF, HI, LO>;
-    int low[16], base[16];
-    pass_groups<SF, HI, LO>(lam, low, base);
+    using Gr = Group<SF, HI, LO>;
     if (PI == 0) {
 #pragma unroll
         for (int s = 0; s < P::SLOTS; ++s) {
-            const int high = base[s] / P::SPAN;
-            const int ib = rev4(high, LO);
+            const int ib = rev4(Gr::high(s, lam), LO);
 #pragma unroll
             for (int a = 0; a < P::GS; ++a) v[s * P::GS + a] = sym[G::lds(ib + P::vidx(a))];
         }
         __syncthreads();
     } else {
 #pragma unroll
-        for (int s = 0; s < P::SLOTS; ++s)
-#pragma unroll
-            for (int a = 0; a < P::GS; ++a) v[s * P::GS + a] = sym[G::lds(base[s] + a * P::MH)];
+        for (int e = 0; e < G::E; ++e) v[e] = sym[G::lds(Gr::pos(e, lam))];
     }
-    pass_butterflies<SF, HI, LO>(v, low, tw);
-#pragma unroll
-    for (int s = 0; s < P::SLOTS; ++s)
-#pragma unroll
-        for (int a = 0; a < P::GS; ++a) pos_of[s * P::GS + a] = base[s] + a * P::MH;
+    pass_butterflies<SF, HI, LO>(v, lam, tw);
     if (!LAST) {
 #pragma unroll
-        for (int e = 0; e < G::E; ++e) sym[G::lds(pos_of[e])] = v[e];
+        for (int e = 0; e < G::E; ++e) sym[G::lds(Gr::pos(e, lam))] = v[e];
         __syncthreads();
     }
 }
 
 template <int SF, int PI>
-__device__ __forceinline__ void run_passes(float2 (&v)[16], int (&pos_of)[16], float2* sym,
-                                           int lam, const float2* __restrict__ tw) {
+__device__ __forceinline__ void run_passes(float2 (&v)[16], float2* sym, int lam,
+                                           const float2* __restrict__ tw) {
     constexpr Passes<SF> PS{};
     if constexpr (PI < PS.n) {
-        run_pass<SF, PI, PI == PS.n - 1>(v, pos_of, sym, lam, tw);
-        run_passes<SF, PI + 1>(v, pos_of, sym, lam, tw);
+        run_pass<SF, PI, PI == PS.n - 1>(v, sym, lam, tw);
+        run_passes<SF, PI + 1>(v, sym, lam, tw);
     }
 }
 
-// Full transform of the staged symbol; on return v[e] holds bin pos_of[e].
-// Must be called by every thread of the tile (contains barriers).
+// Full transform of the staged symbol; on return v[e] holds bin
+// bin_of<SF>(e, lam).  Must be called by every thread of the tile.
 template <int SF>
-__device__ __forceinline__ void fft_tile(float2 (&v)[16], int (&pos_of)[16], float2* sym,
-                                         int lam, const float2* __restrict__ tw) {
-    run_passes<SF, 0>(v, pos_of, sym, lam, tw);
+__device__ __forceinline__ void fft_tile(float2 (&v)[16], float2* sym, int lam,
+                                         const float2* __restrict__ tw) {
+    run_passes<SF, 0>(v, sym, lam, tw);
+}
+
+template <int SF>
+__device__ __forceinline__ int bin_of(int e, int lam) {
+    constexpr Passes<SF> PS{};
+    return Group<SF, PS.hi[PS.n - 1], PS.lo[PS.n - 1]>::pos(e, lam);
 }
 
 // Argmax with the detector's semantics (LoRaDetector.hpp:46-58): strict '>'
@@ -237,18 +242,21 @@ struct ArgMax {
 };
 
 __device__ __forceinline__ ArgMax better(ArgMax a, ArgMax b) {
-    return (b.v > a.v || (b.v == a.v && b.i < a.i)) ? b : a;
+    const bool take = (b.v > a.v) | ((b.v == a.v) & (b.i < a.i));
+    return ArgMax{take ? b.v : a.v, take ? b.i : a.i};
 }
 
 template <int SF>
-__device__ __forceinline__ ArgMax local_argmax(const float2 (&v)[16], const int (&pos_of)[16]) {
+__device__ __forceinline__ ArgMax local_argmax(const float2 (&v)[16], int lam) {
     using G = Geo<SF>;
     ArgMax best{0.0f, 0x7fffffff};
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const float m2 = v[e].x * v[e].x + v[e].y * v[e].y;
-        ArgMax c{m2, pos_of[e]};
-        if (c.v > best.v || (c.v == best.v && c.v > 0.0f && c.i < best.i)) best = c;
+        const int bi = bin_of<SF>(e, lam);
+        const bool take = (m2 > best.v) | ((m2 == best.v) & (bi < best.i));
+        best.v = take ? m2 : best.v;
+        best.i = take ? bi : best.i;
     }
     return best;
 }

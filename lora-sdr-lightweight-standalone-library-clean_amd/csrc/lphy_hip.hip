@@ -102,7 +102,81 @@ __device__ __forceinline__ float2 est_sample(const DemodArgs& A, const float2* f
 }
 
 // ---------------------------------------------------------------------------
-// Prologue: one workgroup per frame
+// Stage 1a (modes 1, 2): per-frame max(|I|,|Q|) of the [dechirped] frame and
+// the normalisation decision (LoRaDemod.cpp:60-78).  A pure streaming
+// reduction: one workgroup per frame, 16-byte loads, 8 in flight per lane.
+// ---------------------------------------------------------------------------
+template <int SF>
+__global__ __launch_bounds__(kTile) void k_maxabs(DemodArgs A) {
+    constexpr int N = 1 << SF;
+    __shared__ float wmax[kTile / 64];
+    const unsigned long long f = blockIdx.x;
+    const int tid = threadIdx.x;
+    const float2* fr = A.iq + f * A.frame_samples;
+    const unsigned long long count = A.frame_samples;
+    const unsigned long long dech_end = A.total_syms * N;  // whole symbols
+    const bool dech = A.mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    float mx = 0.0f;
+    auto acc = [&](float2 x, unsigned long long i) {
+        if (dech) x = i < dech_end ? cmul(x, A.down[i & (N - 1)]) : make_float2(0.0f, 0.0f);
+        const float r = fabsf(x.x), im = fabsf(x.y);
+        const float m = (r < im) ? im : r;  // std::max(r, im): NaN in r never wins
+        if (m > mx) mx = m;
+    };
+    if ((reinterpret_cast<uintptr_t>(fr) & 15) == 0) {
+        const float4* f4 = reinterpret_cast<const float4*>(fr);
+        const unsigned long long n4 = count / 2;
+        constexpr int U = 8;
+        unsigned long long j = tid;
+        for (; j + (U - 1) * kTile < n4; j += U * kTile) {
+            float4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = f4[j + u * kTile];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const unsigned long long i = 2 * (j + u * kTile);
+                acc(make_float2(v[u].x, v[u].y), i);
+                acc(make_float2(v[u].z, v[u].w), i + 1);
+            }
+        }
+        for (; j < n4; j += kTile) {
+            const float4 v = f4[j];
+            acc(make_float2(v.x, v.y), 2 * j);
+            acc(make_float2(v.z, v.w), 2 * j + 1);
+        }
+        if ((count & 1) && tid == 0) acc(fr[count - 1], count - 1);
+    } else {
+        for (unsigned long long i = tid; i < count; i += kTile) acc(fr[i], i);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float o = __shfl_xor(mx, off, 64);
+        mx = o > mx ? o : mx;
+    }
+    if ((tid & 63) == 0) wmax[tid >> 6] = mx;
+    __syncthreads();
+    if (tid == 0) {
+        mx = wmax[0];
+#pragma unroll
+        for (int w = 1; w < kTile / 64; ++w) mx = wmax[w] > mx ? wmax[w] : mx;
+        lphy_frame_meta m{};
+        m.scale = 1.0f;
+        m.have_sync = A.total_syms >= 2;
+        if (mx > 1.0f) {
+            if (A.no_scratch) m.status = -ERANGE;  // LoRaDemod.cpp:69-71
+            m.normalised = 1;
+            m.scale = 1.0f / mx;
+        }
+        A.meta[f] = m;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Stage 1b: offset estimate (LoRaDemod.cpp:80-140 / phy.cpp:81-148).
+// Units = (symbol, osr phase) FFTs; a 256-thread tile packs T units, i.e.
+// T/U whole frames when a frame has U <= T units (8 frames per workgroup at
+// SF7), otherwise loops over one frame's units.  Per frame, one thread folds
+// the unit results in symbol order exactly like the reference loop.
 // ---------------------------------------------------------------------------
 struct UnitResult {
     int idx;
@@ -112,125 +186,101 @@ struct UnitResult {
 };
 
 template <int SF>
-__global__ __launch_bounds__(kTile) void k_prologue(DemodArgs A) {
+__global__ __launch_bounds__(kTile) void k_estimate(DemodArgs A) {
     using G = Geo<SF>;
-    constexpr int N = G::N;
-    __shared__ float2 lds[G::T * G::SSTRIDE];
+    constexpr int N = G::N, T = G::T;
+    __shared__ float2 lds[T * G::SSTRIDE];
+    __shared__ float2 twl[N];
     __shared__ ArgMax red[kTile / 64];
-    __shared__ float wmax[kTile / 64];
-    __shared__ UnitResult units[G::T];
-    __shared__ float fold[4];   // sum_index, phase_diff, prev_phase, have_prev
-    __shared__ unsigned fold_t;
-    __shared__ lphy_frame_meta sm;
+    __shared__ UnitResult units[T];
 
-    const unsigned long long f = blockIdx.x;
     const int tid = threadIdx.x;
-    const float2* fr = A.iq + f * A.frame_samples;
-    const unsigned long long count = A.frame_samples;
+    const int U = A.est_units;
+    const bool packed = U <= T;
+    const int FPT = packed ? T / U : 1;
+    const unsigned long long fbase = (unsigned long long)blockIdx.x * FPT;
     const unsigned long long step = (unsigned long long)N * A.osr;
+    for (int i = tid; i < N; i += kTile) twl[i] = A.tw[i];
 
-    // --- whole-frame max(|I|,|Q|) (lora_demodulate only) -------------------
-    float mx = 0.0f;
-    if (A.mode != LPHY_MODE_DEMODULATE) {
-        const unsigned long long dech_end = A.total_syms * N;  // dechirped span
-        for (unsigned long long i = tid; i < count; i += kTile) {
-            float2 x = fr[i];
-            if (A.mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
-                x = i < dech_end ? cmul(x, A.down[i & (N - 1)]) : make_float2(0.0f, 0.0f);
-            const float r = fabsf(x.x), im = fabsf(x.y);
-            const float m = (r < im) ? im : r;  // std::max(r, im)
-            if (m > mx) mx = m;
+    // fold state of frame (fbase + tid), held by thread tid < FPT
+    float sum_index = 0.0f, phase_diff = 0.0f, prev_phase = 0.0f;
+    bool have_prev = false;
+    unsigned sum_t = 0;
+    lphy_frame_meta mine{};
+    const bool folder = tid < FPT && fbase + tid < A.frames;
+    if (folder) {
+        if (A.mode == LPHY_MODE_DEMODULATE) {
+            mine.scale = 1.0f;
+            mine.have_sync = A.total_syms >= 2;
+        } else {
+            mine = A.meta[fbase + tid];
         }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const float o = __shfl_xor(mx, off, 64);
-            mx = o > mx ? o : mx;
-        }
-        if ((tid & 63) == 0) wmax[tid >> 6] = mx;
-        __syncthreads();
-        mx = wmax[0];
-#pragma unroll
-        for (int w = 1; w < kTile / 64; ++w) mx = wmax[w] > mx ? wmax[w] : mx;
     }
-    if (tid == 0) {
+
+    const int slot = tid / G::LPS, lam = tid % G::LPS;
+    const int chunks = packed ? 1 : (U + T - 1) / T;
+    for (int c = 0; c < chunks; ++c) {
+        int fl, u;
+        if (packed) { fl = slot / U; u = slot % U; }
+        else        { fl = 0; u = c * T + slot; }
+        const unsigned long long f = fbase + fl;
+        bool live = (packed ? fl < FPT : u < U) && f < A.frames;
         lphy_frame_meta m{};
-        m.scale = 1.0f;
-        m.have_sync = A.total_syms >= 2;
-        if (A.mode != LPHY_MODE_DEMODULATE && mx > 1.0f) {
-            if (A.no_scratch) m.status = -ERANGE;
-            m.normalised = 1;
-            m.scale = 1.0f / mx;
+        if (live) {
+            if (A.mode == LPHY_MODE_DEMODULATE) m.scale = 1.0f;
+            else m = A.meta[f];
+            live = m.status == 0;
         }
-        sm = m;
-    }
-    __syncthreads();
-    if (sm.status != 0) {
-        if (tid == 0) A.meta[f] = sm;
-        return;  // whole workgroup leaves together (uniform condition)
-    }
-    const lphy_frame_meta m0 = sm;
-
-    // --- estimate: FFT + detect per (symbol, osr phase) unit, folded in
-    // symbol order exactly like the reference loop (LoRaDemod.cpp:80-140,
-    // phy.cpp:95-147) -------------------------------------------------------
-    if (tid == 0) {
-        fold[0] = 0.0f; fold[1] = 0.0f; fold[2] = 0.0f; fold[3] = 0.0f;
-        fold_t = 0;
-    }
-    const int sym_slot = tid / G::LPS;   // symbol slot within the tile
-    const int lam = tid % G::LPS;        // lane within the symbol
-    for (int u0 = 0; u0 < A.est_units; u0 += G::T) {
-        const int u = u0 + sym_slot;
-        const bool live = u < A.est_units;
         const int s = live ? u / A.osr : 0, t = live ? u % A.osr : 0;
-        float2* sym = lds + sym_slot * G::SSTRIDE;
+        const float2* fr = A.iq + f * A.frame_samples;
+        float2* sym = lds + slot * G::SSTRIDE;
+        __syncthreads();  // previous chunk's readers are done with lds / units
         // stage natural-order samples sym[t + i*osr] (LoRaDemod.cpp:86-92)
 #pragma unroll
         for (int e = 0; e < G::E; ++e) {
             const int i = lam + e * G::LPS;
             float2 x = make_float2(0.0f, 0.0f);
-            if (live) x = est_sample(A, fr, (unsigned long long)s * step + t + (unsigned long long)i * A.osr, i, N, m0);
+            if (live) x = est_sample(A, fr, (unsigned long long)s * step + t + (unsigned long long)i * A.osr, i, N, m);
             sym[G::lds(i)] = x;
         }
         __syncthreads();
         float2 v[16];
-        int pos[16];
-        fft_tile<SF>(v, pos, sym, lam, A.tw);
+        fft_tile<SF>(v, sym, lam, twl);
         // keep the bins for the interpolation and the phase
 #pragma unroll
-        for (int e = 0; e < G::E; ++e) sym[G::lds(pos[e])] = v[e];
-        ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, pos), red);
+        for (int e = 0; e < G::E; ++e) sym[G::lds(bin_of<SF>(e, lam))] = v[e];
+        ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), red);
         __syncthreads();
-        if (live && lam == 0) {
-            // LoRaDetector.hpp:60-71
-            const int idx = best.i;
-            const float mv = best.v > 0.0f ? best.v : 0.0f;
-            const float fund = sqrtf(mv);
-            const float2 lb = sym[G::lds(idx > 0 ? idx - 1 : N - 1)];
-            const float2 rb = sym[G::lds(idx < N - 1 ? idx + 1 : 0)];
-            const float left = lphy_libm::cabsf_exact(lb.x, lb.y);
-            const float right = lphy_libm::cabsf_exact(rb.x, rb.y);
-            const double demon = (2.0 * (double)fund) - (double)right - (double)left;
-            const float fi = demon == 0.0 ? 0.0f : (float)(0.5 * (double)(right - left) / demon);
-            const float2 bin = sym[G::lds(idx)];
-            UnitResult r;
-            r.idx = idx;
-            r.valid = mv > 0.0f;  // osr == 1: p > -1e30 <=> maxValue > 0
-            r.findex = fi;
-            r.phase = lphy_libm::atan2f_exact(bin.y, bin.x);
-            units[sym_slot] = r;
+        if (lam == 0) {
+            UnitResult r{0, 0, 0.0f, 0.0f};
+            if (live) {
+                // LoRaDetector.hpp:60-71
+                const int idx = best.i;
+                const float mv = best.v > 0.0f ? best.v : 0.0f;
+                const float fund = sqrtf(mv);
+                const float2 lb = sym[G::lds(idx > 0 ? idx - 1 : N - 1)];
+                const float2 rb = sym[G::lds(idx < N - 1 ? idx + 1 : 0)];
+                const float left = lphy_libm::cabsf_exact(lb.x, lb.y);
+                const float right = lphy_libm::cabsf_exact(rb.x, rb.y);
+                const double demon = (2.0 * (double)fund) - (double)right - (double)left;
+                const float fi = demon == 0.0 ? 0.0f : (float)(0.5 * (double)(right - left) / demon);
+                const float2 bin = sym[G::lds(idx)];
+                r.idx = idx;
+                r.valid = mv > 0.0f;  // osr == 1: p > -1e30 <=> maxValue > 0
+                r.findex = fi;
+                r.phase = lphy_libm::atan2f_exact(bin.y, bin.x);
+            }
+            units[slot] = r;
         }
         __syncthreads();
-        if (tid == 0) {
-            const int nu = (A.est_units - u0) < G::T ? (A.est_units - u0) : G::T;
-            float sum_index = fold[0], phase_diff = fold[1], prev_phase = fold[2];
-            bool have_prev = fold[3] != 0.0f;
-            unsigned sum_t = fold_t;
+        if (folder) {
+            const int first = packed ? tid * U : 0;
+            const int nu = packed ? U : ((U - c * T) < T ? (U - c * T) : T);
             for (int s0 = 0; s0 < nu; s0 += A.osr) {
                 int best_idx = 0, best_t = 0;
                 float best_f = 0.0f, best_phase = 0.0f;  // atan2(0, 0) of an unset bin
                 for (int t2 = 0; t2 < A.osr; ++t2) {
-                    const UnitResult& r = units[s0 + t2];
+                    const UnitResult& r = units[first + s0 + t2];
                     if (r.valid) {
                         best_idx = r.idx; best_f = r.findex; best_t = t2; best_phase = r.phase;
                         break;
@@ -247,18 +297,12 @@ __global__ __launch_bounds__(kTile) void k_prologue(DemodArgs A) {
                 prev_phase = best_phase;
                 have_prev = true;
             }
-            fold[0] = sum_index; fold[1] = phase_diff; fold[2] = prev_phase;
-            fold[3] = have_prev ? 1.0f : 0.0f;
-            fold_t = sum_t;
         }
-        __syncthreads();
     }
 
-    if (tid == 0) {
-        const int est_syms = A.est_units / A.osr;
-        const float sum_index = fold[0], phase_diff = fold[1];
-        const unsigned sum_t = fold_t;
-        lphy_frame_meta m = m0;
+    if (folder && mine.status == 0) {
+        const int est_syms = U / A.osr;
+        lphy_frame_meta m = mine;
         const float avg_index = sum_index / (float)est_syms;
         const float cfo_coarse = avg_index / (float)N;
         float cfo_fine = 0.0f;
@@ -270,76 +314,113 @@ __global__ __launch_bounds__(kTile) void k_prologue(DemodArgs A) {
         m.time_offset = avg_t - frac * (float)N * (float)A.osr;
         m.t_off = round_to_int(m.time_offset);
         m.rate = -2.0f * kPi * m.cfo / (float)N;
-        A.meta[f] = m;
+        A.meta[fbase + tid] = m;
     }
 }
 
 // ---------------------------------------------------------------------------
-// Demodulation: 256-thread tiles of T symbols
+// Stage 2: per-symbol demodulation.  Persistent grid; each 256-thread
+// workgroup stages the twiddles (and, up to N = 1024, the down-chirp and the
+// window) in LDS once, then loops over tiles of T symbols.
 // ---------------------------------------------------------------------------
-template <int SF>
-__global__ __launch_bounds__(kTile) void k_demod(DemodArgs A) {
+template <int SF, int MODE>
+__global__ __launch_bounds__(kTile, (SF <= 8 ? 3 : 2)) void k_demod(DemodArgs A) {
     using G = Geo<SF>;
     constexpr int N = G::N;
+    constexpr bool TAB = N <= 1024;  // chirp + window tables in LDS
     __shared__ float2 lds[G::T * G::SSTRIDE];
+    __shared__ float2 twl[N];
+    __shared__ float2 dnl[TAB ? N : 1];
+    __shared__ float wnl[TAB ? N : 1];
     __shared__ ArgMax red[kTile / 64];
 
     const int tid = threadIdx.x;
+    for (int i = tid; i < N; i += kTile) {
+        twl[i] = A.tw[i];
+        if constexpr (TAB) {
+            if (MODE != LPHY_MODE_LORA_DEMODULATE) dnl[i] = A.down[i];
+            if (A.win) wnl[i] = A.win[i];
+        }
+    }
+    const float2* down = TAB ? dnl : A.down;
+    const float* win = A.win ? (TAB ? wnl : A.win) : nullptr;
+
     const int slot = tid / G::LPS, lam = tid % G::LPS;
-    const unsigned long long gsym = (unsigned long long)blockIdx.x * G::T + slot;
-    const bool live = gsym < A.frames * A.total_syms;
-    const unsigned long long f = live ? gsym / A.total_syms : 0;
-    const unsigned long long s = live ? gsym % A.total_syms : 0;
-    const lphy_frame_meta m = A.meta[f];
-    const bool ok = live && m.status == 0;
+    const unsigned long long nsym = A.frames * A.total_syms;
+    const unsigned long long tiles = (nsym + G::T - 1) / G::T;
     const unsigned long long step = (unsigned long long)N * A.osr;
-    const float2* fr = A.iq + f * A.frame_samples;
-    const unsigned long long base = shifted_base(s, step, m.t_off, A.frame_samples);
-    const float2* src = fr + base;
     const unsigned long long dech_end = A.total_syms * N;  // whole symbols only
-    const float start = m.rate * ((float)(s * N) + (float)m.t_off / (float)A.osr);
     float2* sym = lds + slot * G::SSTRIDE;
 
-    // stage: rotated samples in natural order (LoRaDemod.cpp:152-163,
-    // phy.cpp:217-229)
+    for (unsigned long long tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        const unsigned long long gsym = tile * G::T + slot;
+        const bool live = gsym < nsym;
+        const unsigned long long f = live ? gsym / A.total_syms : 0;
+        const unsigned long long s = live ? gsym - f * A.total_syms : 0;
+        const lphy_frame_meta m = A.meta[f];
+        const bool ok = live && m.status == 0;
+        const unsigned long long base = shifted_base(s, step, m.t_off, A.frame_samples);
+        const float2* src = A.iq + f * A.frame_samples + base;
+        const float start = m.rate * ((float)(s * N) + (float)m.t_off / (float)A.osr);
+        const bool norm = m.normalised != 0;
+
+        // all of the tile's IQ loads in flight at once (16 per lane)
+        float2 raw[16];
 #pragma unroll
-    for (int e = 0; e < G::E; ++e) {
-        const int i = lam + e * G::LPS;
-        float2 x = make_float2(0.0f, 0.0f);
-        if (ok) {
-            x = src[(unsigned long long)i * A.osr];
-            if (A.mode == LPHY_MODE_DEMODULATE) {
-                x = cmul(x, A.down[i]);  // phy.cpp:219-220: down-chirp of the window
+        for (int e = 0; e < G::E; ++e)
+            raw[e] = src[(unsigned long long)(lam + e * G::LPS) * A.osr];
+
+        // one rotated input sample (LoRaDemod.cpp:152-163, phy.cpp:217-229)
+        auto sample = [&](float2 x, int i, bool large) -> float2 {
+            if constexpr (MODE == LPHY_MODE_DEMODULATE) {
+                x = cmul(x, down[i]);  // phy.cpp:219-220: down-chirp of the window
             } else {
-                if (A.mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE) {
+                if constexpr (MODE == LPHY_MODE_DECHIRP_LORA_DEMODULATE) {
                     // the external dechirp ran on the unshifted buffer
                     // (e2e_chain_test.cpp:88-93): chirp index of the absolute sample
                     const unsigned long long j = base + (unsigned long long)i;
-                    x = j < dech_end ? cmul(x, A.down[j & (N - 1)]) : make_float2(0.0f, 0.0f);
+                    const float2 d = cmul(x, down[j & (N - 1)]);
+                    x = j < dech_end ? d : make_float2(0.0f, 0.0f);
                 }
-                if (m.normalised) x = cscale(x, m.scale);
+                if (norm) x = cscale(x, m.scale);
             }
             const float ph = start + m.rate * (float)i;
             float sn, cs;
-            lphy_libm::sincosf_exact(ph, &sn, &cs);
+            if (large) lphy_libm::sincosf_large(ph, &sn, &cs);
+            else lphy_libm::sincosf_fast(ph, &sn, &cs);
             x = cmul(x, make_float2(cs, sn));
-            if (A.win) x = cscale(x, A.win[i]);
+            if (win) x = cscale(x, win[i]);
+            return ok ? x : make_float2(0.0f, 0.0f);
+        };
+
+        __syncthreads();  // tables staged / previous tile's readers done
+        bool any_large = false;
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) {
+            const int i = lam + e * G::LPS;
+            any_large |= lphy_libm::sincosf_needs_large(start + m.rate * (float)i);
+            sym[G::lds(i)] = sample(raw[e], i, false);
         }
-        sym[G::lds(i)] = x;
-    }
-    __syncthreads();
-    float2 v[16];
-    int pos[16];
-    fft_tile<SF>(v, pos, sym, lam, A.tw);
-    const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, pos), red);
-    if (ok && lam == 0) {
-        const uint16_t idx = (uint16_t)best.i;
-        if (m.have_sync && s < 2) {
-            if (s == 0) A.meta[f].sw0 = idx;
-            else A.meta[f].sw1 = idx;
-        } else {
-            const unsigned long long o = m.have_sync ? s - 2 : s;
-            A.syms[f * A.out_per_frame + o] = idx;
+        if (any_large) {  // rare: |phase| >= 120 rad (large CFO x long frame)
+            for (int e = 0; e < G::E; ++e) {
+                const int i = lam + e * G::LPS;
+                if (lphy_libm::sincosf_needs_large(start + m.rate * (float)i))
+                    sym[G::lds(i)] = sample(src[(unsigned long long)i * A.osr], i, true);
+            }
+        }
+        __syncthreads();
+        float2 v[16];
+        fft_tile<SF>(v, sym, lam, twl);
+        const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), red);
+        if (ok && lam == 0) {
+            const uint16_t idx = (uint16_t)best.i;
+            if (m.have_sync && s < 2) {
+                if (s == 0) A.meta[f].sw0 = idx;
+                else A.meta[f].sw1 = idx;
+            } else {
+                const unsigned long long o = m.have_sync ? s - 2 : s;
+                A.syms[f * A.out_per_frame + o] = idx;
+            }
         }
     }
 }
@@ -581,16 +662,46 @@ void make_hann(std::vector<float>& w, int N) {
                                       (static_cast<float>(N) - 1.0f));
 }
 
+template <int SF, int MODE>
+int demod_grid() {
+    static int grid = 0;
+    if (grid == 0) {
+        int dev = 0, cus = 0, per = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_demod<SF, MODE>, kTile, 0);
+        grid = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
+    }
+    return grid;
+}
+
+template <int SF, int MODE>
+void launch_symbols(const DemodArgs& A, unsigned long long tiles, hipStream_t st) {
+    const unsigned long long g = (unsigned long long)demod_grid<SF, MODE>();
+    const unsigned long long grid = tiles < g ? tiles : g;
+    hipLaunchKernelGGL((k_demod<SF, MODE>), dim3((unsigned)grid), dim3(kTile), 0, st, A);
+}
+
 template <int SF>
 int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symbols) {
     using G = Geo<SF>;
-    if (prologue)
-        hipLaunchKernelGGL(k_prologue<SF>, dim3((unsigned)A.frames), dim3(kTile), 0, st, A);
+    if (prologue) {
+        if (A.mode != LPHY_MODE_DEMODULATE)
+            hipLaunchKernelGGL(k_maxabs<SF>, dim3((unsigned)A.frames), dim3(kTile), 0, st, A);
+        const int fpt = A.est_units <= G::T ? G::T / A.est_units : 1;
+        const unsigned long long blocks = (A.frames + fpt - 1) / fpt;
+        hipLaunchKernelGGL(k_estimate<SF>, dim3((unsigned)blocks), dim3(kTile), 0, st, A);
+    }
     if (symbols) {
         const unsigned long long nsym = A.frames * A.total_syms;
         const unsigned long long tiles = (nsym + G::T - 1) / G::T;
-        if (tiles > 0x7fffffffULL) return -ERANGE;
-        if (tiles) hipLaunchKernelGGL(k_demod<SF>, dim3((unsigned)tiles), dim3(kTile), 0, st, A);
+        if (tiles) {
+            switch (A.mode) {
+                case LPHY_MODE_DEMODULATE: launch_symbols<SF, LPHY_MODE_DEMODULATE>(A, tiles, st); break;
+                case LPHY_MODE_LORA_DEMODULATE: launch_symbols<SF, LPHY_MODE_LORA_DEMODULATE>(A, tiles, st); break;
+                default: launch_symbols<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>(A, tiles, st); break;
+            }
+        }
     }
     HIP_OK(hipGetLastError());
     return 0;
@@ -792,7 +903,10 @@ int lphy_hip_estimate_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     A.est_units = (int)(syms * c->osr);
     hipStream_t st = (hipStream_t)stream;
     switch (c->sf) {
-#define CASE(S) case S: hipLaunchKernelGGL(k_prologue<S>, dim3((unsigned)frames), dim3(kTile), 0, st, A); break;
+#define CASE(S) case S: { \
+        const int fpt = A.est_units <= Geo<S>::T ? Geo<S>::T / A.est_units : 1; \
+        hipLaunchKernelGGL(k_estimate<S>, dim3((unsigned)((frames + fpt - 1) / fpt)), dim3(kTile), 0, st, A); \
+        break; }
         CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6)
         CASE(7) CASE(8) CASE(9) CASE(10) CASE(11) CASE(12)
 #undef CASE
