@@ -160,9 +160,11 @@ LPHY_HD void sincosf_large(float y, float* sinp, float* cosp) {
 LPHY_HD bool sincosf_needs_large(float y) { return top12(y) >= 0x42f; }
 
 // The |y| < 120 path alone (result meaningless when sincosf_needs_large(y)).
+// glibc's tiny-argument shortcut (|y| < 2^-12 -> (y, 1)) is not needed: the
+// polynomial rounds to the same floats for every such input except y = -0,
+// whose sine it returns as +0 (exhaustive check, tests/cpp/libm_exact_check);
+// the y == 0 select restores that sign.
 LPHY_HD void sincosf_fast(float y, float* sinp, float* cosp) {
-    const uint32_t T_2M12 = 0x398;   // top12(0x1p-12f)
-    const uint32_t t = top12(y);
     const double S1 = -0x1.555545995a603p-3, S2 = 0x1.1107605230bc4p-7,
                  S3 = -0x1.994eb3774cf24p-13;
     const double C1 = -0x1.ffffffd0c621cp-2, C2 = 0x1.55553e1068f19p-5,
@@ -177,22 +179,23 @@ LPHY_HD void sincosf_fast(float y, float* sinp, float* cosp) {
     const double s1 = dfma(x2, S3, S2);
     const double s = dfma(x3, S1, xr);
     const double x5 = x3 * x2;
-    float sv = (float)dfma(x5, s1, s);
+    const float sv0 = (float)dfma(x5, s1, s);
     // cos polynomial
     const double x4 = x2 * x2;
     const double c2 = dfma(x2, C4, C3);
     const double c1 = dfma(x2, C1, 1.0);
     const double x6 = x4 * x2;
     const double c = dfma(x4, C2, c1);
-    float cv = (float)dfma(x6, c2, c);
-    const int q = n & 3;
-    if (q == 1 || q == 2) sv = -sv;   // quadrant sign of the odd polynomial
-    if (n & 2) cv = -cv;              // second coefficient table
+    const float cv0 = (float)dfma(x6, c2, c);
+    // quadrant: sin sign flips for n&3 in {1,2} (bit 1 of n+1), the cos
+    // table flips for n&3 in {2,3} (bit 1 of n); odd n swaps the pair
+    const uint32_t sflip = ((uint32_t)(n + 1) & 2u) << 30;
+    const uint32_t cflip = ((uint32_t)n & 2u) << 30;
+    const float sv = u2f(f2u(sv0) ^ sflip);
+    const float cv = u2f(f2u(cv0) ^ cflip);
     const bool swap = (n & 1) != 0;
-    float so = swap ? cv : sv, co = swap ? sv : cv;
-    if (t < T_2M12) { so = y; co = 1.0f; }
-    *sinp = so;
-    *cosp = co;
+    *sinp = y == 0.0f ? y : (swap ? cv : sv);
+    *cosp = swap ? sv : cv;
 }
 
 LPHY_HD void sincosf_exact(float y, float* sinp, float* cosp) {

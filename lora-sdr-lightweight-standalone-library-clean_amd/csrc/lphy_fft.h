@@ -17,7 +17,7 @@
 //   * stages are grouped into "passes" (innermost first) whose combined
 //     radix is <= 16 = E, the complex elements a lane keeps in VGPRs.  Within
 //     a pass every butterfly is lane-local; between passes the symbol makes
-//     one round trip through LDS (its N complex values, padded).
+//     one round trip through LDS (its N complex values, bank-swizzled).
 //   * a symbol is owned by LPS = N/16 consecutive lanes (8 lanes at SF7, one
 //     wavefront at SF10, four wavefronts at SF12); a 256-thread workgroup
 //     tile carries T = 256/LPS symbols and uses 32 KiB of LDS.
@@ -31,13 +31,37 @@ namespace lphy {
 
 constexpr int kTile = 256;  // threads per workgroup tile
 
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-    // GCC's inline complex<float> product: (ac - bd, ad + bc)
-    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+// Complex float held as a native 2-vector: adds/subs/scales issue as one
+// v_pk_*_f32 each (same IEEE ops per component), the complex product as two
+// v_pk_mul_f32 + one sub + one add.  Memory layout = std::complex<float>.
+typedef float cf32 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ cf32 cmul(cf32 a, cf32 b) {
+    // GCC's inline complex<float> product (ac - bd, ad + bc), unfused, as
+    // three packed ops: P = (ac, bc), Q = (bd, ad), P + (-Q.x, Q.y).
+    // x - y == x + (-y) and bc + ad == ad + bc exactly in IEEE arithmetic.
+    const cf32 P = a * b.xx;
+    const cf32 Q = a.yx * b.yy;
+    cf32 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(P), "v"(Q));
+    return r;
 }
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+// KISS radix-4 cross terms with scratch[4] = (s4.y, -s4.x) folded into the
+// operand modifiers (kissfft.hh:178-183): a + (b.y, -b.x) and a - (b.y, -b.x).
+__device__ __forceinline__ cf32 cadd_rot(cf32 a, cf32 b) {
+    cf32 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ cf32 csub_rot(cf32 a, cf32 b) {
+    cf32 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ cf32 cadd(cf32 a, cf32 b) { return a + b; }
+__device__ __forceinline__ cf32 csub(cf32 a, cf32 b) { return a - b; }
+__device__ __forceinline__ cf32 cscale(cf32 a, float s) { return a * s; }
+__device__ __forceinline__ cf32 czero() { return cf32{0.0f, 0.0f}; }
 
 template <int SF>
 struct Geo {
@@ -46,8 +70,38 @@ struct Geo {
     static constexpr int E = N < 16 ? N : 16;       // complex per lane
     static constexpr int LPS = N / E;               // lanes per symbol
     static constexpr int T = kTile / LPS;           // symbols per tile
-    static constexpr int PAD = N >= 32 ? N / 32 : 0;  // LDS pad (complex) per symbol
-    static constexpr int SSTRIDE = N + PAD;         // LDS stride per symbol
+    // LDS layout (bank model of every access pattern in this file, see
+    // DESIGN.md): for SF >= 5 a symbol slot is N complex wide and a position
+    // p lives at slot*N + (swz(p) ^ sx(slot)), where swz XORs higher position
+    // bits into lower ones and sx(slot) = slot*SKX mod N shifts neighbouring
+    // slots to other banks.  Both are GF(2)-linear, so for p = lanepart |
+    // constpart (disjoint bits, always the case here) the address is
+    // lbase(slot, lanepart) ^ cpart(constpart): one XOR per access.  SF <= 4
+    // (one symbol per lane) uses a padded stride N + 1 instead.
+    static constexpr bool XS = SF >= 5;
+    static constexpr int SSTRIDE = XS ? N : N + 1;  // LDS stride per symbol
+    static constexpr int SK1 = SF == 7 || SF == 8 ? 2 : SF <= 6 ? 3 : 4;
+    static constexpr int SM1 = SF <= 4 ? 0 : SF == 5 ? 1 : SF == 6 ? 3 : SF == 7 ? 7 : SF == 8 ? 15 : 31;
+    static constexpr int SK2 = SF == 8 ? 6 : 5;
+    static constexpr int SM2 = SF == 6 || SF == 7 ? 1 : SF == 8 || SF >= 11 ? 3 : 0;
+    static constexpr int SKX = SF == 5 ? 2 : SF == 6 ? 4 : SF == 7 ? 8 : SF == 8 ? 16 : 0;
+    __host__ __device__ static constexpr int swz(int p) {
+        return XS ? (p ^ ((p >> SK1) & SM1) ^ ((p >> SK2) & SM2)) : p;
+    }
+    __host__ __device__ static constexpr int sx(int slot) { return XS ? (slot * SKX) & (N - 1) : 0; }
+    // general address of position p of the symbol in `slot`
+    __host__ __device__ static constexpr int addr(int slot, int p) {
+        return slot * SSTRIDE + (swz(p) ^ sx(slot));
+    }
+    // split form: per-lane base for the lane-dependent position bits ...
+    __host__ __device__ static constexpr int lbase(int slot, int lanepart) {
+        return XS ? ((slot * N) | (swz(lanepart) ^ sx(slot))) : slot * SSTRIDE + lanepart;
+    }
+    // ... and the compile-time part of each access
+    __host__ __device__ static constexpr int cpart(int constpart) { return XS ? swz(constpart) : constpart; }
+    __host__ __device__ static constexpr int at(int lb, int cp) { return XS ? (lb ^ cp) : (lb + cp); }
+    // the same in bytes (complex = 8 B): lb8 = lbase << 3, cp8 = cpart << 3
+    __host__ __device__ static constexpr int at8(int lb8, int cp8) { return XS ? (lb8 ^ cp8) : (lb8 + cp8); }
     __host__ __device__ static constexpr int R(int l) { return ((SF & 1) && l == L - 1) ? 2 : 4; }
     __host__ __device__ static constexpr int M(int l) {
         int p = 1;
@@ -55,8 +109,6 @@ struct Geo {
         return N / p;
     }
     __host__ __device__ static constexpr int FS(int l) { return 1 << (2 * l); }
-    // padded LDS offset of position p inside a symbol (one slot per 32)
-    __device__ static __forceinline__ int lds(int p) { return N >= 32 ? p + (p >> 5) : p; }
 };
 
 // Pass partition: stages [lo, hi], innermost (largest l) first.
@@ -109,7 +161,7 @@ struct PassGeo {
 
 // Base-4 digit reversal of `high` over `ndig` digits (leaf permutation of the
 // digits that precede the first pass).
-__device__ __forceinline__ int rev4(int high, int ndig) {
+__host__ __device__ constexpr int rev4(int high, int ndig) {
     int r = 0;
     for (int d = 0; d < ndig; ++d) { r = (r << 2) | (high & 3); high >>= 2; }
     return r;
@@ -122,23 +174,28 @@ template <int SF, int HI, int LO>
 struct Group {
     using G = Geo<SF>;
     using P = PassGeo<SF, HI, LO>;
-    __device__ static __forceinline__ int g(int s, int lam) { return s * G::LPS + lam; }
-    __device__ static __forceinline__ int low(int s, int lam) { return g(s, lam) % P::MH; }
-    __device__ static __forceinline__ int high(int s, int lam) { return g(s, lam) / P::MH; }
-    __device__ static __forceinline__ int base(int s, int lam) {
+    __host__ __device__ static constexpr int g(int s, int lam) { return s * G::LPS + lam; }
+    __host__ __device__ static constexpr int low(int s, int lam) { return g(s, lam) % P::MH; }
+    __host__ __device__ static constexpr int high(int s, int lam) { return g(s, lam) / P::MH; }
+    __host__ __device__ static constexpr int base(int s, int lam) {
         return high(s, lam) * P::SPAN + low(s, lam);
     }
-    // position of element e (= s*GS + a) of the lane
-    __device__ static __forceinline__ int pos(int e, int lam) {
+    // position of element e (= s*GS + a) of the lane; the lane bits and the
+    // element bits are disjoint: pos(e, lam) = pos(0, lam) | pos(e, 0)
+    __host__ __device__ static constexpr int pos(int e, int lam) {
         return base(e / P::GS, lam) + (e % P::GS) * P::MH;
+    }
+    // first-pass input index of element e (KISS leaf permutation), same split
+    __host__ __device__ static constexpr int inidx(int e, int lam) {
+        return rev4(high(e / P::GS, lam), LO) + P::vidx(e % P::GS);
     }
 };
 
 // All butterflies of one pass on the lane's registers.  v[s*GS + a] is group
 // s, group-local index a.
 template <int SF, int HI, int LO>
-__device__ __forceinline__ void pass_butterflies(float2 (&v)[16], int lam,
-                                                 const float2* __restrict__ tw) {
+__device__ __forceinline__ void pass_butterflies(cf32 (&v)[16], int lam,
+                                                 const cf32* __restrict__ tw) {
     using G = Geo<SF>;
     using P = PassGeo<SF, HI, LO>;
     using Gr = Group<SF, HI, LO>;
@@ -152,86 +209,101 @@ __device__ __forceinline__ void pass_butterflies(float2 (&v)[16], int lam,
             for (int a = 0; a < P::GS; ++a) {
                 if (P::digit(a, l) != 0) continue;
                 const int k = low + (a % w) * P::MH;
-                float2* x = &v[s * P::GS];
+                cf32* x = &v[s * P::GS];
                 if (R == 2) {
-                    const float2 t = cmul(x[a + w], tw[k * fs]);
+                    const cf32 t = cmul(x[a + w], tw[k * fs]);
                     x[a + w] = csub(x[a], t);
                     x[a] = cadd(x[a], t);
                 } else {
-                    const float2 s0 = cmul(x[a + w], tw[k * fs]);
-                    const float2 s1 = cmul(x[a + 2 * w], tw[k * fs * 2]);
-                    const float2 s2 = cmul(x[a + 3 * w], tw[k * fs * 3]);
-                    const float2 s5 = csub(x[a], s1);
-                    const float2 a0 = cadd(x[a], s1);
-                    const float2 s3 = cadd(s0, s2);
-                    const float2 s4 = csub(s0, s2);
-                    const float2 r4 = make_float2(s4.y, -s4.x);
+                    const cf32 s0 = cmul(x[a + w], tw[k * fs]);
+                    const cf32 s1 = cmul(x[a + 2 * w], tw[k * fs * 2]);
+                    const cf32 s2 = cmul(x[a + 3 * w], tw[k * fs * 3]);
+                    const cf32 s5 = csub(x[a], s1);
+                    const cf32 a0 = cadd(x[a], s1);
+                    const cf32 s3 = cadd(s0, s2);
+                    const cf32 s4 = csub(s0, s2);
                     x[a + 2 * w] = csub(a0, s3);
                     x[a] = cadd(a0, s3);
-                    x[a + w] = cadd(s5, r4);
-                    x[a + 3 * w] = csub(s5, r4);
+                    x[a + w] = cadd_rot(s5, s4);
+                    x[a + 3 * w] = csub_rot(s5, s4);
                 }
             }
         }
     }
 }
 
-// Pass PI of the transform.  `sym` points at the symbol's LDS slot.
-//  first pass: read inputs from the natural-order staging copy at index
-//              rev4(high) + vidx(a) (KISS's leaf permutation), barrier,
-//              compute, write positions;
+// Pass PI of the transform on the tile's LDS (`lds`), symbol in `slot`.
+//  first pass: read inputs from the natural-order staging copy at KISS's
+//              leaf-permuted index, barrier, compute, write positions;
 //  last pass:  leave results in registers for the detector.
+__device__ __forceinline__ cf32 lds_ld(const cf32* lds, int byte_off) {
+    return *reinterpret_cast<const cf32*>(reinterpret_cast<const char*>(lds) + byte_off);
+}
+__device__ __forceinline__ void lds_st(cf32* lds, int byte_off, cf32 v) {
+    *reinterpret_cast<cf32*>(reinterpret_cast<char*>(lds) + byte_off) = v;
+}
+
 template <int SF, int PI, bool LAST>
-__device__ __forceinline__ void run_pass(float2 (&v)[16], float2* sym, int lam,
-                                         const float2* __restrict__ tw) {
+__device__ __forceinline__ void run_pass(cf32 (&v)[16], cf32* lds, int slot, int lam,
+                                         const cf32* __restrict__ tw) {
     using G = Geo<SF>;
     constexpr Passes<SF> PS{};
     constexpr int HI = PS.hi[PI], LO = PS.lo[PI];
-    using P = PassGeo<SF, HI, LO>;
     using Gr = Group<SF, HI, LO>;
     if (PI == 0) {
+        const int lb8 = G::lbase(slot, Gr::inidx(0, lam)) << 3;
 #pragma unroll
-        for (int s = 0; s < P::SLOTS; ++s) {
-            const int ib = rev4(Gr::high(s, lam), LO);
-#pragma unroll
-            for (int a = 0; a < P::GS; ++a) v[s * P::GS + a] = sym[G::lds(ib + P::vidx(a))];
-        }
+        for (int e = 0; e < G::E; ++e) v[e] = lds_ld(lds, G::at8(lb8, G::cpart(Gr::inidx(e, 0)) << 3));
         __syncthreads();
     } else {
+        const int lb8 = G::lbase(slot, Gr::pos(0, lam)) << 3;
 #pragma unroll
-        for (int e = 0; e < G::E; ++e) v[e] = sym[G::lds(Gr::pos(e, lam))];
+        for (int e = 0; e < G::E; ++e) v[e] = lds_ld(lds, G::at8(lb8, G::cpart(Gr::pos(e, 0)) << 3));
     }
     pass_butterflies<SF, HI, LO>(v, lam, tw);
     if (!LAST) {
+        const int lb8 = G::lbase(slot, Gr::pos(0, lam)) << 3;
 #pragma unroll
-        for (int e = 0; e < G::E; ++e) sym[G::lds(Gr::pos(e, lam))] = v[e];
+        for (int e = 0; e < G::E; ++e) lds_st(lds, G::at8(lb8, G::cpart(Gr::pos(e, 0)) << 3), v[e]);
         __syncthreads();
     }
 }
 
 template <int SF, int PI>
-__device__ __forceinline__ void run_passes(float2 (&v)[16], float2* sym, int lam,
-                                           const float2* __restrict__ tw) {
+__device__ __forceinline__ void run_passes(cf32 (&v)[16], cf32* lds, int slot, int lam,
+                                           const cf32* __restrict__ tw) {
     constexpr Passes<SF> PS{};
     if constexpr (PI < PS.n) {
-        run_pass<SF, PI, PI == PS.n - 1>(v, sym, lam, tw);
-        run_passes<SF, PI + 1>(v, sym, lam, tw);
+        run_pass<SF, PI, PI == PS.n - 1>(v, lds, slot, lam, tw);
+        run_passes<SF, PI + 1>(v, lds, slot, lam, tw);
     }
 }
 
-// Full transform of the staged symbol; on return v[e] holds bin
-// bin_of<SF>(e, lam).  Must be called by every thread of the tile.
+// Full transform of the symbol staged (natural order) in `slot` of the tile
+// LDS; on return v[e] holds bin bin_of<SF>(e, lam).  Must be called by every
+// thread of the tile (contains barriers).
 template <int SF>
-__device__ __forceinline__ void fft_tile(float2 (&v)[16], float2* sym, int lam,
-                                         const float2* __restrict__ tw) {
-    run_passes<SF, 0>(v, sym, lam, tw);
+__device__ __forceinline__ void fft_tile(cf32 (&v)[16], cf32* lds, int slot, int lam,
+                                         const cf32* __restrict__ tw) {
+    run_passes<SF, 0>(v, lds, slot, lam, tw);
 }
 
 template <int SF>
-__device__ __forceinline__ int bin_of(int e, int lam) {
+__host__ __device__ constexpr int bin_of(int e, int lam) {
     constexpr Passes<SF> PS{};
     return Group<SF, PS.hi[PS.n - 1], PS.lo[PS.n - 1]>::pos(e, lam);
 }
+
+// Natural-order staging address of sample i = lam + e*LPS of the slot.
+template <int SF>
+struct Stage {
+    using G = Geo<SF>;
+    int lb8;
+    __device__ __forceinline__ Stage(int slot, int lam) : lb8(G::lbase(slot, lam) << 3) {}
+    __device__ __forceinline__ void put(cf32* lds, int e, cf32 x) const {
+        lds_st(lds, G::at8(lb8, G::cpart(e * G::LPS) << 3), x);
+    }
+};
 
 // Argmax with the detector's semantics (LoRaDetector.hpp:46-58): strict '>'
 // from maxValue = 0 scanning upward, i.e. the lowest index among the maxima
@@ -246,17 +318,37 @@ __device__ __forceinline__ ArgMax better(ArgMax a, ArgMax b) {
     return ArgMax{take ? b.v : a.v, take ? b.i : a.i};
 }
 
+// Element order of the last pass sorted by increasing bin: bin_of(e, lam) =
+// bin_of(0, lam) | bin_of(e, 0), so this order is increasing for every lane.
 template <int SF>
-__device__ __forceinline__ ArgMax local_argmax(const float2 (&v)[16], int lam) {
+struct BinOrder {
+    int e[16] = {};
+    constexpr BinOrder() {
+        constexpr int E = Geo<SF>::E;
+        for (int i = 0; i < E; ++i) e[i] = i;
+        for (int i = 0; i < E; ++i)
+            for (int j = i + 1; j < E; ++j)
+                if (bin_of<SF>(e[j], 0) < bin_of<SF>(e[i], 0)) { int t = e[i]; e[i] = e[j]; e[j] = t; }
+    }
+};
+
+// Lane-local part of the detector's scan: visiting the lane's bins in
+// increasing order with a strict '>' keeps the first maximum, exactly like
+// the reference loop restricted to these bins.
+template <int SF>
+__device__ __forceinline__ ArgMax local_argmax(const cf32 (&v)[16], int lam) {
     using G = Geo<SF>;
+    constexpr BinOrder<SF> BO{};
     ArgMax best{0.0f, 0x7fffffff};
+    const int lane_bin = bin_of<SF>(0, lam);
 #pragma unroll
-    for (int e = 0; e < G::E; ++e) {
-        const float m2 = v[e].x * v[e].x + v[e].y * v[e].y;
-        const int bi = bin_of<SF>(e, lam);
-        const bool take = (m2 > best.v) | ((m2 == best.v) & (bi < best.i));
+    for (int k = 0; k < G::E; ++k) {
+        const int e = BO.e[k];
+        const cf32 sq = v[e] * v[e];
+        const float m2 = sq.x + sq.y;
+        const bool take = m2 > best.v;
         best.v = take ? m2 : best.v;
-        best.i = take ? bi : best.i;
+        best.i = take ? (lane_bin | bin_of<SF>(e, 0)) : best.i;
     }
     return best;
 }

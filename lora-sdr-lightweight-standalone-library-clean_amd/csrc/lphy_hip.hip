@@ -11,7 +11,7 @@
 //   k_prologue   one 256-thread workgroup per frame: max-abs reduction,
 //                estimate FFTs (tile machinery of lphy_fft.h), offsets.
 //   k_demod<SF>  256-thread tiles of T = 256/(N/16) symbols; each symbol is
-//                staged to LDS with coalesced float2 loads while the rotation
+//                staged to LDS with coalesced cf32 loads while the rotation
 //                (glibc-exact sincosf in FP64) is applied, transformed by
 //                LPS = N/16 lanes holding 16 complex each, and reduced by
 //                cross-lane argmax.  No MFMA: the path is HBM/VALU bound.
@@ -28,6 +28,7 @@
 #include <cmath>
 #include <complex>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -46,9 +47,9 @@ constexpr float kPi = 3.14159265358979323846f;  // lora_phy::PI (phy.hpp:20)
 // Per-launch parameters
 // ---------------------------------------------------------------------------
 struct DemodArgs {
-    const float2* iq;        // frames * frame_samples
-    const float2* tw;        // N twiddles (KISS, forward)
-    const float2* down;      // N down-chirp samples (genChirp, down=true)
+    const cf32* iq;        // frames * frame_samples
+    const cf32* tw;        // N twiddles (KISS, forward)
+    const cf32* down;      // N down-chirp samples (genChirp, down=true)
     const float* win;        // N window coefficients or nullptr
     uint16_t* syms;          // output symbols
     lphy_frame_meta* meta;   // per-frame meta (prologue -> demod hand-off)
@@ -89,13 +90,13 @@ __device__ __forceinline__ unsigned long long shifted_base(unsigned long long s,
 // Input sample for the estimate (no rotation): raw (mode 0) or
 // [dechirped,] [normalised] (modes 1, 2).  idx is the absolute sample index
 // in the frame, i the index inside the symbol (window / mode-0 chirp).
-__device__ __forceinline__ float2 est_sample(const DemodArgs& A, const float2* fr,
+__device__ __forceinline__ cf32 est_sample(const DemodArgs& A, const cf32* fr,
                                              unsigned long long idx, int i, int N,
                                              const lphy_frame_meta& m) {
-    float2 x = fr[idx];
+    cf32 x = fr[idx];
     if (A.mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
         x = idx < A.total_syms * (unsigned long long)N ? cmul(x, A.down[idx & (N - 1)])
-                                                       : make_float2(0.0f, 0.0f);
+                                                       : czero();
     if (A.mode != LPHY_MODE_DEMODULATE && m.normalised) x = cscale(x, m.scale);
     if (A.win) x = cscale(x, A.win[i]);
     return x;
@@ -112,13 +113,13 @@ __global__ __launch_bounds__(kTile) void k_maxabs(DemodArgs A) {
     __shared__ float wmax[kTile / 64];
     const unsigned long long f = blockIdx.x;
     const int tid = threadIdx.x;
-    const float2* fr = A.iq + f * A.frame_samples;
+    const cf32* fr = A.iq + f * A.frame_samples;
     const unsigned long long count = A.frame_samples;
     const unsigned long long dech_end = A.total_syms * N;  // whole symbols
     const bool dech = A.mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     float mx = 0.0f;
-    auto acc = [&](float2 x, unsigned long long i) {
-        if (dech) x = i < dech_end ? cmul(x, A.down[i & (N - 1)]) : make_float2(0.0f, 0.0f);
+    auto acc = [&](cf32 x, unsigned long long i) {
+        if (dech) x = i < dech_end ? cmul(x, A.down[i & (N - 1)]) : czero();
         const float r = fabsf(x.x), im = fabsf(x.y);
         const float m = (r < im) ? im : r;  // std::max(r, im): NaN in r never wins
         if (m > mx) mx = m;
@@ -135,14 +136,14 @@ __global__ __launch_bounds__(kTile) void k_maxabs(DemodArgs A) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const unsigned long long i = 2 * (j + u * kTile);
-                acc(make_float2(v[u].x, v[u].y), i);
-                acc(make_float2(v[u].z, v[u].w), i + 1);
+                acc(cf32{v[u].x, v[u].y}, i);
+                acc(cf32{v[u].z, v[u].w}, i + 1);
             }
         }
         for (; j < n4; j += kTile) {
             const float4 v = f4[j];
-            acc(make_float2(v.x, v.y), 2 * j);
-            acc(make_float2(v.z, v.w), 2 * j + 1);
+            acc(cf32{v.x, v.y}, 2 * j);
+            acc(cf32{v.z, v.w}, 2 * j + 1);
         }
         if ((count & 1) && tid == 0) acc(fr[count - 1], count - 1);
     } else {
@@ -189,8 +190,8 @@ template <int SF>
 __global__ __launch_bounds__(kTile) void k_estimate(DemodArgs A) {
     using G = Geo<SF>;
     constexpr int N = G::N, T = G::T;
-    __shared__ float2 lds[T * G::SSTRIDE];
-    __shared__ float2 twl[N];
+    __shared__ cf32 lds[T * G::SSTRIDE];
+    __shared__ cf32 twl[N];
     __shared__ ArgMax red[kTile / 64];
     __shared__ UnitResult units[T];
 
@@ -232,23 +233,23 @@ __global__ __launch_bounds__(kTile) void k_estimate(DemodArgs A) {
             live = m.status == 0;
         }
         const int s = live ? u / A.osr : 0, t = live ? u % A.osr : 0;
-        const float2* fr = A.iq + f * A.frame_samples;
-        float2* sym = lds + slot * G::SSTRIDE;
+        const cf32* fr = A.iq + f * A.frame_samples;
         __syncthreads();  // previous chunk's readers are done with lds / units
         // stage natural-order samples sym[t + i*osr] (LoRaDemod.cpp:86-92)
+        const Stage<SF> st(slot, lam);
 #pragma unroll
         for (int e = 0; e < G::E; ++e) {
             const int i = lam + e * G::LPS;
-            float2 x = make_float2(0.0f, 0.0f);
+            cf32 x = czero();
             if (live) x = est_sample(A, fr, (unsigned long long)s * step + t + (unsigned long long)i * A.osr, i, N, m);
-            sym[G::lds(i)] = x;
+            st.put(lds, e, x);
         }
         __syncthreads();
-        float2 v[16];
-        fft_tile<SF>(v, sym, lam, twl);
+        cf32 v[16];
+        fft_tile<SF>(v, lds, slot, lam, twl);
         // keep the bins for the interpolation and the phase
 #pragma unroll
-        for (int e = 0; e < G::E; ++e) sym[G::lds(bin_of<SF>(e, lam))] = v[e];
+        for (int e = 0; e < G::E; ++e) lds[G::addr(slot, bin_of<SF>(e, lam))] = v[e];
         ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), red);
         __syncthreads();
         if (lam == 0) {
@@ -258,13 +259,13 @@ __global__ __launch_bounds__(kTile) void k_estimate(DemodArgs A) {
                 const int idx = best.i;
                 const float mv = best.v > 0.0f ? best.v : 0.0f;
                 const float fund = sqrtf(mv);
-                const float2 lb = sym[G::lds(idx > 0 ? idx - 1 : N - 1)];
-                const float2 rb = sym[G::lds(idx < N - 1 ? idx + 1 : 0)];
+                const cf32 lb = lds[G::addr(slot, idx > 0 ? idx - 1 : N - 1)];
+                const cf32 rb = lds[G::addr(slot, idx < N - 1 ? idx + 1 : 0)];
                 const float left = lphy_libm::cabsf_exact(lb.x, lb.y);
                 const float right = lphy_libm::cabsf_exact(rb.x, rb.y);
                 const double demon = (2.0 * (double)fund) - (double)right - (double)left;
                 const float fi = demon == 0.0 ? 0.0f : (float)(0.5 * (double)(right - left) / demon);
-                const float2 bin = sym[G::lds(idx)];
+                const cf32 bin = lds[G::addr(slot, idx)];
                 r.idx = idx;
                 r.valid = mv > 0.0f;  // osr == 1: p > -1e30 <=> maxValue > 0
                 r.findex = fi;
@@ -323,14 +324,14 @@ __global__ __launch_bounds__(kTile) void k_estimate(DemodArgs A) {
 // workgroup stages the twiddles (and, up to N = 1024, the down-chirp and the
 // window) in LDS once, then loops over tiles of T symbols.
 // ---------------------------------------------------------------------------
-template <int SF, int MODE>
-__global__ __launch_bounds__(kTile, (SF <= 8 ? 3 : 2)) void k_demod(DemodArgs A) {
+template <int SF, int MODE, int OCC>
+__global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
     using G = Geo<SF>;
     constexpr int N = G::N;
     constexpr bool TAB = N <= 1024;  // chirp + window tables in LDS
-    __shared__ float2 lds[G::T * G::SSTRIDE];
-    __shared__ float2 twl[N];
-    __shared__ float2 dnl[TAB ? N : 1];
+    __shared__ cf32 lds[G::T * G::SSTRIDE];
+    __shared__ cf32 twl[N];
+    __shared__ cf32 dnl[TAB ? N : 1];
     __shared__ float wnl[TAB ? N : 1];
     __shared__ ArgMax red[kTile / 64];
 
@@ -342,15 +343,14 @@ __global__ __launch_bounds__(kTile, (SF <= 8 ? 3 : 2)) void k_demod(DemodArgs A)
             if (A.win) wnl[i] = A.win[i];
         }
     }
-    const float2* down = TAB ? dnl : A.down;
+    const cf32* down = TAB ? dnl : A.down;
     const float* win = A.win ? (TAB ? wnl : A.win) : nullptr;
 
     const int slot = tid / G::LPS, lam = tid % G::LPS;
     const unsigned long long nsym = A.frames * A.total_syms;
     const unsigned long long tiles = (nsym + G::T - 1) / G::T;
-    const unsigned long long step = (unsigned long long)N * A.osr;
-    const unsigned long long dech_end = A.total_syms * N;  // whole symbols only
-    float2* sym = lds + slot * G::SSTRIDE;
+    const unsigned long long step = (unsigned long long)N;  // osr == 1 (lphy_hip_ctx_create)
+    const Stage<SF> stg(slot, lam);
 
     for (unsigned long long tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
         const unsigned long long gsym = tile * G::T + slot;
@@ -360,57 +360,56 @@ __global__ __launch_bounds__(kTile, (SF <= 8 ? 3 : 2)) void k_demod(DemodArgs A)
         const lphy_frame_meta m = A.meta[f];
         const bool ok = live && m.status == 0;
         const unsigned long long base = shifted_base(s, step, m.t_off, A.frame_samples);
-        const float2* src = A.iq + f * A.frame_samples + base;
-        const float start = m.rate * ((float)(s * N) + (float)m.t_off / (float)A.osr);
-        const bool norm = m.normalised != 0;
+        const cf32* src = A.iq + f * A.frame_samples + base;
+        const float start = m.rate * ((float)(s * N) + (float)m.t_off / 1.0f);  // osr == 1
 
         // all of the tile's IQ loads in flight at once (16 per lane)
-        float2 raw[16];
+        cf32 raw[16];
 #pragma unroll
-        for (int e = 0; e < G::E; ++e)
-            raw[e] = src[(unsigned long long)(lam + e * G::LPS) * A.osr];
+        for (int e = 0; e < G::E; ++e) raw[e] = src[lam + e * G::LPS];  // osr == 1
 
-        // one rotated input sample (LoRaDemod.cpp:152-163, phy.cpp:217-229)
-        auto sample = [&](float2 x, int i, bool large) -> float2 {
+        // one rotated input sample (LoRaDemod.cpp:152-163, phy.cpp:217-229).
+        // Dead lanes (past the batch / failed frames) compute on in-bounds
+        // data of frame 0 and never store a result.
+        auto sample = [&](cf32 x, int i, bool large) -> cf32 {
             if constexpr (MODE == LPHY_MODE_DEMODULATE) {
                 x = cmul(x, down[i]);  // phy.cpp:219-220: down-chirp of the window
             } else {
                 if constexpr (MODE == LPHY_MODE_DECHIRP_LORA_DEMODULATE) {
                     // the external dechirp ran on the unshifted buffer
-                    // (e2e_chain_test.cpp:88-93): chirp index of the absolute sample
-                    const unsigned long long j = base + (unsigned long long)i;
-                    const float2 d = cmul(x, down[j & (N - 1)]);
-                    x = j < dech_end ? d : make_float2(0.0f, 0.0f);
+                    // (e2e_chain_test.cpp:88-93): chirp index of the absolute
+                    // sample (frames hold whole symbols in this mode)
+                    x = cmul(x, down[((unsigned)base + (unsigned)i) & (N - 1)]);
                 }
-                if (norm) x = cscale(x, m.scale);
+                // LoRaDemod.cpp:74-76; scale == 1.0f exactly when no rescale was
+                // needed and x * 1.0f == x, so the multiply is unconditional
+                x = cscale(x, m.scale);
             }
             const float ph = start + m.rate * (float)i;
             float sn, cs;
             if (large) lphy_libm::sincosf_large(ph, &sn, &cs);
             else lphy_libm::sincosf_fast(ph, &sn, &cs);
-            x = cmul(x, make_float2(cs, sn));
+            x = cmul(x, cf32{cs, sn});
             if (win) x = cscale(x, win[i]);
-            return ok ? x : make_float2(0.0f, 0.0f);
+            return x;
         };
 
         __syncthreads();  // tables staged / previous tile's readers done
-        bool any_large = false;
 #pragma unroll
-        for (int e = 0; e < G::E; ++e) {
-            const int i = lam + e * G::LPS;
-            any_large |= lphy_libm::sincosf_needs_large(start + m.rate * (float)i);
-            sym[G::lds(i)] = sample(raw[e], i, false);
-        }
-        if (any_large) {  // rare: |phase| >= 120 rad (large CFO x long frame)
+        for (int e = 0; e < G::E; ++e) stg.put(lds, e, sample(raw[e], lam + e * G::LPS, false));
+        // rare: |phase| >= 120 rad (large CFO x long frame).  The angle is
+        // monotone in i, so the lane's first and last samples bound it.
+        if (lphy_libm::sincosf_needs_large(start + m.rate * (float)lam) ||
+            lphy_libm::sincosf_needs_large(start + m.rate * (float)(lam + (G::E - 1) * G::LPS))) {
             for (int e = 0; e < G::E; ++e) {
                 const int i = lam + e * G::LPS;
                 if (lphy_libm::sincosf_needs_large(start + m.rate * (float)i))
-                    sym[G::lds(i)] = sample(src[(unsigned long long)i * A.osr], i, true);
+                    stg.put(lds, e, sample(src[i], i, true));
             }
         }
         __syncthreads();
-        float2 v[16];
-        fft_tile<SF>(v, sym, lam, twl);
+        cf32 v[16];
+        fft_tile<SF>(v, lds, slot, lam, twl);
         const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), red);
         if (ok && lam == 0) {
             const uint16_t idx = (uint16_t)best.i;
@@ -513,7 +512,7 @@ __global__ void k_finalize(FinalArgs A) {
 // ---------------------------------------------------------------------------
 struct ModArgs {
     const uint16_t* syms;
-    float2* iq;
+    cf32* iq;
     float* phase0;           // frames * (nsyms + 2) phase at symbol start
     unsigned long long frames, nsyms;
     int N, osr;
@@ -569,34 +568,34 @@ __global__ void k_mod_samples(ModArgs A) {
     const int step = A.N * A.osr;
     float phase = A.phase0[g];
     float fr = fmin + mod_f0(A, f, s);
-    float2* out = A.iq + (f * ns + s) * (unsigned long long)step;
+    cf32* out = A.iq + (f * ns + s) * (unsigned long long)step;
     for (int i = 0; i < step; ++i) {
         fr += fstep;
         if (fr > fmax) fr -= (fmax - fmin);
         phase += fr;
         float sn, cs;
         lphy_libm::sincosf_exact(phase, &sn, &cs);
-        out[i] = make_float2(A.ampl * cs, A.ampl * sn);
+        out[i] = cf32{A.ampl * cs, A.ampl * sn};
     }
 }
 
 // compensate_offsets (phy.cpp:150-180): rotation then integer time shift.
-__global__ void k_comp_rotate(float2* out, const float2* in, unsigned long long count,
+__global__ void k_comp_rotate(cf32* out, const cf32* in, unsigned long long count,
                               float rate) {
     const unsigned long long n = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= count) return;
     const float ph = rate * (float)n;
     float sn, cs;
     lphy_libm::sincosf_exact(ph, &sn, &cs);
-    out[n] = cmul(in[n], make_float2(cs, sn));
+    out[n] = cmul(in[n], cf32{cs, sn});
 }
 
-__global__ void k_comp_shift(float2* out, const float2* in, unsigned long long count,
+__global__ void k_comp_shift(cf32* out, const cf32* in, unsigned long long count,
                              long long offset) {
     const unsigned long long n = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= count) return;
     const long long src = (long long)n - offset;
-    out[n] = (src >= 0 && src < (long long)count) ? in[src] : make_float2(0.0f, 0.0f);
+    out[n] = (src >= 0 && src < (long long)count) ? in[src] : czero();
 }
 
 }  // namespace
@@ -608,8 +607,8 @@ struct lphy_hip_ctx {
     int device = 0;
     unsigned sf = 0, N = 0, bw_hz = 0, osr = 1;
     int window = 0;
-    float2* d_tw = nullptr;
-    float2* d_down = nullptr;
+    cf32* d_tw = nullptr;
+    cf32* d_down = nullptr;
     float* d_win = nullptr;
     // staging for the host convenience entry points
     std::mutex mu;
@@ -662,24 +661,42 @@ void make_hann(std::vector<float>& w, int N) {
                                       (static_cast<float>(N) - 1.0f));
 }
 
-template <int SF, int MODE>
+// Waves per SIMD the demod kernel is register-budgeted for (launch bound):
+// 3 (<= 168 VGPRs) or 2 (<= 256).  LPHY_DEMOD_OCC overrides for experiments.
+inline int demod_occ(int sf) {
+    static int env = -1;
+    if (env < 0) {
+        const char* e = getenv("LPHY_DEMOD_OCC");
+        env = e ? atoi(e) : 0;
+    }
+    if (env == 2 || env == 3) return env;
+    return sf <= 8 ? 3 : 2;
+}
+
+template <int SF, int MODE, int OCC>
 int demod_grid() {
     static int grid = 0;
     if (grid == 0) {
         int dev = 0, cus = 0, per = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_demod<SF, MODE>, kTile, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_demod<SF, MODE, OCC>, kTile, 0);
         grid = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
     }
     return grid;
 }
 
+template <int SF, int MODE, int OCC>
+void launch_symbols_occ(const DemodArgs& A, unsigned long long tiles, hipStream_t st) {
+    const unsigned long long g = (unsigned long long)demod_grid<SF, MODE, OCC>();
+    const unsigned long long grid = tiles < g ? tiles : g;
+    hipLaunchKernelGGL((k_demod<SF, MODE, OCC>), dim3((unsigned)grid), dim3(kTile), 0, st, A);
+}
+
 template <int SF, int MODE>
 void launch_symbols(const DemodArgs& A, unsigned long long tiles, hipStream_t st) {
-    const unsigned long long g = (unsigned long long)demod_grid<SF, MODE>();
-    const unsigned long long grid = tiles < g ? tiles : g;
-    hipLaunchKernelGGL((k_demod<SF, MODE>), dim3((unsigned)grid), dim3(kTile), 0, st, A);
+    if (demod_occ(SF) == 3) launch_symbols_occ<SF, MODE, 3>(A, tiles, st);
+    else launch_symbols_occ<SF, MODE, 2>(A, tiles, st);
 }
 
 template <int SF>
@@ -765,13 +782,13 @@ int lphy_hip_ctx_create(lphy_hip_ctx** out, int device, unsigned sf, unsigned bw
     std::vector<std::complex<float>> tw, down;
     make_twiddles(tw, (int)c->N);
     make_downchirp(down, (int)c->N, (float)bw_hz / 125000.0f);
-    if (hipMalloc(&c->d_tw, c->N * sizeof(float2)) != hipSuccess ||
-        hipMalloc(&c->d_down, c->N * sizeof(float2)) != hipSuccess) {
+    if (hipMalloc(&c->d_tw, c->N * sizeof(cf32)) != hipSuccess ||
+        hipMalloc(&c->d_down, c->N * sizeof(cf32)) != hipSuccess) {
         lphy_hip_ctx_destroy(c);
         return -ENOMEM;
     }
-    HIP_OK(hipMemcpy(c->d_tw, tw.data(), c->N * sizeof(float2), hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(c->d_down, down.data(), c->N * sizeof(float2), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(c->d_tw, tw.data(), c->N * sizeof(cf32), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(c->d_down, down.data(), c->N * sizeof(cf32), hipMemcpyHostToDevice));
     if (window == LPHY_WINDOW_HANN) {
         std::vector<float> w;
         make_hann(w, (int)c->N);
@@ -816,11 +833,11 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
         if (frame_samples % step != 0) return -EINVAL;
         if (total < 2) return -ERANGE;
     }
-    if (mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE && c->osr != 1) return -EINVAL;
+    if (mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE && (c->osr != 1 || frame_samples % c->N)) return -EINVAL;
     HIP_OK(hipSetDevice(c->device));
     hipStream_t st = (hipStream_t)stream;
     DemodArgs A{};
-    A.iq = reinterpret_cast<const float2*>(d_iq);
+    A.iq = reinterpret_cast<const cf32*>(d_iq);
     A.tw = c->d_tw;
     A.down = c->d_down;
     A.win = c->window == LPHY_WINDOW_HANN ? c->d_win : nullptr;
@@ -890,7 +907,7 @@ int lphy_hip_estimate_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     if (syms * c->osr > 0x7fffffffULL) return -ERANGE;
     HIP_OK(hipSetDevice(c->device));
     DemodArgs A{};
-    A.iq = reinterpret_cast<const float2*>(d_iq);
+    A.iq = reinterpret_cast<const cf32*>(d_iq);
     A.tw = c->d_tw;
     A.down = c->d_down;
     A.win = c->window == LPHY_WINDOW_HANN ? c->d_win : nullptr;
@@ -924,17 +941,17 @@ int lphy_hip_compensate(lphy_hip_ctx* c, float* d_iq, size_t count, float cfo,
     hipStream_t st = (hipStream_t)stream;
     // phy.cpp:159-160
     const float rate = -2.0f * kPi * cfo / (static_cast<float>(c->N) * static_cast<float>(c->osr));
-    float2* tmp = nullptr;
-    HIP_OK(hipMallocAsync((void**)&tmp, count * sizeof(float2), st));
+    cf32* tmp = nullptr;
+    HIP_OK(hipMallocAsync((void**)&tmp, count * sizeof(cf32), st));
     const unsigned blocks = (unsigned)((count + 255) / 256);
-    float2* x = reinterpret_cast<float2*>(d_iq);
+    cf32* x = reinterpret_cast<cf32*>(d_iq);
     hipLaunchKernelGGL(k_comp_rotate, dim3(blocks), dim3(256), 0, st, tmp, x, (unsigned long long)count, rate);
     const float r = std::round(time_offset);
     long long off = (r >= -2147483648.0f && r < 2147483648.0f) ? (long long)(int)r : (long long)(int)0x80000000u;
     if (off != 0 && (unsigned long long)(off > 0 ? off : -off) < count) {
         hipLaunchKernelGGL(k_comp_shift, dim3(blocks), dim3(256), 0, st, x, tmp, (unsigned long long)count, off);
     } else {
-        HIP_OK(hipMemcpyAsync(x, tmp, count * sizeof(float2), hipMemcpyDeviceToDevice, st));
+        HIP_OK(hipMemcpyAsync(x, tmp, count * sizeof(cf32), hipMemcpyDeviceToDevice, st));
     }
     HIP_OK(hipFreeAsync(tmp, st));
     HIP_OK(hipGetLastError());
@@ -950,7 +967,7 @@ int lphy_hip_modulate_batch(lphy_hip_ctx* c, const uint16_t* d_syms, size_t fram
     hipStream_t st = (hipStream_t)stream;
     ModArgs A{};
     A.syms = d_syms;
-    A.iq = reinterpret_cast<float2*>(d_iq);
+    A.iq = reinterpret_cast<cf32*>(d_iq);
     A.frames = frames;
     A.nsyms = nsyms;
     A.N = (int)c->N;
@@ -980,7 +997,7 @@ int lphy_hip_demod_host(lphy_hip_ctx* c, const float* h_iq, size_t frames,
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_OK(hipSetDevice(c->device));
     const size_t per = lphy_hip_syms_per_frame(c, frame_samples, mode);
-    const size_t iq_b = align_up(frames * frame_samples * sizeof(float2));
+    const size_t iq_b = align_up(frames * frame_samples * sizeof(cf32));
     const size_t sym_b = align_up(std::max<size_t>(1, frames * per) * sizeof(uint16_t));
     const size_t byte_b = align_up(std::max<size_t>(1, frames * (per / 2)));
     const size_t meta_b = align_up(frames * sizeof(lphy_frame_meta));
@@ -991,7 +1008,7 @@ int lphy_hip_demod_host(lphy_hip_ctx* c, const float* h_iq, size_t frames,
     uint16_t* d_syms = (uint16_t*)(base + iq_b);
     uint8_t* d_bytes = (uint8_t*)(base + iq_b + sym_b);
     lphy_frame_meta* d_meta = (lphy_frame_meta*)(base + iq_b + sym_b + byte_b);
-    HIP_OK(hipMemcpy(d_iq, h_iq, frames * frame_samples * sizeof(float2), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_iq, h_iq, frames * frame_samples * sizeof(cf32), hipMemcpyHostToDevice));
     HIP_OK(hipMemset(d_meta, 0, frames * sizeof(lphy_frame_meta)));
     rc = lphy_hip_demod_batch(c, d_iq, frames, frame_samples, d_syms,
                               (flags & LPHY_F_DECODE) ? d_bytes : nullptr, d_meta, mode, flags,
@@ -1036,14 +1053,14 @@ int lphy_hip_estimate_host(lphy_hip_ctx* c, const float* h_iq, size_t count,
     if (!c || !h_iq || !h_meta) return -EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_OK(hipSetDevice(c->device));
-    const size_t iq_b = align_up(std::max<size_t>(1, count) * sizeof(float2));
+    const size_t iq_b = align_up(std::max<size_t>(1, count) * sizeof(cf32));
     const size_t meta_b = align_up(sizeof(lphy_frame_meta));
     int rc = ensure_stage(c, iq_b + meta_b);
     if (rc) return rc;
     char* base = (char*)c->d_stage;
     float* d_iq = (float*)base;
     lphy_frame_meta* d_meta = (lphy_frame_meta*)(base + iq_b);
-    HIP_OK(hipMemcpy(d_iq, h_iq, count * sizeof(float2), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_iq, h_iq, count * sizeof(cf32), hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(d_meta, h_meta, sizeof(lphy_frame_meta), hipMemcpyHostToDevice));
     rc = lphy_hip_estimate_batch(c, d_iq, 1, count, count, d_meta, nullptr);
     if (rc) return rc;
@@ -1058,14 +1075,14 @@ int lphy_hip_compensate_host(lphy_hip_ctx* c, float* h_iq, size_t count, float c
     if (count == 0) return 0;
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_OK(hipSetDevice(c->device));
-    int rc = ensure_stage(c, align_up(count * sizeof(float2)));
+    int rc = ensure_stage(c, align_up(count * sizeof(cf32)));
     if (rc) return rc;
     float* d = (float*)c->d_stage;
-    HIP_OK(hipMemcpy(d, h_iq, count * sizeof(float2), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d, h_iq, count * sizeof(cf32), hipMemcpyHostToDevice));
     rc = lphy_hip_compensate(c, d, count, cfo, time_offset, nullptr);
     if (rc) return rc;
     HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(h_iq, d, count * sizeof(float2), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(h_iq, d, count * sizeof(cf32), hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -1076,7 +1093,7 @@ int lphy_hip_modulate_host(lphy_hip_ctx* c, const uint16_t* h_syms, size_t nsyms
     HIP_OK(hipSetDevice(c->device));
     const size_t samples = (nsyms + 2) * (size_t)c->N * c->osr;
     const size_t sym_b = align_up(std::max<size_t>(1, nsyms) * sizeof(uint16_t));
-    int rc = ensure_stage(c, sym_b + align_up(samples * sizeof(float2)));
+    int rc = ensure_stage(c, sym_b + align_up(samples * sizeof(cf32)));
     if (rc) return rc;
     char* base = (char*)c->d_stage;
     uint16_t* d_syms = (uint16_t*)base;
@@ -1085,7 +1102,7 @@ int lphy_hip_modulate_host(lphy_hip_ctx* c, const uint16_t* h_syms, size_t nsyms
     rc = lphy_hip_modulate_batch(c, d_syms, 1, nsyms, d_iq, amplitude, sync, nullptr);
     if (rc) return rc;
     HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(h_iq, d_iq, samples * sizeof(float2), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(h_iq, d_iq, samples * sizeof(cf32), hipMemcpyDeviceToHost));
     return 0;
 }
 
