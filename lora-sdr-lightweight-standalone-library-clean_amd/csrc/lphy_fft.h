@@ -159,6 +159,21 @@ struct PassGeo {
     }
 };
 
+// Synchronisation of the lanes that share a symbol ("team" of LPS lanes).
+// Up to LPS = 64 a team lives inside one wavefront: its LDS exchanges only
+// need this wave's LDS operations drained and no compiler motion across the
+// point (a wave's LDS instructions execute in order).  Larger teams span
+// wavefronts and need the workgroup barrier.
+template <int SF>
+__device__ __forceinline__ void team_sync() {
+    if constexpr (Geo<SF>::LPS <= 64) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+    } else {
+        __syncthreads();
+    }
+}
+
 // Base-4 digit reversal of `high` over `ndig` digits (leaf permutation of the
 // digits that precede the first pass).
 __host__ __device__ constexpr int rev4(int high, int ndig) {
@@ -254,7 +269,7 @@ __device__ __forceinline__ void run_pass(cf32 (&v)[16], cf32* lds, int slot, int
         const int lb8 = G::lbase(slot, Gr::inidx(0, lam)) << 3;
 #pragma unroll
         for (int e = 0; e < G::E; ++e) v[e] = lds_ld(lds, G::at8(lb8, G::cpart(Gr::inidx(e, 0)) << 3));
-        __syncthreads();
+        team_sync<SF>();
     } else {
         const int lb8 = G::lbase(slot, Gr::pos(0, lam)) << 3;
 #pragma unroll
@@ -265,7 +280,7 @@ __device__ __forceinline__ void run_pass(cf32 (&v)[16], cf32* lds, int slot, int
         const int lb8 = G::lbase(slot, Gr::pos(0, lam)) << 3;
 #pragma unroll
         for (int e = 0; e < G::E; ++e) lds_st(lds, G::at8(lb8, G::cpart(Gr::pos(e, 0)) << 3), v[e]);
-        __syncthreads();
+        team_sync<SF>();
     }
 }
 

@@ -61,6 +61,9 @@ struct DemodArgs {
     int mode;
     int no_scratch;
     int est_units;           // estimate units per frame (est_syms * osr)
+    // persistent demod workers: symbol stride per step split into whole
+    // frames + symbols (host-computed, so the kernel never divides)
+    unsigned stride_f, stride_s;
 };
 
 // (int)std::round(x) as the x86-64 reference evaluates it: cvttss2si on the
@@ -324,11 +327,120 @@ __global__ __launch_bounds__(kTile) void k_estimate(DemodArgs A) {
 // workgroup stages the twiddles (and, up to N = 1024, the down-chirp and the
 // window) in LDS once, then loops over tiles of T symbols.
 // ---------------------------------------------------------------------------
+// Per-tile context of the symbol a team (LPS lanes) works on.  Frame and
+// symbol indices are 32-bit (lphy_hip_demod_batch checks frames*symbols and
+// frame_samples fit) and advance incrementally: no division per tile.
+struct SymCtx {
+    unsigned f, s;            // frame, symbol within the frame
+    unsigned base;            // first sample of the (shifted) window in the frame
+    float start, rate, scale;
+    bool ok, have_sync;
+};
+
+__device__ __forceinline__ SymCtx sym_ctx(const DemodArgs& A, unsigned f, unsigned s, bool live,
+                                          int N, const lphy_frame_meta& m) {
+    SymCtx c;
+    c.f = f;
+    c.s = s;
+    c.ok = live && m.status == 0;
+    c.have_sync = m.have_sync != 0;
+    // LoRaDemod.cpp:144-151 with osr == 1, in 32 bits
+    const unsigned step = (unsigned)N, count = (unsigned)A.frame_samples;
+    unsigned base = s * step;
+    const int t = m.t_off;
+    if (t > 0) {
+        if ((unsigned long long)base + (unsigned)t + step <= count) base += (unsigned)t;
+    } else if (t < 0) {
+        const unsigned long long off = (t == (int)0x80000000u) ? (unsigned long long)(long long)t
+                                                               : (unsigned long long)(-(long long)t);
+        if (off <= base) base -= (unsigned)off;
+    }
+    c.base = base;
+    c.rate = m.rate;
+    c.scale = m.scale;
+    // LoRaDemod.cpp:152-153 / phy.cpp:217-218 with osr == 1; (float) of the
+    // size_t product equals (float) of the same value held in 32 bits
+    c.start = m.rate * ((float)(s * step) + (float)m.t_off / 1.0f);
+    return c;
+}
+
+// One rotated input sample (LoRaDemod.cpp:152-163, phy.cpp:217-229).
+template <int SF, int MODE>
+__device__ __forceinline__ cf32 rotate_sample(cf32 x, int i, const SymCtx& c,
+                                              const cf32* down, const float* win, bool large) {
+    constexpr int N = 1 << SF;
+    if constexpr (MODE == LPHY_MODE_DEMODULATE) {
+        x = cmul(x, down[i]);  // phy.cpp:219-220: down-chirp of the window
+    } else {
+        if constexpr (MODE == LPHY_MODE_DECHIRP_LORA_DEMODULATE) {
+            // the external dechirp ran on the unshifted buffer
+            // (e2e_chain_test.cpp:88-93): chirp index of the absolute sample
+            // (frames hold whole symbols in this mode)
+            x = cmul(x, down[((unsigned)c.base + (unsigned)i) & (N - 1)]);
+        }
+        // LoRaDemod.cpp:74-76; scale == 1.0f exactly when no rescale was
+        // needed and x * 1.0f == x, so the multiply is unconditional
+        x = cscale(x, c.scale);
+    }
+    const float ph = c.start + c.rate * (float)i;
+    float sn, cs;
+#ifdef LPHY_ABLATE_SINCOS  // timing experiments only (tools/ubench/demod_ablate)
+    sn = ph; cs = 1.0f - ph;
+    (void)large;
+#else
+    if (large) lphy_libm::sincosf_large(ph, &sn, &cs);
+    else lphy_libm::sincosf_fast(ph, &sn, &cs);
+#endif
+    x = cmul(x, cf32{cs, sn});
+    if (win) x = cscale(x, win[i]);
+    return x;
+}
+
+// Stage the team's symbol (rotated, natural order) into its LDS slot.
+template <int SF, int MODE>
+__device__ __forceinline__ void stage_symbol(cf32* lds, const Stage<SF>& stg, const cf32 (&raw)[16],
+                                             const cf32* src, const SymCtx& c, int lam,
+                                             const cf32* down, const float* win) {
+    using G = Geo<SF>;
+#pragma unroll
+    for (int e = 0; e < G::E; ++e)
+        stg.put(lds, e, rotate_sample<SF, MODE>(raw[e], lam + e * G::LPS, c, down, win, false));
+    // rare: |phase| >= 120 rad (large CFO x long frame).  The angle is
+    // monotone in i, so the lane's first and last samples bound it.
+    if (lphy_libm::sincosf_needs_large(c.start + c.rate * (float)lam) ||
+        lphy_libm::sincosf_needs_large(c.start + c.rate * (float)(lam + (G::E - 1) * G::LPS))) {
+        for (int e = 0; e < G::E; ++e) {
+            const int i = lam + e * G::LPS;
+            if (lphy_libm::sincosf_needs_large(c.start + c.rate * (float)i))
+                stg.put(lds, e, rotate_sample<SF, MODE>(src[i], i, c, down, win, true));
+        }
+    }
+}
+
+__device__ __forceinline__ void store_symbol(const DemodArgs& A, const SymCtx& c, uint16_t idx) {
+    if (c.have_sync && c.s < 2) {
+        if (c.s == 0) A.meta[c.f].sw0 = idx;
+        else A.meta[c.f].sw1 = idx;
+    } else {
+        const unsigned o = c.have_sync ? c.s - 2 : c.s;
+        A.syms[(unsigned long long)c.f * A.out_per_frame + o] = idx;
+    }
+}
+
+// Stage 2: per-symbol demodulation, persistent grid.  The workgroup stages
+// the twiddles (and, up to N = 1024, the down-chirp and window) in LDS once.
+//  * SF <= 10 (a symbol's LPS <= 64 lanes sit in one wavefront): every
+//    wavefront is an independent worker with its own LDS slots and no
+//    workgroup barrier in its loop; it software-pipelines the next tile's
+//    frame record (during staging) and IQ (during the FFT).
+//  * SF 11-12: workgroup tiles with barriers (a symbol spans wavefronts).
 template <int SF, int MODE, int OCC>
 __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
     using G = Geo<SF>;
     constexpr int N = G::N;
     constexpr bool TAB = N <= 1024;  // chirp + window tables in LDS
+    constexpr bool WAVE = G::LPS <= 64;
+    constexpr int WT = WAVE ? 64 / G::LPS : G::T;  // symbols per worker tile
     __shared__ cf32 lds[G::T * G::SSTRIDE];
     __shared__ cf32 twl[N];
     __shared__ cf32 dnl[TAB ? N : 1];
@@ -343,84 +455,83 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
             if (A.win) wnl[i] = A.win[i];
         }
     }
+    __syncthreads();
     const cf32* down = TAB ? dnl : A.down;
     const float* win = A.win ? (TAB ? wnl : A.win) : nullptr;
 
     const int slot = tid / G::LPS, lam = tid % G::LPS;
-    const unsigned long long nsym = A.frames * A.total_syms;
-    const unsigned long long tiles = (nsym + G::T - 1) / G::T;
-    const unsigned long long step = (unsigned long long)N;  // osr == 1 (lphy_hip_ctx_create)
+    const unsigned S = (unsigned)A.total_syms;
+    const unsigned nframes = (unsigned)A.frames;
+    const int wslot = WAVE ? slot % WT : slot;  // symbol slot inside the worker tile
+    unsigned worker;
+    if constexpr (WAVE) worker = blockIdx.x * (kTile / 64) + (tid >> 6);
+    else worker = blockIdx.x;
     const Stage<SF> stg(slot, lam);
 
-    for (unsigned long long tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-        const unsigned long long gsym = tile * G::T + slot;
-        const bool live = gsym < nsym;
-        const unsigned long long f = live ? gsym / A.total_syms : 0;
-        const unsigned long long s = live ? gsym - f * A.total_syms : 0;
-        const lphy_frame_meta m = A.meta[f];
-        const bool ok = live && m.status == 0;
-        const unsigned long long base = shifted_base(s, step, m.t_off, A.frame_samples);
-        const cf32* src = A.iq + f * A.frame_samples + base;
-        const float start = m.rate * ((float)(s * N) + (float)m.t_off / 1.0f);  // osr == 1
+    // this team's first symbol and its (frame, symbol) coordinates
+    const unsigned g0 = worker * WT + wslot;
+    unsigned f = g0 / S, s = g0 - f * S;
+    auto step = [&](unsigned& ff, unsigned& ss) {
+        ss += A.stride_s;
+        ff += A.stride_f;
+        if (ss >= S) { ss -= S; ++ff; }
+    };
+    // the worker's tile loop ends when its first team passes the last frame
+    const unsigned fw0 = (worker * WT) / S;
+    unsigned fw = fw0, sw = worker * WT - fw0 * S;
 
-        // all of the tile's IQ loads in flight at once (16 per lane)
-        cf32 raw[16];
+    // prologue of the software pipeline
+    lphy_frame_meta m = A.meta[f < nframes ? f : 0];
+    SymCtx c = sym_ctx(A, f < nframes ? f : 0, f < nframes ? s : 0, f < nframes, N, m);
+    cf32 raw[16];
+    {
+        const cf32* src = A.iq + (unsigned long long)c.f * A.frame_samples + c.base;
 #pragma unroll
-        for (int e = 0; e < G::E; ++e) raw[e] = src[lam + e * G::LPS];  // osr == 1
+        for (int e = 0; e < G::E; ++e) raw[e] = src[lam + e * G::LPS];
+    }
 
-        // one rotated input sample (LoRaDemod.cpp:152-163, phy.cpp:217-229).
-        // Dead lanes (past the batch / failed frames) compute on in-bounds
-        // data of frame 0 and never store a result.
-        auto sample = [&](cf32 x, int i, bool large) -> cf32 {
-            if constexpr (MODE == LPHY_MODE_DEMODULATE) {
-                x = cmul(x, down[i]);  // phy.cpp:219-220: down-chirp of the window
-            } else {
-                if constexpr (MODE == LPHY_MODE_DECHIRP_LORA_DEMODULATE) {
-                    // the external dechirp ran on the unshifted buffer
-                    // (e2e_chain_test.cpp:88-93): chirp index of the absolute
-                    // sample (frames hold whole symbols in this mode)
-                    x = cmul(x, down[((unsigned)base + (unsigned)i) & (N - 1)]);
-                }
-                // LoRaDemod.cpp:74-76; scale == 1.0f exactly when no rescale was
-                // needed and x * 1.0f == x, so the multiply is unconditional
-                x = cscale(x, m.scale);
-            }
-            const float ph = start + m.rate * (float)i;
-            float sn, cs;
-            if (large) lphy_libm::sincosf_large(ph, &sn, &cs);
-            else lphy_libm::sincosf_fast(ph, &sn, &cs);
-            x = cmul(x, cf32{cs, sn});
-            if (win) x = cscale(x, win[i]);
-            return x;
-        };
+    while (fw < nframes) {
+        // next tile: coordinates and frame record (in flight during staging)
+        unsigned nf = f, ns = s, nfw = fw, nsw = sw;
+        step(nf, ns);
+        step(nfw, nsw);
+        const bool nlive = nf < nframes;
+        const lphy_frame_meta nm = A.meta[nlive ? nf : 0];
 
-        __syncthreads();  // tables staged / previous tile's readers done
+        if constexpr (!WAVE) __syncthreads();  // previous tile's readers done
+        stage_symbol<SF, MODE>(lds, stg, raw, A.iq + (unsigned long long)c.f * A.frame_samples + c.base,
+                               c, lam, down, win);
+        team_sync<SF>();
+
+        // next tile's IQ: in flight during this tile's FFT
+        const SymCtx nc = sym_ctx(A, nlive ? nf : 0, nlive ? ns : 0, nlive, N, nm);
+        if (nfw < nframes) {
+            const cf32* nsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base;
+#ifdef LPHY_ABLATE_LOAD  // timing experiments only
+            (void)nsrc;
 #pragma unroll
-        for (int e = 0; e < G::E; ++e) stg.put(lds, e, sample(raw[e], lam + e * G::LPS, false));
-        // rare: |phase| >= 120 rad (large CFO x long frame).  The angle is
-        // monotone in i, so the lane's first and last samples bound it.
-        if (lphy_libm::sincosf_needs_large(start + m.rate * (float)lam) ||
-            lphy_libm::sincosf_needs_large(start + m.rate * (float)(lam + (G::E - 1) * G::LPS))) {
-            for (int e = 0; e < G::E; ++e) {
-                const int i = lam + e * G::LPS;
-                if (lphy_libm::sincosf_needs_large(start + m.rate * (float)i))
-                    stg.put(lds, e, sample(src[i], i, true));
-            }
+            for (int e = 0; e < G::E; ++e) raw[e] = raw[e] * 0.999f + cf32{(float)e, (float)lam};
+#else
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) raw[e] = nsrc[lam + e * G::LPS];
+#endif
         }
-        __syncthreads();
+
         cf32 v[16];
-        fft_tile<SF>(v, lds, slot, lam, twl);
-        const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), red);
-        if (ok && lam == 0) {
-            const uint16_t idx = (uint16_t)best.i;
-            if (m.have_sync && s < 2) {
-                if (s == 0) A.meta[f].sw0 = idx;
-                else A.meta[f].sw1 = idx;
-            } else {
-                const unsigned long long o = m.have_sync ? s - 2 : s;
-                A.syms[f * A.out_per_frame + o] = idx;
-            }
+#ifdef LPHY_ABLATE_FFT  // timing experiments only
+        {
+            const Stage<SF> st2(slot, lam);
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) v[e] = lds_ld(lds, G::at8(st2.lb8, G::cpart(e * G::LPS) << 3));
         }
+#else
+        fft_tile<SF>(v, lds, slot, lam, twl);
+#endif
+        const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), red);
+        if (c.ok && lam == 0) store_symbol(A, c, (uint16_t)best.i);
+        if constexpr (WAVE) team_sync<SF>();  // slot reads done before restaging
+        c = nc;
+        f = nf; s = ns; fw = nfw; sw = nsw;
     }
 }
 
@@ -614,6 +725,10 @@ struct lphy_hip_ctx {
     std::mutex mu;
     void* d_stage = nullptr;
     size_t stage_bytes = 0;
+    // device scratch of the producer / compensation kernels (grown on demand
+    // with a synchronous hipMalloc; never on the demodulation path)
+    void* d_scratch = nullptr;
+    size_t scratch_bytes = 0;
 };
 
 namespace {
@@ -687,16 +802,32 @@ int demod_grid() {
 }
 
 template <int SF, int MODE, int OCC>
-void launch_symbols_occ(const DemodArgs& A, unsigned long long tiles, hipStream_t st) {
+void launch_symbols_occ(const DemodArgs& A0, unsigned long long tiles, hipStream_t st) {
+    using G = Geo<SF>;
+    constexpr bool WAVE = G::LPS <= 64;
+    constexpr int WT = WAVE ? 64 / G::LPS : G::T;      // symbols per worker tile
+    constexpr int WPB = WAVE ? kTile / 64 : 1;         // workers per workgroup
     const unsigned long long g = (unsigned long long)demod_grid<SF, MODE, OCC>();
-    const unsigned long long grid = tiles < g ? tiles : g;
+    const unsigned long long wtiles = (A0.frames * A0.total_syms + WT - 1) / WT;
+    unsigned long long grid = (wtiles + WPB - 1) / WPB;
+    if (grid > g) grid = g;
+    DemodArgs A = A0;
+    const unsigned long long stride = grid * WPB * WT;  // symbols per worker step
+    A.stride_f = (unsigned)(stride / A0.total_syms);
+    A.stride_s = (unsigned)(stride % A0.total_syms);
+    (void)tiles;
     hipLaunchKernelGGL((k_demod<SF, MODE, OCC>), dim3((unsigned)grid), dim3(kTile), 0, st, A);
 }
 
 template <int SF, int MODE>
 void launch_symbols(const DemodArgs& A, unsigned long long tiles, hipStream_t st) {
-    if (demod_occ(SF) == 3) launch_symbols_occ<SF, MODE, 3>(A, tiles, st);
-    else launch_symbols_occ<SF, MODE, 2>(A, tiles, st);
+    if constexpr (SF <= 10) {
+        if (demod_occ(SF) == 3) {
+            launch_symbols_occ<SF, MODE, 3>(A, tiles, st);
+            return;
+        }
+    }
+    launch_symbols_occ<SF, MODE, 2>(A, tiles, st);
 }
 
 template <int SF>
@@ -754,6 +885,17 @@ int ensure_stage(lphy_hip_ctx* c, size_t bytes) {
 
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
+int ensure_scratch(lphy_hip_ctx* c, size_t bytes, hipStream_t st) {
+    if (c->scratch_bytes >= bytes) return 0;
+    HIP_OK(hipStreamSynchronize(st));  // previous users of the old buffer
+    if (c->d_scratch) (void)hipFree(c->d_scratch);
+    c->d_scratch = nullptr;
+    c->scratch_bytes = 0;
+    HIP_OK(hipMalloc(&c->d_scratch, bytes));
+    c->scratch_bytes = bytes;
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -809,6 +951,7 @@ void lphy_hip_ctx_destroy(lphy_hip_ctx* c) {
     if (c->d_down) (void)hipFree(c->d_down);
     if (c->d_win) (void)hipFree(c->d_win);
     if (c->d_stage) (void)hipFree(c->d_stage);
+    if (c->d_scratch) (void)hipFree(c->d_scratch);
     delete c;
 }
 
@@ -852,7 +995,10 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     A.no_scratch = (flags & LPHY_F_NO_SCRATCH) ? 1 : 0;
     const size_t est_syms = mode == LPHY_MODE_DEMODULATE ? 2 : (total < 2 ? total : 2);
     A.est_units = (int)(est_syms * c->osr);
-    if (frames > 0x7fffffffULL) return -ERANGE;
+    // 32-bit symbol / sample bookkeeping in the kernels
+    if (frames > 0x7fffffffULL || frames * (total ? total : 1) >= 0xffffffffULL ||
+        frame_samples >= 0x7fffffffULL)
+        return -ERANGE;
     const unsigned stages = flags & (LPHY_F_STAGE_PROLOGUE | LPHY_F_STAGE_SYMBOLS | LPHY_F_STAGE_FINAL);
     const bool all = stages == 0;
     int rc = launch_demod(c->sf, A, st, all || (stages & LPHY_F_STAGE_PROLOGUE),
@@ -941,8 +1087,9 @@ int lphy_hip_compensate(lphy_hip_ctx* c, float* d_iq, size_t count, float cfo,
     hipStream_t st = (hipStream_t)stream;
     // phy.cpp:159-160
     const float rate = -2.0f * kPi * cfo / (static_cast<float>(c->N) * static_cast<float>(c->osr));
-    cf32* tmp = nullptr;
-    HIP_OK(hipMallocAsync((void**)&tmp, count * sizeof(cf32), st));
+    int rc = ensure_scratch(c, count * sizeof(cf32), st);
+    if (rc) return rc;
+    cf32* tmp = static_cast<cf32*>(c->d_scratch);
     const unsigned blocks = (unsigned)((count + 255) / 256);
     cf32* x = reinterpret_cast<cf32*>(d_iq);
     hipLaunchKernelGGL(k_comp_rotate, dim3(blocks), dim3(256), 0, st, tmp, x, (unsigned long long)count, rate);
@@ -953,7 +1100,6 @@ int lphy_hip_compensate(lphy_hip_ctx* c, float* d_iq, size_t count, float cfo,
     } else {
         HIP_OK(hipMemcpyAsync(x, tmp, count * sizeof(cf32), hipMemcpyDeviceToDevice, st));
     }
-    HIP_OK(hipFreeAsync(tmp, st));
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -976,10 +1122,11 @@ int lphy_hip_modulate_batch(lphy_hip_ctx* c, const uint16_t* d_syms, size_t fram
     A.ampl = std::max(-1.0f, std::min(1.0f, amplitude));  // LoRaMod.cpp:18
     A.sync = sync;
     const size_t nph = frames * (nsyms + 2);
-    HIP_OK(hipMallocAsync((void**)&A.phase0, nph * sizeof(float), st));
+    int rc = ensure_scratch(c, nph * sizeof(float), st);
+    if (rc) return rc;
+    A.phase0 = static_cast<float*>(c->d_scratch);
     hipLaunchKernelGGL(k_mod_phase, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, A);
     hipLaunchKernelGGL(k_mod_samples, dim3((unsigned)((nph + 63) / 64)), dim3(64), 0, st, A);
-    HIP_OK(hipFreeAsync(A.phase0, st));
     HIP_OK(hipGetLastError());
     return 0;
 }

@@ -100,6 +100,19 @@ def test_modulate_bit_exact(oracle, lphy):
         np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
+def test_modulate_repeated_contexts(oracle, lphy):
+    """Stress: many producer calls with fresh contexts and varying sizes
+    (guards the phase-scratch hand-off between the two modulate kernels)."""
+    rng = np.random.default_rng(11)
+    for k in range(24):
+        sf = int(rng.integers(2, 10))
+        bw = [125000, 250000, 500000][k % 3]
+        syms = rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint16)
+        a = lphy.Demodulator(sf, bw).modulate_host(syms, 1.0, 0x12)
+        b = oracle.modulate(syms, sf, bw_hz=bw)
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32), err_msg=f"iter {k}")
+
+
 def test_zero_and_overrange_frames(oracle, lphy):
     sf, N = 7, 128
     d = lphy.Demodulator(sf)
