@@ -80,7 +80,10 @@ enum lphy_flags {
      * only the selected stages are launched; none set = all three. */
     LPHY_F_STAGE_PROLOGUE = 4u,  /* per-frame max-abs + offset estimate   */
     LPHY_F_STAGE_SYMBOLS = 8u,   /* per-symbol rotate + FFT + argmax      */
-    LPHY_F_STAGE_FINAL = 16u     /* per-frame sync word, decode, CRC      */
+    LPHY_F_STAGE_FINAL = 16u,    /* per-frame sync word, decode, CRC      */
+    LPHY_F_UNFUSED = 32u         /* separate prologue / symbol launches
+                                    instead of the fused single launch
+                                    (same results; for comparison)       */
 };
 
 enum lphy_window { LPHY_WINDOW_NONE = 0, LPHY_WINDOW_HANN = 1 };

@@ -74,22 +74,6 @@ __device__ __forceinline__ int round_to_int(float x) {
     return (int)r;
 }
 
-// Symbol base offset after the timing shift (LoRaDemod.cpp:144-151).
-__device__ __forceinline__ unsigned long long shifted_base(unsigned long long s,
-                                                           unsigned long long step, int t_off,
-                                                           unsigned long long count) {
-    unsigned long long base = s * step;
-    if (t_off > 0) {
-        if (base + (unsigned long long)t_off + step <= count) base += (unsigned long long)t_off;
-    } else if (t_off < 0) {
-        unsigned long long off = (t_off == (int)0x80000000u)
-                                     ? (unsigned long long)(long long)t_off
-                                     : (unsigned long long)(-(long long)t_off);
-        if (off <= base) base -= off;
-    }
-    return base;
-}
-
 // Input sample for the estimate (no rotation): raw (mode 0) or
 // [dechirped,] [normalised] (modes 1, 2).  idx is the absolute sample index
 // in the frame, i the index inside the symbol (window / mode-0 chirp).
@@ -103,6 +87,28 @@ __device__ __forceinline__ cf32 est_sample(const DemodArgs& A, const cf32* fr,
     if (A.mode != LPHY_MODE_DEMODULATE && m.normalised) x = cscale(x, m.scale);
     if (A.win) x = cscale(x, A.win[i]);
     return x;
+}
+
+// max(|I|,|Q|) accumulation of LoRaDemod.cpp:62-66 for one sample:
+// std::max(r, im) keeps r when im is NaN and yields NaN (never > mx) when r
+// is NaN, so a NaN real part hides the whole sample.
+__device__ __forceinline__ void maxabs_acc(float& mx, cf32 x) {
+    const float r = fabsf(x.x), im = fabsf(x.y);
+    const float m = (r < im) ? im : r;
+    if (m > mx) mx = m;
+}
+
+// Normalisation decision of LoRaDemod.cpp:60-78 from the frame's max-abs.
+__device__ __forceinline__ lphy_frame_meta norm_meta(float mx, bool have_sync, int no_scratch) {
+    lphy_frame_meta m{};
+    m.scale = 1.0f;
+    m.have_sync = have_sync;
+    if (mx > 1.0f) {
+        if (no_scratch) m.status = -ERANGE;  // LoRaDemod.cpp:69-71
+        m.normalised = 1;
+        m.scale = 1.0f / mx;
+    }
+    return m;
 }
 
 // ---------------------------------------------------------------------------
@@ -123,9 +129,7 @@ __global__ __launch_bounds__(kTile) void k_maxabs(DemodArgs A) {
     float mx = 0.0f;
     auto acc = [&](cf32 x, unsigned long long i) {
         if (dech) x = i < dech_end ? cmul(x, A.down[i & (N - 1)]) : czero();
-        const float r = fabsf(x.x), im = fabsf(x.y);
-        const float m = (r < im) ? im : r;  // std::max(r, im): NaN in r never wins
-        if (m > mx) mx = m;
+        maxabs_acc(mx, x);
     };
     if ((reinterpret_cast<uintptr_t>(fr) & 15) == 0) {
         const float4* f4 = reinterpret_cast<const float4*>(fr);
@@ -163,15 +167,7 @@ __global__ __launch_bounds__(kTile) void k_maxabs(DemodArgs A) {
         mx = wmax[0];
 #pragma unroll
         for (int w = 1; w < kTile / 64; ++w) mx = wmax[w] > mx ? wmax[w] : mx;
-        lphy_frame_meta m{};
-        m.scale = 1.0f;
-        m.have_sync = A.total_syms >= 2;
-        if (mx > 1.0f) {
-            if (A.no_scratch) m.status = -ERANGE;  // LoRaDemod.cpp:69-71
-            m.normalised = 1;
-            m.scale = 1.0f / mx;
-        }
-        A.meta[f] = m;
+        A.meta[f] = norm_meta(mx, A.total_syms >= 2, A.no_scratch);
     }
 }
 
@@ -187,6 +183,64 @@ struct UnitResult {
     int valid;   // p > best_p reachable (maxValue > 0)
     float findex;
     float phase;
+};
+
+// Detector outputs of one estimate unit from its FFT bins, which the team
+// has written back to its LDS slot (LoRaDetector.hpp:60-71).
+template <int SF>
+__device__ __forceinline__ UnitResult unit_result(const cf32* lds, int slot, ArgMax best) {
+    using G = Geo<SF>;
+    constexpr int N = G::N;
+    UnitResult r;
+    const int idx = best.i;
+    const float mv = best.v > 0.0f ? best.v : 0.0f;
+    const float fund = sqrtf(mv);
+    const cf32 lb = lds[G::addr(slot, idx > 0 ? idx - 1 : N - 1)];
+    const cf32 rb = lds[G::addr(slot, idx < N - 1 ? idx + 1 : 0)];
+    const float left = lphy_libm::cabsf_exact(lb.x, lb.y);
+    const float right = lphy_libm::cabsf_exact(rb.x, rb.y);
+    const double demon = (2.0 * (double)fund) - (double)right - (double)left;
+    const float fi = demon == 0.0 ? 0.0f : (float)(0.5 * (double)(right - left) / demon);
+    const cf32 bin = lds[G::addr(slot, idx)];
+    r.idx = idx;
+    r.valid = mv > 0.0f;  // osr == 1: p > -1e30 <=> maxValue > 0
+    r.findex = fi;
+    r.phase = lphy_libm::atan2f_exact(bin.y, bin.x);
+    return r;
+}
+
+// Running fold of the per-symbol estimates in symbol order
+// (LoRaDemod.cpp:95-128 / phy.cpp:95-135).
+struct EstFold {
+    float sum_index = 0.0f, phase_diff = 0.0f, prev_phase = 0.0f;
+    bool have_prev = false;
+    unsigned sum_t = 0;
+    __device__ __forceinline__ void add(int best_idx, float best_f, int best_t, float best_phase) {
+        sum_t += (unsigned)best_t;
+        sum_index += (float)best_idx + best_f;
+        if (have_prev) {
+            float d = best_phase - prev_phase;
+            while (d > kPi) d -= 2.0f * kPi;
+            while (d < -kPi) d += 2.0f * kPi;
+            phase_diff += d;
+        }
+        prev_phase = best_phase;
+        have_prev = true;
+    }
+    // offsets of LoRaDemod.cpp:130-140 / phy.cpp:137-147 into m
+    __device__ __forceinline__ void finish(lphy_frame_meta& m, int est_syms, int N, int osr) const {
+        const float avg_index = sum_index / (float)est_syms;
+        const float cfo_coarse = avg_index / (float)N;
+        float cfo_fine = 0.0f;
+        if (est_syms > 1)
+            cfo_fine = (phase_diff / (float)(est_syms - 1)) / (2.0f * kPi * (float)N);
+        m.cfo = cfo_coarse + cfo_fine;
+        const float frac = avg_index - floorf(avg_index + 0.5f);
+        const float avg_t = (float)sum_t / (float)est_syms;
+        m.time_offset = avg_t - frac * (float)N * (float)osr;
+        m.t_off = round_to_int(m.time_offset);
+        m.rate = -2.0f * kPi * m.cfo / (float)N;
+    }
 };
 
 template <int SF>
@@ -207,9 +261,7 @@ __global__ __launch_bounds__(kTile) void k_estimate(DemodArgs A) {
     for (int i = tid; i < N; i += kTile) twl[i] = A.tw[i];
 
     // fold state of frame (fbase + tid), held by thread tid < FPT
-    float sum_index = 0.0f, phase_diff = 0.0f, prev_phase = 0.0f;
-    bool have_prev = false;
-    unsigned sum_t = 0;
+    EstFold fold;
     lphy_frame_meta mine{};
     const bool folder = tid < FPT && fbase + tid < A.frames;
     if (folder) {
@@ -255,27 +307,7 @@ __global__ __launch_bounds__(kTile) void k_estimate(DemodArgs A) {
         for (int e = 0; e < G::E; ++e) lds[G::addr(slot, bin_of<SF>(e, lam))] = v[e];
         ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), red);
         __syncthreads();
-        if (lam == 0) {
-            UnitResult r{0, 0, 0.0f, 0.0f};
-            if (live) {
-                // LoRaDetector.hpp:60-71
-                const int idx = best.i;
-                const float mv = best.v > 0.0f ? best.v : 0.0f;
-                const float fund = sqrtf(mv);
-                const cf32 lb = lds[G::addr(slot, idx > 0 ? idx - 1 : N - 1)];
-                const cf32 rb = lds[G::addr(slot, idx < N - 1 ? idx + 1 : 0)];
-                const float left = lphy_libm::cabsf_exact(lb.x, lb.y);
-                const float right = lphy_libm::cabsf_exact(rb.x, rb.y);
-                const double demon = (2.0 * (double)fund) - (double)right - (double)left;
-                const float fi = demon == 0.0 ? 0.0f : (float)(0.5 * (double)(right - left) / demon);
-                const cf32 bin = lds[G::addr(slot, idx)];
-                r.idx = idx;
-                r.valid = mv > 0.0f;  // osr == 1: p > -1e30 <=> maxValue > 0
-                r.findex = fi;
-                r.phase = lphy_libm::atan2f_exact(bin.y, bin.x);
-            }
-            units[slot] = r;
-        }
+        if (lam == 0) units[slot] = live ? unit_result<SF>(lds, slot, best) : UnitResult{0, 0, 0.0f, 0.0f};
         __syncthreads();
         if (folder) {
             const int first = packed ? tid * U : 0;
@@ -290,34 +322,14 @@ __global__ __launch_bounds__(kTile) void k_estimate(DemodArgs A) {
                         break;
                     }
                 }
-                sum_t += (unsigned)best_t;
-                sum_index += (float)best_idx + best_f;
-                if (have_prev) {
-                    float d = best_phase - prev_phase;
-                    while (d > kPi) d -= 2.0f * kPi;
-                    while (d < -kPi) d += 2.0f * kPi;
-                    phase_diff += d;
-                }
-                prev_phase = best_phase;
-                have_prev = true;
+                fold.add(best_idx, best_f, best_t, best_phase);
             }
         }
     }
 
     if (folder && mine.status == 0) {
-        const int est_syms = U / A.osr;
         lphy_frame_meta m = mine;
-        const float avg_index = sum_index / (float)est_syms;
-        const float cfo_coarse = avg_index / (float)N;
-        float cfo_fine = 0.0f;
-        if (est_syms > 1)
-            cfo_fine = (phase_diff / (float)(est_syms - 1)) / (2.0f * kPi * (float)N);
-        m.cfo = cfo_coarse + cfo_fine;
-        const float frac = avg_index - floorf(avg_index + 0.5f);
-        const float avg_t = (float)sum_t / (float)est_syms;
-        m.time_offset = avg_t - frac * (float)N * (float)A.osr;
-        m.t_off = round_to_int(m.time_offset);
-        m.rate = -2.0f * kPi * m.cfo / (float)N;
+        fold.finish(m, U / A.osr, N, A.osr);
         A.meta[fbase + tid] = m;
     }
 }
@@ -334,7 +346,7 @@ struct SymCtx {
     unsigned f, s;            // frame, symbol within the frame
     unsigned base;            // first sample of the (shifted) window in the frame
     float start, rate, scale;
-    bool ok, have_sync;
+    bool ok, have_sync, live;
 };
 
 __device__ __forceinline__ SymCtx sym_ctx(const DemodArgs& A, unsigned f, unsigned s, bool live,
@@ -343,6 +355,7 @@ __device__ __forceinline__ SymCtx sym_ctx(const DemodArgs& A, unsigned f, unsign
     c.f = f;
     c.s = s;
     c.ok = live && m.status == 0;
+    c.live = live;
     c.have_sync = m.have_sync != 0;
     // LoRaDemod.cpp:144-151 with osr == 1, in 32 bits
     const unsigned step = (unsigned)N, count = (unsigned)A.frame_samples;
@@ -532,6 +545,331 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
         if constexpr (WAVE) team_sync<SF>();  // slot reads done before restaging
         c = nc;
         f = nf; s = ns; fw = nfw; sw = nsw;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fused single launch (LPS <= 64 i.e. SF <= 10, two estimate symbols, osr 1).
+// Every wavefront owns the frames f = w, w + W, w + 2W, ... (W waves in the
+// grid) and runs their whole chain itself, so no data crosses wavefronts:
+//   M  max(|I|,|Q|) scan of the frame (LoRaDemod.cpp:60-78), wave-wide
+//   E  the two estimate FFTs (LoRaDemod.cpp:80-140 / phy.cpp:81-148) and the
+//      fold into the frame's offsets
+//   D  the frame's symbols (rotation, FFT, argmax)
+// The wave works through a stream of "units" in tiles of WT = 64/LPS, one
+// unit per team of LPS lanes:
+//   [E(0) x2, pad to a tile] then per frame k: [E(k+1) x2, D(k) x S]
+// so the estimate of frame k+1 shares tiles with symbols of frame k and no
+// team idles; E(k+1) lies >= S + 2 units ahead of D(k+1), i.e. (with
+// S + 3 >= 2 WT, checked on the host) at least two tiles, which is what the
+// one-tile-ahead IQ prefetch needs.  M(k) runs right before the tile
+// holding E(k)'s first unit.  Frame records pass between teams through a
+// 3-slot ring per wave in LDS.  Compared with separate launches this
+// removes a whole-batch pass (the prologue kernels) and overlaps the
+// HBM-bound max-abs scans of some waves with the VALU-bound transforms of
+// the others.
+// ---------------------------------------------------------------------------
+struct FrameArgs {
+    DemodArgs A;
+    unsigned waves;  // wavefronts in the grid
+};
+
+// Per-frame record of the public meta array written by E: every field but
+// sw0 / sw1, which the D tasks of symbols 0 and 1 write (disjoint bytes, so
+// the two L2 write-backs cannot clobber each other).
+__device__ __forceinline__ void meta_put_est(lphy_frame_meta* dst, const lphy_frame_meta& m) {
+    float4* d16 = reinterpret_cast<float4*>(dst);
+    d16[0] = float4{m.cfo, m.time_offset, m.rate, m.scale};
+    int* d8 = reinterpret_cast<int*>(dst);
+    d8[4] = m.t_off;
+    d8[5] = m.status;
+    uint8_t* b = reinterpret_cast<uint8_t*>(dst);
+    b[28] = m.sync_word;
+    b[29] = m.crc_ok;
+    b[30] = m.normalised;
+    b[31] = m.have_sync;
+}
+
+// Max-abs of frame f by one wavefront (16-byte loads, 8 in flight per
+// lane), same arithmetic as k_maxabs; the result is in every lane.
+template <int SF, int MODE>
+__device__ __forceinline__ float wave_maxabs(const DemodArgs& A, unsigned f, const cf32* down) {
+    constexpr int N = 1 << SF;
+    const int lane = threadIdx.x & 63;
+    const cf32* fr = A.iq + (unsigned long long)f * A.frame_samples;
+    const unsigned count = (unsigned)A.frame_samples;
+    const unsigned dech_end = (unsigned)A.total_syms * N;
+    float mx = 0.0f;
+    auto acc = [&](cf32 x, unsigned i) {
+        if constexpr (MODE == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+            x = i < dech_end ? cmul(x, down[i & (N - 1)]) : czero();
+        maxabs_acc(mx, x);
+    };
+    if ((reinterpret_cast<uintptr_t>(fr) & 15) == 0) {
+        const float4* f4 = reinterpret_cast<const float4*>(fr);
+        const unsigned n4 = count / 2;
+        constexpr int U = 8;
+        unsigned j = lane;
+        for (; j + (U - 1) * 64 < n4; j += U * 64) {
+            float4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = f4[j + u * 64];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const unsigned i = 2 * (j + u * 64);
+                acc(cf32{v[u].x, v[u].y}, i);
+                acc(cf32{v[u].z, v[u].w}, i + 1);
+            }
+        }
+        for (; j < n4; j += 64) {
+            const float4 v = f4[j];
+            acc(cf32{v.x, v.y}, 2 * j);
+            acc(cf32{v.z, v.w}, 2 * j + 1);
+        }
+        if ((count & 1) && lane == 0) acc(fr[count - 1], count - 1);
+    } else {
+        for (unsigned i = lane; i < count; i += 64) acc(fr[i], i);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float o = __shfl_xor(mx, off, 64);
+        mx = o > mx ? o : mx;
+    }
+    return mx;
+}
+
+// Staging of a tile that mixes estimate units (no rotation; mode 0: raw
+// samples, modes 1/2: [dechirped,] normalised; zero when the frame is not
+// estimated) with symbol units (as stage_symbol).  est_sample() semantics.
+template <int SF, int MODE>
+__device__ __forceinline__ void stage_mixed(cf32* lds, const Stage<SF>& stg, const cf32 (&raw)[16],
+                                            const cf32* src, const SymCtx& c, int lam,
+                                            const cf32* down, const float* win, bool est) {
+    using G = Geo<SF>;
+    constexpr int N = G::N;
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) {
+        const int i = lam + e * G::LPS;
+        cf32 x = raw[e];
+        cf32 pre;  // input of the rotation
+        if constexpr (MODE == LPHY_MODE_DEMODULATE) {
+            pre = cmul(x, down[i]);
+        } else {
+            if constexpr (MODE == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+                x = cmul(x, down[((unsigned)c.base + (unsigned)i) & (N - 1)]);
+            x = cscale(x, c.scale);
+            pre = x;
+        }
+        const float ph = c.start + c.rate * (float)i;
+        float sn, cs;
+        lphy_libm::sincosf_fast(ph, &sn, &cs);
+        cf32 y = cmul(pre, cf32{cs, sn});
+        y = est ? (c.ok ? x : czero()) : y;
+        if (win) y = cscale(y, win[i]);
+        stg.put(lds, e, y);
+    }
+    if (!est && (lphy_libm::sincosf_needs_large(c.start + c.rate * (float)lam) ||
+                 lphy_libm::sincosf_needs_large(c.start + c.rate * (float)(lam + (G::E - 1) * G::LPS)))) {
+        for (int e = 0; e < G::E; ++e) {
+            const int i = lam + e * G::LPS;
+            if (lphy_libm::sincosf_needs_large(c.start + c.rate * (float)i))
+                stg.put(lds, e, rotate_sample<SF, MODE>(src[i], i, c, down, win, true));
+        }
+    }
+}
+
+enum : int { kUnitDead = 0, kUnitEst = 1, kUnitSym = 2 };
+
+template <int SF, int MODE, int OCC>
+__global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
+    using G = Geo<SF>;
+    static_assert(G::LPS <= 64, "fused path needs a symbol inside one wavefront");
+    constexpr int N = G::N;
+    constexpr bool TAB = N <= 1024;
+    constexpr int WT = 64 / G::LPS;               // units per tile
+    constexpr unsigned U = 2;                      // estimate units per frame
+    // prefix tiles: E of the first frame, then one tile that keeps its
+    // symbols two tiles behind it like every later frame's
+    constexpr unsigned PT = (U + WT - 1) / WT + 1;
+    constexpr int WPB = kTile / 64;
+    const DemodArgs& A = P.A;
+    __shared__ cf32 lds[G::T * G::SSTRIDE];
+    __shared__ cf32 twl[N];
+    __shared__ cf32 dnl[TAB ? N : 1];
+    __shared__ float wnl[TAB ? N : 1];
+    __shared__ UnitResult ures[WPB][U];
+    __shared__ float4 ring[WPB][3];  // frame records: rate, scale, t_off, flags
+
+    const int tid = threadIdx.x;
+    for (int i = tid; i < N; i += kTile) {
+        twl[i] = A.tw[i];
+        if constexpr (TAB) {
+            if (MODE != LPHY_MODE_LORA_DEMODULATE) dnl[i] = A.down[i];
+            if (A.win) wnl[i] = A.win[i];
+        }
+    }
+    __syncthreads();  // the last workgroup barrier: waves are independent below
+    const cf32* down = TAB ? dnl : A.down;
+    const float* win = A.win ? (TAB ? wnl : A.win) : nullptr;
+
+    const int lane = tid & 63, wv = tid >> 6;
+    const int slot = tid / G::LPS, lam = tid % G::LPS;
+    const unsigned wslot = (unsigned)(slot % WT);
+    const Stage<SF> stg(slot, lam);
+    const unsigned nframes = (unsigned)A.frames;
+    const unsigned S = (unsigned)A.total_syms, SL = U + S;
+    const unsigned W = P.waves;
+    const unsigned w = blockIdx.x * WPB + wv;
+    if (w >= nframes) return;
+    const unsigned nk = (nframes - 1 - w) / W + 1;  // frames of this wave
+    const unsigned long long L = (unsigned long long)PT * WT + (unsigned long long)nk * SL;
+    const unsigned ntiles = (unsigned)((L + WT - 1) / WT);
+
+    // unit of this team in tile t; (k, o) = slice and offset for t >= PT
+    auto unit_of = [&](unsigned t, unsigned k, unsigned o, unsigned& kind, unsigned& fk,
+                       unsigned& s) {
+        if (t < PT) {
+            const unsigned q = t * WT + wslot;
+            kind = q < U ? kUnitEst : kUnitDead;
+            fk = 0;
+            s = q;
+        } else if (o < U) {
+            kind = k + 1 < nk ? kUnitEst : kUnitDead;
+            fk = k + 1;
+            s = o;
+        } else {
+            kind = k < nk ? kUnitSym : kUnitDead;
+            fk = k;
+            s = o - U;
+        }
+    };
+    // context of a unit; symbol units read their frame record from the ring
+    auto ctx_of = [&](unsigned kind, unsigned fk, unsigned s) -> SymCtx {
+        const unsigned f = w + fk * W;
+        if (kind == kUnitSym) {
+            const float4 r = ring[wv][fk % 3];
+            lphy_frame_meta m{};
+            m.rate = r.x;
+            m.scale = r.y;
+            m.t_off = __float_as_int(r.z);
+            const unsigned fl = __float_as_uint(r.w);
+            m.status = (fl & 1u) ? 0 : -1;
+            m.have_sync = (fl & 2u) ? 1 : 0;
+            return sym_ctx(A, f, s, true, N, m);
+        }
+        SymCtx c{};
+        c.f = kind == kUnitEst ? f : w;
+        c.s = s;
+        c.base = kind == kUnitEst ? s * N : 0;
+        c.scale = 1.0f;
+        c.live = kind == kUnitEst;
+        return c;
+    };
+
+    unsigned k = 0, o = wslot;  // position of tile t (t >= PT)
+    unsigned kind, fk, su;
+    unit_of(0, k, o, kind, fk, su);
+    SymCtx c = ctx_of(kind, fk, su);
+    cf32 raw[16];
+    {
+        const cf32* src = A.iq + (unsigned long long)c.f * A.frame_samples + c.base;
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) raw[e] = src[lam + e * G::LPS];
+    }
+    unsigned m_seq = 0xffffffffu;  // frame whose max-abs `mx` holds
+    float mx = 0.0f;
+
+    for (unsigned t = 0; t < ntiles; ++t) {
+        // estimate units in this tile (all of one frame): its max-abs first
+        const unsigned long long emask = __ballot(kind == kUnitEst);
+        unsigned ke = 0;
+        if (emask) {
+            ke = (unsigned)__shfl((int)fk, __ffsll((long long)emask) - 1, 64);
+            if (MODE != LPHY_MODE_DEMODULATE && ke != m_seq) {
+                mx = wave_maxabs<SF, MODE>(A, w + ke * W, down);
+                m_seq = ke;
+            }
+            if (kind == kUnitEst) {
+                if (MODE != LPHY_MODE_DEMODULATE) {
+                    const lphy_frame_meta nm = norm_meta(mx, true, A.no_scratch);
+                    c.scale = nm.scale;
+                    c.live = nm.status == 0;
+                }
+                c.ok = c.live;  // estimate this unit (else stage zeros)
+            }
+            stage_mixed<SF, MODE>(lds, stg, raw, A.iq + (unsigned long long)c.f * A.frame_samples + c.base,
+                                  c, lam, down, win, kind != kUnitSym);
+        } else {
+            stage_symbol<SF, MODE>(lds, stg, raw, A.iq + (unsigned long long)c.f * A.frame_samples + c.base,
+                                   c, lam, down, win);
+        }
+        team_sync<SF>();
+
+        // next tile's unit, context and IQ (in flight during the FFT)
+        unsigned nkk = k, no = o;
+        if (t + 1 == PT) {
+            nkk = 0;
+            no = wslot;
+        } else if (t + 1 > PT) {
+            no += WT;
+            if (no >= SL) { no -= SL; ++nkk; }
+        }
+        unsigned nkind, nfk, nsu;
+        unit_of(t + 1, nkk, no, nkind, nfk, nsu);
+        const SymCtx nc = ctx_of(nkind, nfk, nsu);
+        if (t + 1 < ntiles) {
+            const cf32* nsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base;
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) raw[e] = nsrc[lam + e * G::LPS];
+        }
+
+        cf32 v[16];
+        fft_tile<SF>(v, lds, slot, lam, twl);
+        const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), nullptr);
+        if (emask) {
+            // detector outputs of the estimate units (LoRaDetector.hpp:60-71)
+            if (kind == kUnitEst) {
+#pragma unroll
+                for (int e = 0; e < G::E; ++e) lds[G::addr(slot, bin_of<SF>(e, lam))] = v[e];
+            }
+            team_sync<SF>();
+            if (kind == kUnitEst && lam == 0)
+                ures[wv][su] = c.ok ? unit_result<SF>(lds, slot, best) : UnitResult{0, 0, 0.0f, 0.0f};
+        }
+        if (kind == kUnitSym && lam == 0) {
+            // sw0 / sw1 also for frames that are not demodulated (0, as the
+            // separate-launch path leaves them)
+            if (c.have_sync && c.s < 2) store_symbol(A, c, c.ok ? (uint16_t)best.i : (uint16_t)0);
+            else if (c.ok) store_symbol(A, c, (uint16_t)best.i);
+        }
+        team_sync<SF>();  // slot reads (and ures) done
+        // the frame whose last estimate unit was in this tile: fold
+        if (__ballot(kind == kUnitEst && su == U - 1) && lane == 0) {
+            lphy_frame_meta m{};
+            m.scale = 1.0f;
+            m.have_sync = 1;
+            if (MODE != LPHY_MODE_DEMODULATE) m = norm_meta(mx, true, A.no_scratch);
+            if (m.status == 0) {
+                EstFold fold;
+#pragma unroll
+                for (unsigned u = 0; u < U; ++u) {
+                    const UnitResult r = ures[wv][u];
+                    if (r.valid) fold.add(r.idx, r.findex, 0, r.phase);
+                    else fold.add(0, 0.0f, 0, 0.0f);
+                }
+                fold.finish(m, (int)U, N, 1);
+            }
+            ring[wv][ke % 3] = float4{m.rate, m.scale, __int_as_float(m.t_off),
+                                      __uint_as_float((m.status == 0 ? 1u : 0u) | 2u)};
+            meta_put_est(&A.meta[w + ke * W], m);
+        }
+        team_sync<SF>();
+        k = nkk;
+        o = no;
+        kind = nkind;
+        fk = nfk;
+        su = nsu;
+        c = nc;
     }
 }
 
@@ -830,6 +1168,65 @@ void launch_symbols(const DemodArgs& A, unsigned long long tiles, hipStream_t st
     launch_symbols_occ<SF, MODE, 2>(A, tiles, st);
 }
 
+// Fused path (k_frames).
+template <int SF, int MODE, int OCC>
+int frames_grid() {
+    static int grid = 0;
+    if (grid == 0) {
+        int dev = 0, cus = 0, per = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_frames<SF, MODE, OCC>, kTile, 0);
+        grid = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
+    }
+    return grid;
+}
+
+template <int SF, int MODE, int OCC>
+int launch_frames_occ(const DemodArgs& A, hipStream_t st) {
+    FrameArgs P{};
+    P.A = A;
+    constexpr unsigned WPB = kTile / 64;
+    unsigned long long blocks = (unsigned long long)frames_grid<SF, MODE, OCC>();
+    const unsigned long long need = (A.frames + WPB - 1) / WPB;
+    if (blocks > need) blocks = need;
+    P.waves = (unsigned)(blocks * WPB);
+    hipLaunchKernelGGL((k_frames<SF, MODE, OCC>), dim3((unsigned)blocks), dim3(kTile), 0, st, P);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+// Waves per SIMD of k_frames: 2 (<= 256 VGPRs; its loop carries more state
+// than k_demod's and spills at 3).  LPHY_FRAMES_OCC=3 for experiments.
+inline int frames_occ() {
+    static int env = -1;
+    if (env < 0) {
+        const char* e = getenv("LPHY_FRAMES_OCC");
+        env = e ? atoi(e) : 0;
+    }
+    return env == 3 ? 3 : 2;
+}
+
+template <int SF, int MODE>
+int launch_frames_mode(const DemodArgs& A, hipStream_t st) {
+    if constexpr (SF <= 10) {
+        if (frames_occ() == 3) return launch_frames_occ<SF, MODE, 3>(A, st);
+    }
+    return launch_frames_occ<SF, MODE, 2>(A, st);
+}
+
+// Whether k_frames can take this batch: a symbol within one wavefront, the
+// two-symbol estimate, and frames long enough that a frame's estimate tile
+// precedes its first symbol tile by two tiles (S + 3 >= 2 * units/tile).
+inline bool frames_fit(unsigned sf, unsigned osr, int est_units, size_t total) {
+    if (sf > 10 || osr != 1 || est_units != 2 || total < 2) return false;
+    const size_t E = sf >= 4 ? 16 : ((size_t)1 << sf);
+    const size_t lps = ((size_t)1 << sf) / E;
+    const size_t wt = 64 / lps;
+    return total + 3 >= 2 * wt;
+}
+
+
 template <int SF>
 int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symbols) {
     using G = Geo<SF>;
@@ -871,6 +1268,45 @@ int launch_demod(unsigned sf, const DemodArgs& A, hipStream_t st, bool pro, bool
         case 12: return launch_demod_sf<12>(A, st, pro, sym);
         default: return -EINVAL;
     }
+}
+
+template <int SF>
+int launch_frames_sf(const DemodArgs& A, hipStream_t st) {
+    if constexpr (Geo<SF>::LPS > 64) {
+        (void)A; (void)st;
+        return -ENOTSUP;
+    } else {
+        switch (A.mode) {
+            case LPHY_MODE_DEMODULATE: return launch_frames_mode<SF, LPHY_MODE_DEMODULATE>(A, st);
+            case LPHY_MODE_LORA_DEMODULATE: return launch_frames_mode<SF, LPHY_MODE_LORA_DEMODULATE>(A, st);
+            default: return launch_frames_mode<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>(A, st);
+        }
+    }
+}
+
+int launch_frames(unsigned sf, const DemodArgs& A, hipStream_t st) {
+    switch (sf) {
+        case 1: return launch_frames_sf<1>(A, st);
+        case 2: return launch_frames_sf<2>(A, st);
+        case 3: return launch_frames_sf<3>(A, st);
+        case 4: return launch_frames_sf<4>(A, st);
+        case 5: return launch_frames_sf<5>(A, st);
+        case 6: return launch_frames_sf<6>(A, st);
+        case 7: return launch_frames_sf<7>(A, st);
+        case 8: return launch_frames_sf<8>(A, st);
+        case 9: return launch_frames_sf<9>(A, st);
+        case 10: return launch_frames_sf<10>(A, st);
+        default: return -ENOTSUP;
+    }
+}
+
+bool fused_enabled() {
+    static int env = -1;
+    if (env < 0) {
+        const char* e = getenv("LPHY_FUSED");
+        env = (e && e[0] == '0') ? 0 : 1;
+    }
+    return env == 1;
 }
 
 int ensure_stage(lphy_hip_ctx* c, size_t bytes) {
@@ -1001,8 +1437,12 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
         return -ERANGE;
     const unsigned stages = flags & (LPHY_F_STAGE_PROLOGUE | LPHY_F_STAGE_SYMBOLS | LPHY_F_STAGE_FINAL);
     const bool all = stages == 0;
-    int rc = launch_demod(c->sf, A, st, all || (stages & LPHY_F_STAGE_PROLOGUE),
-                          all || (stages & LPHY_F_STAGE_SYMBOLS));
+    // one fused launch when the frame shape allows it (see k_frames)
+    const bool fused = all && !(flags & LPHY_F_UNFUSED) && fused_enabled() &&
+                       frames_fit(c->sf, c->osr, A.est_units, total);
+    int rc = fused ? launch_frames(c->sf, A, st)
+                   : launch_demod(c->sf, A, st, all || (stages & LPHY_F_STAGE_PROLOGUE),
+                                  all || (stages & LPHY_F_STAGE_SYMBOLS));
     if (rc) return rc;
     if (!all && !(stages & LPHY_F_STAGE_FINAL)) return 0;
     FinalArgs F{};

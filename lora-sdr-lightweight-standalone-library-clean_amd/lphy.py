@@ -28,6 +28,7 @@ F_NO_SCRATCH = 2
 F_STAGE_PROLOGUE = 4
 F_STAGE_SYMBOLS = 8
 F_STAGE_FINAL = 16
+F_UNFUSED = 32  # separate prologue / symbol launches (lphy_hip.h)
 WINDOW_NONE = 0
 WINDOW_HANN = 1
 

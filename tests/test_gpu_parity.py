@@ -48,13 +48,19 @@ CASES = [
 ]
 
 
+# launch paths: the fused single launch (default, SF <= 10) and the
+# separate prologue / symbol kernels
+LAUNCH = [0, 32]
+
+
 @pytest.mark.parametrize("sf,bw,nf,plen,snr,delay,hann", CASES)
-def test_mode_demodulate_vs_oracle(oracle, lphy, sf, bw, nf, plen, snr, delay, hann):
+@pytest.mark.parametrize("launch", LAUNCH)
+def test_mode_demodulate_vs_oracle(oracle, lphy, sf, bw, nf, plen, snr, delay, hann, launch):
     """lora_phy::demodulate + decode (phy.cpp:182-261) per frame."""
     iq, _ = _frames(oracle, sf, bw, nf, plen, seed=sf * 100 + nf, snr_db=snr, delay=delay)
     d = lphy.Demodulator(sf, bw, 1, lphy.WINDOW_HANN if hann else lphy.WINDOW_NONE)
     fs = iq.shape[1]
-    syms, pay, meta = d.demod_host(iq, nf, fs, lphy.MODE_DEMODULATE, lphy.F_DECODE)
+    syms, pay, meta = d.demod_host(iq, nf, fs, lphy.MODE_DEMODULATE, lphy.F_DECODE | launch)
     for f in range(nf):
         r, osyms, osync, omet = oracle.demodulate(iq[f], sf, bw_hz=bw, hann=hann)
         assert r == syms.shape[1]
@@ -69,14 +75,16 @@ def test_mode_demodulate_vs_oracle(oracle, lphy, sf, bw, nf, plen, snr, delay, h
 
 @pytest.mark.parametrize("sf,bw,nf,plen,snr,delay,hann", CASES)
 @pytest.mark.parametrize("fused", [False, True])
-def test_mode_lora_demodulate_vs_oracle(oracle, lphy, sf, bw, nf, plen, snr, delay, hann, fused):
+@pytest.mark.parametrize("launch", LAUNCH)
+def test_mode_lora_demodulate_vs_oracle(oracle, lphy, sf, bw, nf, plen, snr, delay, hann, fused,
+                                        launch):
     """external dechirp -> lora_demodulate -> lora_decode (LoRaDemod.cpp:50-197)."""
     iq, payloads = _frames(oracle, sf, bw, nf, plen, seed=sf * 7 + nf, snr_db=snr, delay=delay)
     dech = np.stack([oracle.dechirp(x, sf, bw) for x in iq])
     d = lphy.Demodulator(sf, bw, 1, lphy.WINDOW_HANN if hann else lphy.WINDOW_NONE)
     fs = iq.shape[1]
     mode = lphy.MODE_DECHIRP_LORA_DEMODULATE if fused else lphy.MODE_LORA_DEMODULATE
-    syms, pay, meta = d.demod_host(iq if fused else dech, nf, fs, mode, lphy.F_DECODE)
+    syms, pay, meta = d.demod_host(iq if fused else dech, nf, fs, mode, lphy.F_DECODE | launch)
     for f in range(nf):
         r, osyms, osync, omet = oracle.lora_demodulate(dech[f], sf, hann=hann)
         np.testing.assert_array_equal(syms[f], osyms)
@@ -127,3 +135,56 @@ def test_zero_and_overrange_frames(oracle, lphy):
     syms, _, meta = d.demod_host(big, 1, N, lphy.MODE_LORA_DEMODULATE)
     r, osyms, osync, omet = oracle.lora_demodulate(big[0], sf)
     np.testing.assert_array_equal(syms[0], osyms)
+
+
+@pytest.mark.parametrize("sf,nf", [(7, 3001), (8, 1203), (9, 517), (10, 129), (5, 2049)])
+def test_large_batch_fused_equals_unfused(oracle, lphy, sf, nf):
+    """Many frames through the fused ticket scheduler (look-ahead, partial
+    groups, waits) against the separate launches, every output bit; the
+    first frames also against the oracle.  Frames get random CFO-like
+    rotations, delays and noise so that normalisation, offsets and the
+    large-phase sincos branch all occur."""
+    rng = np.random.default_rng(sf * 1000 + nf)
+    N = 1 << sf
+    base = oracle.modulate(oracle.encode(bytes(range(16))), sf)
+    fs = base.size
+    t = np.arange(fs, dtype=np.float64)
+    iq = np.empty((nf, fs), np.complex64)
+    for f in range(nf):
+        x = base * np.exp(2j * np.pi * rng.uniform(-0.4, 0.4) / N * t)
+        x = np.roll(x, int(rng.integers(0, 4)))
+        sig = [0.0, 0.05, 0.5, 2.0][f % 4]
+        x = x + sig * (rng.standard_normal(fs) + 1j * rng.standard_normal(fs))
+        iq[f] = (x * [1.0, 0.5, 3.0][f % 3]).astype(np.complex64)
+    d = lphy.Demodulator(sf)
+    for mode in (lphy.MODE_DEMODULATE, lphy.MODE_DECHIRP_LORA_DEMODULATE):
+        a = d.demod_host(iq, nf, fs, mode, lphy.F_DECODE)
+        b = d.demod_host(iq, nf, fs, mode, lphy.F_DECODE | lphy.F_UNFUSED)
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
+        np.testing.assert_array_equal(a[2].view(np.uint8), b[2].view(np.uint8))
+    for f in range(4):
+        r, osyms, osync, omet = oracle.lora_demodulate(oracle.dechirp(iq[f], sf, 125000), sf)
+        np.testing.assert_array_equal(a[0][f], osyms)
+        assert _bits(a[2]["cfo"][f]) == _bits(omet[0])
+
+
+def test_fused_no_scratch_mixed(oracle, lphy):
+    """-ERANGE frames (rescale needed, no scratch) interleaved with normal
+    ones in one fused batch."""
+    sf, N = 7, 128
+    base = oracle.modulate(oracle.encode(bytes(range(8))), sf)
+    fs = base.size
+    nf = 37
+    iq = np.stack([base * (2.0 if f % 3 == 1 else 0.9) for f in range(nf)]).astype(np.complex64)
+    d = lphy.Demodulator(sf)
+    for flags in (lphy.F_NO_SCRATCH, lphy.F_NO_SCRATCH | lphy.F_UNFUSED):
+        syms, _, meta = d.demod_host(iq, nf, fs, lphy.MODE_DECHIRP_LORA_DEMODULATE, flags)
+        for f in range(nf):
+            dech = oracle.dechirp(iq[f], sf, 125000)
+            if f % 3 == 1:
+                assert meta["status"][f] == -34
+            else:
+                assert meta["status"][f] == 0
+                r, osyms, osync, omet = oracle.lora_demodulate(dech, sf)
+                np.testing.assert_array_equal(syms[f], osyms)
