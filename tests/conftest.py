@@ -6,7 +6,7 @@ import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
 PKG = ROOT / "lora-sdr-lightweight-standalone-library-clean_amd"
-for p in (str(ROOT / "tests"), str(PKG), str(ROOT)):
+for p in (str(ROOT / "tests" / "golden"), str(ROOT / "tests"), str(PKG), str(ROOT)):
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -7,7 +7,7 @@
 #include "../../lora-sdr-lightweight-standalone-library-clean_amd/csrc/libm_exact.h"
 
 #include <atomic>
-#include <complex.h>
+#include <complex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -80,7 +80,7 @@ int main(int argc, char** argv) {
                     if (is_atan) { g = atan2f(y, x); o = lphy_libm::atan2f_exact(y, x); }
                     else {
                         if (!std::isfinite(x) || !std::isfinite(y)) continue;
-                        g = cabsf(y + I * x);
+                        g = std::abs(std::complex<float>(y, x));  // glibc cabsf, as the reference's std::abs
                         o = lphy_libm::cabsf_exact(y, x);
                     }
                     ++n;

@@ -1,0 +1,103 @@
+"""Pin the CPU oracle (oracle/lphy_oracle.c) to the reference library itself
+(oracle/_ref/libloraref.so, compiled from /root/reference's sources by
+oracle/Makefile) on seeded random inputs: every output bit of each function
+on the hot path.  Skipped where the reference build is absent (GPU boxes)."""
+import numpy as np
+import pytest
+
+
+def _iq(rng, n, scale=1.0):
+    return ((rng.standard_normal(n) + 1j * rng.standard_normal(n)) * scale).astype(np.complex64)
+
+
+def _frame(oracle, rng, sf, bw, plen, snr=None, delay=0, cfo=0.0):
+    iq = oracle.modulate(oracle.encode(rng.integers(0, 256, plen, dtype=np.uint8).tobytes()), sf, bw_hz=bw)
+    if cfo:
+        iq = (iq * np.exp(2j * np.pi * cfo / (1 << sf) * np.arange(iq.size))).astype(np.complex64)
+    if delay:
+        iq = np.concatenate([np.zeros(delay, np.complex64), iq[:-delay]])
+    if snr is not None:
+        s = np.sqrt(10 ** (-snr / 10) / 2)
+        iq = (iq + s * (rng.standard_normal(iq.size) + 1j * rng.standard_normal(iq.size))).astype(np.complex64)
+    return iq
+
+
+def _bits(x):
+    return np.asarray(x, np.float32).view(np.uint32)
+
+
+@pytest.mark.parametrize("sf", range(1, 13))
+def test_fft_bit_exact(oracle, reference, sf):
+    rng = np.random.default_rng(sf)
+    for _ in range(4):
+        x = _iq(rng, 1 << sf, scale=10.0 ** rng.uniform(-3, 3))
+        np.testing.assert_array_equal(oracle.fft(x).view(np.uint32), reference.fft(x).view(np.uint32))
+
+
+@pytest.mark.parametrize("sf,bw", [(s, b) for s in (2, 5, 7, 9, 12) for b in (125000, 250000, 500000)])
+def test_modulate_and_dechirp_bit_exact(oracle, reference, sf, bw):
+    rng = np.random.default_rng(sf * 7 + bw // 125000)
+    syms = rng.integers(0, 1 << min(sf, 8), 12, dtype=np.uint16)
+    for sync in (0x12, 0x34, 0xAB):
+        a = oracle.modulate(syms, sf, bw_hz=bw, sync=sync)
+        b = reference.modulate(syms, sf, bw_hz=bw, sync=sync)
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+    x = _iq(rng, 5 * (1 << sf))
+    np.testing.assert_array_equal(oracle.dechirp(x, sf, bw).view(np.uint32),
+                                  reference.dechirp(x, sf, bw).view(np.uint32))
+
+
+CASES = [(sf, bw, plen, snr, delay, cfo, hann)
+         for sf, bw, plen, snr, delay, cfo, hann in [
+             (7, 125000, 32, None, 0, 0.0, False), (7, 125000, 16, -10.0, 0, 0.0, False),
+             (7, 125000, 20, -18.0, 3, 0.0, False), (7, 250000, 8, None, 0, 0.3, False),
+             (8, 125000, 32, None, 11, -0.2, True), (8, 500000, 12, 0.0, 0, 0.45, False),
+             (9, 125000, 32, -10.0, 0, 0.0, False), (9, 125000, 32, -15.0, 0, 0.0, False),
+             (10, 125000, 16, None, 5, 0.1, False), (11, 125000, 8, -5.0, 0, 0.0, False),
+             (12, 125000, 4, None, 0, -0.35, False), (5, 125000, 8, None, 0, 0.0, False),
+             (6, 250000, 8, 3.0, 2, 0.0, True), (3, 125000, 6, None, 0, 0.0, False)]]
+
+
+@pytest.mark.parametrize("sf,bw,plen,snr,delay,cfo,hann", CASES)
+def test_demodulate_paths_bit_exact(oracle, reference, sf, bw, plen, snr, delay, cfo, hann):
+    """lora_phy::demodulate + decode and dechirp -> lora_demodulate ->
+    lora_decode, every output including the float metrics' bits."""
+    rng = np.random.default_rng(sf * 1000 + plen + delay)
+    for rep in range(3):
+        iq = _frame(oracle, rng, sf, bw, plen, snr, delay, cfo)
+        a = oracle.demodulate(iq, sf, bw_hz=bw, hann=hann)
+        b = reference.demodulate(iq, sf, bw_hz=bw, hann=hann)
+        assert a[0] == b[0] and a[2] == b[2]
+        np.testing.assert_array_equal(a[1], b[1])
+        np.testing.assert_array_equal(_bits(a[3][:2]), _bits(b[3][:2]))
+        np.testing.assert_array_equal(oracle.decode(a[1])[1], reference.decode(b[1])[1])
+        x = oracle.dechirp(iq, sf, bw)
+        for scratch in (True, False):
+            a = oracle.lora_demodulate(x, sf, hann=hann, scratch=scratch)
+            b = reference.lora_demodulate(x, sf, hann=hann, scratch=scratch)
+            assert a[0] == b[0] and a[2] == b[2]
+            np.testing.assert_array_equal(a[1], b[1])
+            np.testing.assert_array_equal(_bits(a[3][:2]), _bits(b[3][:2]))
+
+
+def test_noise_frames_large_phase(oracle, reference):
+    """Pure noise: bogus CFO estimates drive the rotation angle past 120 rad
+    (glibc sincosf's large-argument path)."""
+    rng = np.random.default_rng(77)
+    for sf in (7, 8):
+        for _ in range(4):
+            x = _iq(rng, 60 * (1 << sf))
+            a = oracle.lora_demodulate(x, sf)
+            b = reference.lora_demodulate(x, sf)
+            np.testing.assert_array_equal(a[1], b[1])
+            np.testing.assert_array_equal(_bits(a[3][:2]), _bits(b[3][:2]))
+
+
+def test_encode_decode_roundtrip(oracle, reference):
+    rng = np.random.default_rng(5)
+    for n in (0, 1, 2, 7, 32, 255):
+        p = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        np.testing.assert_array_equal(oracle.encode(p), reference.encode(p))
+        syms = oracle.encode(p) ^ rng.integers(0, 2, 2 * n, dtype=np.uint16) << rng.integers(0, 8, 2 * n, dtype=np.uint16)
+        np.testing.assert_array_equal(oracle.decode(syms)[1], reference.decode(syms)[1])
+        assert oracle.decode(syms)[2] == reference.decode(syms)[2]
