@@ -1,0 +1,35 @@
+"""The lora_phy:: C++ drop-in (include/lora_phy/phy.hpp + liblora_phy_amd.so,
+GPU behind the C ABI) against the reference library: the same probe source
+(tests/cpp/lora_phy_api_probe.cpp) is built against both and must print
+identical transcripts — return codes, symbols, sync words, cfo / time_offset
+bits, CRC flags and payload bytes over the scenarios of the reference's own
+tests (error_code, roundtrip, no_alloc, e2e_chain profiles, bit_exact on
+modulation_tests.bin, equal_power_bin, scratch_buffer_error,
+odd_symbol_count, sync_word) and impaired frames."""
+import subprocess
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+PKG = ROOT / "lora-sdr-lightweight-standalone-library-clean_amd"
+REF_PROBE = ROOT / "oracle" / "_ref" / "lora_phy_api_probe_ref"
+
+
+def test_cxx_api_transcript_matches_reference(tmp_path):
+    if not REF_PROBE.exists():
+        pytest.skip("reference probe not built (oracle/Makefile probe)")
+    exe = tmp_path / "probe_amd"
+    subprocess.run(["g++", "-O2", "-std=gnu++17", "-ffp-contract=off", f"-I{ROOT / 'include'}",
+                    "-o", str(exe), str(ROOT / "tests" / "cpp" / "lora_phy_api_probe.cpp"),
+                    f"-L{PKG / 'lib'}", "-llora_phy_amd", f"-Wl,-rpath,{PKG / 'lib'}"], check=True)
+    golden = str(ROOT / "tests" / "golden")
+    ours = subprocess.run([str(exe), golden], capture_output=True, text=True, timeout=300)
+    assert ours.returncode == 0, ours.stderr
+    ref = subprocess.run([str(REF_PROBE), golden], capture_output=True, text=True, timeout=300)
+    assert ref.returncode == 0, ref.stderr
+    a, b = ours.stdout.splitlines(), ref.stdout.splitlines()
+    assert len(a) == len(b) and len(b) >= 25
+    bad = [(x, y) for x, y in zip(a, b) if x != y]
+    assert not bad, "\n".join(f"ours: {x[:300]}\nref:  {y[:300]}" for x, y in bad[:5])
