@@ -38,6 +38,7 @@ sys.path.insert(0, str(PKG))
 sys.path.insert(0, str(ROOT / "tests"))
 
 import lphy  # noqa: E402
+import shard  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 PAYLOAD = 32                  # bytes per frame (performance_test.cpp:67)
@@ -91,22 +92,33 @@ class Workload:
                              flags, payload=self.pay,
                              stream=torch.cuda.current_stream().cuda_stream)
 
-    def stage_times(self, mode: int, reps: int = 3):
-        """Average device time per launch of each stage (HIP events recorded
-        on the stream the kernels are launched on)."""
-        names = [("prologue", lphy.F_STAGE_PROLOGUE), ("symbols", lphy.F_STAGE_SYMBOLS),
-                 ("final", lphy.F_STAGE_FINAL)]
-        acc = {n: 0.0 for n, _ in names}
+    def _event_ms(self, mode: int, flags: int, reps: int) -> float:
+        """Average device time of one demod_batch call with `flags` (HIP
+        events recorded on the stream the kernels are launched on)."""
+        self.run(mode, flags)
+        torch.cuda.synchronize()
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
         for _ in range(reps):
-            for n, fl in names:
-                a = torch.cuda.Event(enable_timing=True)
-                b = torch.cuda.Event(enable_timing=True)
-                a.record()
-                self.run(mode, lphy.F_DECODE | fl)
-                b.record()
-                torch.cuda.synchronize()
-                acc[n] += a.elapsed_time(b)
-        return {n: v / reps for n, v in acc.items()}
+            self.run(mode, flags)
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps
+
+    def stage_times(self, mode: int, reps: int = 5) -> dict:
+        """Device time per launch of each kernel of the product path: the
+        fused prologue+symbols kernel (k_frames, PROLOGUE|SYMBOLS selects it
+        alone) and k_finalize; plus the separate-launch path's stages
+        (LPHY_F_UNFUSED) for comparison."""
+        D = lphy.F_DECODE
+        both = lphy.F_STAGE_PROLOGUE | lphy.F_STAGE_SYMBOLS
+        return {
+            "fused": self._event_ms(mode, D | both, reps),
+            "final": self._event_ms(mode, D | lphy.F_STAGE_FINAL, reps),
+            "unfused_prologue": self._event_ms(mode, D | lphy.F_UNFUSED | lphy.F_STAGE_PROLOGUE, reps),
+            "unfused_symbols": self._event_ms(mode, D | lphy.F_UNFUSED | lphy.F_STAGE_SYMBOLS, reps),
+        }
 
     def check(self, mode: int) -> dict:
         """Size-independent property over the whole batch (every payload
@@ -135,11 +147,11 @@ class Workload:
         return res
 
 
-def timed(wl: Workload, mode: int, steps: int, warmup: int, world: int, gathered=None):
+def timed(wl: Workload, mode: int, steps: int, warmup: int, world: int):
     def step():
         wl.run(mode)
-        if world > 1:
-            torch.distributed.all_gather_into_tensor(gathered, wl.pay)
+        if world > 1:  # the only exchange: decoded payloads (RCCL all_gather)
+            shard.gather_payloads(wl.pay, wl.frames, PAYLOAD, world * wl.frames)
 
     for _ in range(warmup):
         step()
@@ -184,6 +196,28 @@ def cpu_baseline(wl: Workload, seconds: float) -> dict:
                       f"{el:.1f} s), dechirp+lora_demodulate+lora_decode, payloads ok={ok}"}
 
 
+def frames_fused(sf: int) -> bool:
+    """Whether the bench frame shape takes the fused k_frames launch."""
+    return sf <= 10 and os.environ.get("LPHY_FUSED", "1") != "0"
+
+
+def measured_traffic(kernel: str, frames: int):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (profiles/pmc_*.json written by tools/pmc_summary.py from rocprofv3 --pmc
+    passes of this bench's configuration; FETCH_SIZE x2 on gfx950 +
+    WRITE_SIZE, per the MI355X guide), or None when no summary matches."""
+    best = None
+    for f in sorted((ROOT / "profiles").glob("pmc_*.json")):
+        try:
+            d = json.loads(f.read_text())
+        except ValueError:
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if k and d.get("frames") == frames:
+            best = {"bytes": k["hbm_bytes_per_launch"], "source": f"{f.name}"}
+    return best
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -197,11 +231,8 @@ def main():
 
     frames = args.frames or DEFAULT_FRAMES.get(args.sf, 4096)
     wl = Workload(args.sf, args.bw, frames, rank, dev)
-    gathered = (torch.empty(world * frames * PAYLOAD, dtype=torch.uint8, device=dev)
-                if world > 1 else None)
-
     mode_b = lphy.MODE_DECHIRP_LORA_DEMODULATE
-    dt = timed(wl, mode_b, args.steps, args.warmup, world, gathered)
+    dt = timed(wl, mode_b, args.steps, args.warmup, world)
     ms = dt / args.steps * 1e3
     data_syms = world * frames * DATA_SYMS
     value = data_syms * args.steps / dt
@@ -209,15 +240,18 @@ def main():
     st = wl.stage_times(mode_b)
 
     N = wl.N
-    # dominant kernel = per-symbol demod: reads every IQ sample once, writes
-    # one u16 per data symbol (sync bins go to the 32-B frame record)
-    sym_bytes = frames * (wl.fs * 8 + DATA_SYMS * 2)
-    achieved = sym_bytes / (st["symbols"] * 1e-3) / 1e9
+    # dominant kernel = the fused k_frames launch: algorithmic bytes = every
+    # IQ sample once + one u16 per data symbol + the 32-B frame record
+    # (its own max-abs pre-scan re-reads the frame, which the
+    # PMC traffic below shows)
+    kern_bytes = frames * (wl.fs * 8 + DATA_SYMS * 2 + 32)
+    achieved = kern_bytes / (st["fused"] * 1e-3) / 1e9
     step_gbps = frames * DATA_SYMS * bytes_per_data_symbol(N) / (ms * 1e-3) / 1e9
+    traffic = measured_traffic(f"k_frames<{args.sf}>", frames)
 
     extra = {}
     if not args.no_mode_a:
-        dta = timed(wl, lphy.MODE_DEMODULATE, max(3, args.steps // 2), 1, world, gathered)
+        dta = timed(wl, lphy.MODE_DEMODULATE, max(3, args.steps // 2), 1, world)
         extra["demodulate_mode_A"] = {
             "value": data_syms * max(3, args.steps // 2) / dta, "unit": "data symbols/s",
             "check": wl.check(lphy.MODE_DEMODULATE)}
@@ -227,11 +261,11 @@ def main():
         for sf in range(8, 13):
             w2 = Workload(sf, args.bw, DEFAULT_FRAMES[sf] // 4, rank, dev)
             d2 = timed(w2, mode_b, 3, 1, 1)
-            s2 = w2.stage_times(mode_b, 1)
+            k2 = w2._event_ms(mode_b, lphy.F_DECODE | lphy.F_STAGE_PROLOGUE | lphy.F_STAGE_SYMBOLS, 2)
             sweep[f"SF{sf}"] = {"value": w2.frames * DATA_SYMS * 3 / d2,
                                 "frames": w2.frames,
-                                "symbols_kernel_frac_hbm": w2.frames * (w2.fs * 8 + DATA_SYMS * 2)
-                                / (s2["symbols"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                                "kernel_frac_hbm": w2.frames * (w2.fs * 8 + DATA_SYMS * 2 + 32)
+                                / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                                 "check": w2.check(mode_b)["payloads_recovered"]}
             del w2
             torch.cuda.empty_cache()
@@ -269,10 +303,12 @@ def main():
             },
             "hbm_gbps_step": step_gbps,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                         "kernel": f"k_demod<{args.sf}>",
-                         "bytes_per_launch": sym_bytes,
-                         "avg_launch_ms": st["symbols"]},
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
+                         "traffic": traffic["bytes"] if traffic else None,
+                         "traffic_source": traffic["source"] if traffic else None,
+                         "kernel": f"k_frames<{args.sf}>" if frames_fused(args.sf) else f"k_demod<{args.sf}>",
+                         "bytes_per_launch": kern_bytes,
+                         "avg_launch_ms": st["fused"]},
             "stage_ms": st,
             "check": check_b,
             "cpu_baseline": cpu,

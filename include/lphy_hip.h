@@ -77,7 +77,9 @@ enum lphy_flags {
     LPHY_F_NO_SCRATCH = 2u,  /* modes 1/2: behave as lora_demodulate with no
                                 scratch buffer (-ERANGE when rescale needed) */
     /* Stage selection (profiling / overlap): when any of these bits is set
-     * only the selected stages are launched; none set = all three. */
+     * only the selected stages are launched; none set = all three.  With
+     * PROLOGUE | SYMBOLS both set, the fused kernel (when it applies) runs
+     * both in one launch. */
     LPHY_F_STAGE_PROLOGUE = 4u,  /* per-frame max-abs + offset estimate   */
     LPHY_F_STAGE_SYMBOLS = 8u,   /* per-symbol rotate + FFT + argmax      */
     LPHY_F_STAGE_FINAL = 16u,    /* per-frame sync word, decode, CRC      */

@@ -1437,9 +1437,11 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
         return -ERANGE;
     const unsigned stages = flags & (LPHY_F_STAGE_PROLOGUE | LPHY_F_STAGE_SYMBOLS | LPHY_F_STAGE_FINAL);
     const bool all = stages == 0;
-    // one fused launch when the frame shape allows it (see k_frames)
-    const bool fused = all && !(flags & LPHY_F_UNFUSED) && fused_enabled() &&
-                       frames_fit(c->sf, c->osr, A.est_units, total);
+    // one fused launch for prologue + symbols when the frame shape allows it
+    // (see k_frames); selecting exactly those two stages runs it alone
+    const unsigned both = LPHY_F_STAGE_PROLOGUE | LPHY_F_STAGE_SYMBOLS;
+    const bool fused = (all || (stages & both) == both) && !(flags & LPHY_F_UNFUSED) &&
+                       fused_enabled() && frames_fit(c->sf, c->osr, A.est_units, total);
     int rc = fused ? launch_frames(c->sf, A, st)
                    : launch_demod(c->sf, A, st, all || (stages & LPHY_F_STAGE_PROLOGUE),
                                   all || (stages & LPHY_F_STAGE_SYMBOLS));
