@@ -42,6 +42,18 @@ using namespace lphy;
 namespace {
 
 constexpr float kPi = 3.14159265358979323846f;  // lora_phy::PI (phy.hpp:20)
+// Kernel MODE template argument: the lphy_mode in bits 0-1, plus kWinBit when
+// a window is applied, so the per-sample window multiply is compile-time
+// (a runtime branch per sample would split the staging block and serialise
+// the 16 independent sincos chains of a lane).
+constexpr int kWinBit = 4;
+
+#ifdef LPHY_PROFILE_PHASES
+__device__ unsigned long long g_phase_cycles[4];
+#endif
+
+// Experiments only: -DLPHY_ONLY_SF=n instantiates the kernels of one SF
+// (the launch switches below); the default build has every SF.
 
 // ---------------------------------------------------------------------------
 // Per-launch parameters
@@ -382,10 +394,10 @@ template <int SF, int MODE>
 __device__ __forceinline__ cf32 rotate_sample(cf32 x, int i, const SymCtx& c,
                                               const cf32* down, const float* win, bool large) {
     constexpr int N = 1 << SF;
-    if constexpr (MODE == LPHY_MODE_DEMODULATE) {
+    if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) {
         x = cmul(x, down[i]);  // phy.cpp:219-220: down-chirp of the window
     } else {
-        if constexpr (MODE == LPHY_MODE_DECHIRP_LORA_DEMODULATE) {
+        if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) {
             // the external dechirp ran on the unshifted buffer
             // (e2e_chain_test.cpp:88-93): chirp index of the absolute sample
             // (frames hold whole symbols in this mode)
@@ -405,7 +417,7 @@ __device__ __forceinline__ cf32 rotate_sample(cf32 x, int i, const SymCtx& c,
     else lphy_libm::sincosf_fast(ph, &sn, &cs);
 #endif
     x = cmul(x, cf32{cs, sn});
-    if (win) x = cscale(x, win[i]);
+    if constexpr ((MODE & kWinBit) != 0) x = cscale(x, win[i]);
     return x;
 }
 
@@ -464,7 +476,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
     for (int i = tid; i < N; i += kTile) {
         twl[i] = A.tw[i];
         if constexpr (TAB) {
-            if (MODE != LPHY_MODE_LORA_DEMODULATE) dnl[i] = A.down[i];
+            if ((MODE & 3) != LPHY_MODE_LORA_DEMODULATE) dnl[i] = A.down[i];
             if (A.win) wnl[i] = A.win[i];
         }
     }
@@ -503,7 +515,13 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
         for (int e = 0; e < G::E; ++e) raw[e] = src[lam + e * G::LPS];
     }
 
+#ifdef LPHY_PROFILE_PHASES  // timing experiments only: per-phase clock sums
+    unsigned long long ph_stage = 0, ph_fft = 0, ph_tail = 0;
+#endif
     while (fw < nframes) {
+#ifdef LPHY_PROFILE_PHASES
+        const unsigned long long p0 = clock64();
+#endif
         // next tile: coordinates and frame record (in flight during staging)
         unsigned nf = f, ns = s, nfw = fw, nsw = sw;
         step(nf, ns);
@@ -515,6 +533,9 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
         stage_symbol<SF, MODE>(lds, stg, raw, A.iq + (unsigned long long)c.f * A.frame_samples + c.base,
                                c, lam, down, win);
         team_sync<SF>();
+#ifdef LPHY_PROFILE_PHASES
+        const unsigned long long p1 = clock64();
+#endif
 
         // next tile's IQ: in flight during this tile's FFT
         const SymCtx nc = sym_ctx(A, nlive ? nf : 0, nlive ? ns : 0, nlive, N, nm);
@@ -540,12 +561,26 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
 #else
         fft_tile<SF>(v, lds, slot, lam, twl);
 #endif
+#ifdef LPHY_PROFILE_PHASES
+        const unsigned long long p2 = clock64();
+#endif
         const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), red);
         if (c.ok && lam == 0) store_symbol(A, c, (uint16_t)best.i);
         if constexpr (WAVE) team_sync<SF>();  // slot reads done before restaging
         c = nc;
         f = nf; s = ns; fw = nfw; sw = nsw;
+#ifdef LPHY_PROFILE_PHASES
+        const unsigned long long p3 = clock64();
+        ph_stage += p1 - p0; ph_fft += p2 - p1; ph_tail += p3 - p2;
+#endif
     }
+#ifdef LPHY_PROFILE_PHASES
+    if ((tid & 63) == 0) {
+        atomicAdd(&g_phase_cycles[0], ph_stage);
+        atomicAdd(&g_phase_cycles[1], ph_fft);
+        atomicAdd(&g_phase_cycles[2], ph_tail);
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -558,12 +593,14 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
 //   D  the frame's symbols (rotation, FFT, argmax)
 // The wave works through a stream of "units" in tiles of WT = 64/LPS, one
 // unit per team of LPS lanes:
-//   [E(0) x2, pad to a tile] then per frame k: [E(k+1) x2, D(k) x S]
+//   [E(0) x2, pad, one spacer tile] then per frame k (a "slice"):
+//   [D(k) x PE, E(k+1) x2, D(k) x (S - PE)],   PE = S + 1 - 2 WT
 // so the estimate of frame k+1 shares tiles with symbols of frame k and no
-// team idles; E(k+1) lies >= S + 2 units ahead of D(k+1), i.e. (with
-// S + 3 >= 2 WT, checked on the host) at least two tiles, which is what the
-// one-tile-ahead IQ prefetch needs.  M(k) runs right before the tile
-// holding E(k)'s first unit.  Frame records pass between teams through a
+// team idles, and E(k+1) leads D(k+1) by 2 WT units (two tiles: what the
+// one-tile-ahead IQ prefetch needs).  M(k+1) runs right before the tile
+// holding E(k+1)'s first unit, one slice before D(k+1) re-reads the frame
+// (Infinity-Cache distance).  (Streaming M in row chunks between tiles,
+// held in registers across the FFT, spilled and ran 1.35x slower.)  Frame records pass between teams through a
 // 3-slot ring per wave in LDS.  Compared with separate launches this
 // removes a whole-batch pass (the prologue kernels) and overlaps the
 // HBM-bound max-abs scans of some waves with the VALU-bound transforms of
@@ -601,14 +638,17 @@ __device__ __forceinline__ float wave_maxabs(const DemodArgs& A, unsigned f, con
     const unsigned dech_end = (unsigned)A.total_syms * N;
     float mx = 0.0f;
     auto acc = [&](cf32 x, unsigned i) {
-        if constexpr (MODE == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+        if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
             x = i < dech_end ? cmul(x, down[i & (N - 1)]) : czero();
         maxabs_acc(mx, x);
     };
     if ((reinterpret_cast<uintptr_t>(fr) & 15) == 0) {
         const float4* f4 = reinterpret_cast<const float4*>(fr);
         const unsigned n4 = count / 2;
-        constexpr int U = 8;
+#ifndef LPHY_MAXABS_U
+#define LPHY_MAXABS_U 16
+#endif
+        constexpr int U = LPHY_MAXABS_U;  // loads in flight per lane
         unsigned j = lane;
         for (; j + (U - 1) * 64 < n4; j += U * 64) {
             float4 v[U];
@@ -652,10 +692,10 @@ __device__ __forceinline__ void stage_mixed(cf32* lds, const Stage<SF>& stg, con
         const int i = lam + e * G::LPS;
         cf32 x = raw[e];
         cf32 pre;  // input of the rotation
-        if constexpr (MODE == LPHY_MODE_DEMODULATE) {
+        if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) {
             pre = cmul(x, down[i]);
         } else {
-            if constexpr (MODE == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+            if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
                 x = cmul(x, down[((unsigned)c.base + (unsigned)i) & (N - 1)]);
             x = cscale(x, c.scale);
             pre = x;
@@ -665,7 +705,7 @@ __device__ __forceinline__ void stage_mixed(cf32* lds, const Stage<SF>& stg, con
         lphy_libm::sincosf_fast(ph, &sn, &cs);
         cf32 y = cmul(pre, cf32{cs, sn});
         y = est ? (c.ok ? x : czero()) : y;
-        if (win) y = cscale(y, win[i]);
+        if constexpr ((MODE & kWinBit) != 0) y = cscale(y, win[i]);
         stg.put(lds, e, y);
     }
     if (!est && (lphy_libm::sincosf_needs_large(c.start + c.rate * (float)lam) ||
@@ -704,7 +744,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     for (int i = tid; i < N; i += kTile) {
         twl[i] = A.tw[i];
         if constexpr (TAB) {
-            if (MODE != LPHY_MODE_LORA_DEMODULATE) dnl[i] = A.down[i];
+            if ((MODE & 3) != LPHY_MODE_LORA_DEMODULATE) dnl[i] = A.down[i];
             if (A.win) wnl[i] = A.win[i];
         }
     }
@@ -718,6 +758,9 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     const Stage<SF> stg(slot, lam);
     const unsigned nframes = (unsigned)A.frames;
     const unsigned S = (unsigned)A.total_syms, SL = U + S;
+    // offset of E(k+1) inside slice k: as late as the two-tile lead over
+    // D(k+1) allows (frames_fit guarantees S + 1 >= 2 WT)
+    const unsigned PE = S + 1 - 2 * WT;
     const unsigned W = P.waves;
     const unsigned w = blockIdx.x * WPB + wv;
     if (w >= nframes) return;
@@ -733,14 +776,14 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             kind = q < U ? kUnitEst : kUnitDead;
             fk = 0;
             s = q;
-        } else if (o < U) {
+        } else if (o >= PE && o < PE + U) {
             kind = k + 1 < nk ? kUnitEst : kUnitDead;
             fk = k + 1;
-            s = o;
+            s = o - PE;
         } else {
             kind = k < nk ? kUnitSym : kUnitDead;
             fk = k;
-            s = o - U;
+            s = o < PE ? o : o - U;
         }
     };
     // context of a unit; symbol units read their frame record from the ring
@@ -785,12 +828,12 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         unsigned ke = 0;
         if (emask) {
             ke = (unsigned)__shfl((int)fk, __ffsll((long long)emask) - 1, 64);
-            if (MODE != LPHY_MODE_DEMODULATE && ke != m_seq) {
+            if ((MODE & 3) != LPHY_MODE_DEMODULATE && ke != m_seq) {
                 mx = wave_maxabs<SF, MODE>(A, w + ke * W, down);
                 m_seq = ke;
             }
             if (kind == kUnitEst) {
-                if (MODE != LPHY_MODE_DEMODULATE) {
+                if ((MODE & 3) != LPHY_MODE_DEMODULATE) {
                     const lphy_frame_meta nm = norm_meta(mx, true, A.no_scratch);
                     c.scale = nm.scale;
                     c.live = nm.status == 0;
@@ -848,7 +891,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             lphy_frame_meta m{};
             m.scale = 1.0f;
             m.have_sync = 1;
-            if (MODE != LPHY_MODE_DEMODULATE) m = norm_meta(mx, true, A.no_scratch);
+            if ((MODE & 3) != LPHY_MODE_DEMODULATE) m = norm_meta(mx, true, A.no_scratch);
             if (m.status == 0) {
                 EstFold fold;
 #pragma unroll
@@ -1223,9 +1266,15 @@ inline bool frames_fit(unsigned sf, unsigned osr, int est_units, size_t total) {
     const size_t E = sf >= 4 ? 16 : ((size_t)1 << sf);
     const size_t lps = ((size_t)1 << sf) / E;
     const size_t wt = 64 / lps;
-    return total + 3 >= 2 * wt;
+    return total + 1 >= 2 * wt;
 }
 
+
+template <int SF, int MODE>
+void launch_symbols_w(const DemodArgs& A, unsigned long long tiles, hipStream_t st) {
+    if (A.win) launch_symbols<SF, MODE | kWinBit>(A, tiles, st);
+    else launch_symbols<SF, MODE>(A, tiles, st);
+}
 
 template <int SF>
 int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symbols) {
@@ -1242,9 +1291,9 @@ int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symb
         const unsigned long long tiles = (nsym + G::T - 1) / G::T;
         if (tiles) {
             switch (A.mode) {
-                case LPHY_MODE_DEMODULATE: launch_symbols<SF, LPHY_MODE_DEMODULATE>(A, tiles, st); break;
-                case LPHY_MODE_LORA_DEMODULATE: launch_symbols<SF, LPHY_MODE_LORA_DEMODULATE>(A, tiles, st); break;
-                default: launch_symbols<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>(A, tiles, st); break;
+                case LPHY_MODE_DEMODULATE: launch_symbols_w<SF, LPHY_MODE_DEMODULATE>(A, tiles, st); break;
+                case LPHY_MODE_LORA_DEMODULATE: launch_symbols_w<SF, LPHY_MODE_LORA_DEMODULATE>(A, tiles, st); break;
+                default: launch_symbols_w<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>(A, tiles, st); break;
             }
         }
     }
@@ -1254,18 +1303,42 @@ int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symb
 
 int launch_demod(unsigned sf, const DemodArgs& A, hipStream_t st, bool pro, bool sym) {
     switch (sf) {
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 1
         case 1: return launch_demod_sf<1>(A, st, pro, sym);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 2
         case 2: return launch_demod_sf<2>(A, st, pro, sym);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 3
         case 3: return launch_demod_sf<3>(A, st, pro, sym);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 4
         case 4: return launch_demod_sf<4>(A, st, pro, sym);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 5
         case 5: return launch_demod_sf<5>(A, st, pro, sym);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 6
         case 6: return launch_demod_sf<6>(A, st, pro, sym);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 7
         case 7: return launch_demod_sf<7>(A, st, pro, sym);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 8
         case 8: return launch_demod_sf<8>(A, st, pro, sym);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 9
         case 9: return launch_demod_sf<9>(A, st, pro, sym);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 10
         case 10: return launch_demod_sf<10>(A, st, pro, sym);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 11
         case 11: return launch_demod_sf<11>(A, st, pro, sym);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 12
         case 12: return launch_demod_sf<12>(A, st, pro, sym);
+#endif
         default: return -EINVAL;
     }
 }
@@ -1277,25 +1350,51 @@ int launch_frames_sf(const DemodArgs& A, hipStream_t st) {
         return -ENOTSUP;
     } else {
         switch (A.mode) {
-            case LPHY_MODE_DEMODULATE: return launch_frames_mode<SF, LPHY_MODE_DEMODULATE>(A, st);
-            case LPHY_MODE_LORA_DEMODULATE: return launch_frames_mode<SF, LPHY_MODE_LORA_DEMODULATE>(A, st);
-            default: return launch_frames_mode<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>(A, st);
+            case LPHY_MODE_DEMODULATE:
+                return A.win ? launch_frames_mode<SF, LPHY_MODE_DEMODULATE | kWinBit>(A, st)
+                             : launch_frames_mode<SF, LPHY_MODE_DEMODULATE>(A, st);
+            case LPHY_MODE_LORA_DEMODULATE:
+                return A.win ? launch_frames_mode<SF, LPHY_MODE_LORA_DEMODULATE | kWinBit>(A, st)
+                             : launch_frames_mode<SF, LPHY_MODE_LORA_DEMODULATE>(A, st);
+            default:
+                return A.win ? launch_frames_mode<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE | kWinBit>(A, st)
+                             : launch_frames_mode<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>(A, st);
         }
     }
 }
 
 int launch_frames(unsigned sf, const DemodArgs& A, hipStream_t st) {
     switch (sf) {
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 1
         case 1: return launch_frames_sf<1>(A, st);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 2
         case 2: return launch_frames_sf<2>(A, st);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 3
         case 3: return launch_frames_sf<3>(A, st);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 4
         case 4: return launch_frames_sf<4>(A, st);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 5
         case 5: return launch_frames_sf<5>(A, st);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 6
         case 6: return launch_frames_sf<6>(A, st);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 7
         case 7: return launch_frames_sf<7>(A, st);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 8
         case 8: return launch_frames_sf<8>(A, st);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 9
         case 9: return launch_frames_sf<9>(A, st);
+#endif
+#if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 10
         case 10: return launch_frames_sf<10>(A, st);
+#endif
         default: return -ENOTSUP;
     }
 }
@@ -1461,6 +1560,17 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     HIP_OK(hipGetLastError());
     return 0;
 }
+
+#ifdef LPHY_PROFILE_PHASES
+// experiments only: read and clear k_demod's per-phase clock sums
+int lphy_hip_phase_cycles(unsigned long long* out4) {
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_phase_cycles), 4 * sizeof(unsigned long long)));
+    unsigned long long z[4] = {0, 0, 0, 0};
+    HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof(z)));
+    return 0;
+}
+#endif
 
 int lphy_hip_decode_batch(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames,
                           size_t syms_per_frame, uint8_t* d_bytes, lphy_frame_meta* d_meta,
