@@ -599,9 +599,12 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
 // team idles, and E(k+1) leads D(k+1) by 2 WT units (two tiles: what the
 // one-tile-ahead IQ prefetch needs).  M(k+1) runs right before the tile
 // holding E(k+1)'s first unit, one slice before D(k+1) re-reads the frame
-// (Infinity-Cache distance).  (Streaming M in row chunks between tiles,
-// held in registers across the FFT, spilled and ran 1.35x slower.)  Frame records pass between teams through a
-// 3-slot ring per wave in LDS.  Compared with separate launches this
+// (Infinity-Cache distance).  Measured alternatives, all slower at SF7 than
+// this blocking 16-deep scan (2.3 ms per 65,536 frames): M streamed in row
+// chunks held in registers across the FFT (spills, 1.35x), M streamed by
+// LDS-DMA into a per-wave ring (1.15x), scan-only workgroups beside the
+// symbol waves (1.3-5x: they need ~25 % of the slots to stay ahead).
+// Frame records pass between teams through a 3-slot ring per wave in LDS.  Compared with separate launches this
 // removes a whole-batch pass (the prologue kernels) and overlaps the
 // HBM-bound max-abs scans of some waves with the VALU-bound transforms of
 // the others.
