@@ -64,18 +64,23 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-mode-a", action="store_true")
     ap.add_argument("--sweep", action="store_true", help="also time SF8..SF12 (extra field)")
+    ap.add_argument("--config", default="c1", choices=["c1", "c2", "c3", "c4"],
+                    help="BASELINE.json config: c1 SF7 x 65,536 (headline, default), c2 SF12 x "
+                         "4,096, c3 mixed SF7-12 (1M frames over the ranks), c4 SF9 AWGN BER")
+    ap.add_argument("--total-frames", type=int, default=1 << 20, help="c3: frames over all ranks")
     return ap.parse_args()
 
 
 class Workload:
     """One SF configuration resident on this rank's GPU."""
 
-    def __init__(self, sf: int, bw: int, frames: int, rank: int, dev: torch.device):
+    def __init__(self, sf: int, bw: int, frames: int, rank: int, dev: torch.device, payloads=None):
         self.sf, self.N, self.bw, self.frames = sf, 1 << sf, bw, frames
         self.fs = TOTAL_SYMS * self.N
         self.dem = lphy.Demodulator(sf, bw, 1, lphy.WINDOW_NONE, device=dev.index)
         rng = np.random.default_rng(0x5EED + 7919 * rank + sf)
-        self.payloads = rng.integers(0, 256, (frames, PAYLOAD), dtype=np.uint8)
+        self.payloads = (payloads if payloads is not None
+                         else rng.integers(0, 256, (frames, PAYLOAD), dtype=np.uint8))
         syms = lphy.encode_payloads(self.payloads)
         stream = torch.cuda.current_stream().cuda_stream
         t_in = torch.from_numpy(syms.view(np.int16).reshape(-1).copy()).to(dev)
@@ -218,6 +223,113 @@ def measured_traffic(kernel: str, frames: int):
     return best
 
 
+def _sync_time(fn, steps, warmup, world, dev):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+def run_c3(args, baseline, world, rank, dev) -> dict:
+    """C3: mixed SF7-12 stream, `--total-frames` frames with SF drawn
+    uniformly (seeded), split across ranks by cost-balanced contiguous
+    ranges (sum of 66 N log2 N), bucketed by SF on each rank
+    (one resident batch and one launch per SF); payloads gathered."""
+    total = args.total_frames
+    rng = np.random.default_rng(0xC3)
+    sfs = rng.integers(7, 13, total)
+    cost = (1 << sfs) * sfs.astype(np.float64)
+    first, count = shard.balanced_ranges(cost, world)[rank]
+    mine = sfs[first:first + count]
+    pay_rng = np.random.default_rng(0xC3 + 1)
+    payloads = pay_rng.integers(0, 256, (total, PAYLOAD), dtype=np.uint8)[first:first + count]
+    buckets = []
+    for sf in range(7, 13):
+        idx = np.nonzero(mine == sf)[0]
+        if idx.size:
+            buckets.append(Workload(sf, args.bw, int(idx.size), rank, dev, payloads=payloads[idx]))
+    mode_b = lphy.MODE_DECHIRP_LORA_DEMODULATE
+
+    def step():
+        for wl in buckets:
+            wl.run(mode_b)
+        if world > 1:
+            for wl in buckets:  # the only exchange: decoded payloads
+                shard.gather_varlen(wl.pay)
+    steps = max(2, args.steps // 4)
+    dt = _sync_time(step, steps, 1, world, dev)
+    syms = torch.tensor([sum(w.frames for w in buckets) * DATA_SYMS], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(syms)
+    ok = sum(w.check(mode_b)["payloads_recovered"] for w in buckets)
+    per_sf = {f"SF{w.sf}": w.frames for w in buckets}
+    iq_gb = sum(w.frames * w.fs * 8 for w in buckets) / 1e9
+    return {"metric": baseline["metric"], "value": float(syms.item()) * steps / dt,
+            "unit": "data symbols/s", "n_gpus": world, "steps": steps, "warmup": 1,
+            "ms_per_step": dt / steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (device-generated lora_modulate IQ of random payloads)",
+            "config": {"workload": f"C3 mixed SF7-12, {total} frames over {world} rank(s), "
+                                   "cost-balanced shards, one launch per SF bucket",
+                       "frames_this_rank": int(count), "frames_per_sf_rank0": per_sf,
+                       "iq_gb_rank0": iq_gb, "parallelism": f"frames sharded x{world}"},
+            "check": {"payloads_recovered": ok, "frames": int(count)}}
+
+
+def run_c4(args, baseline, world, rank, dev) -> dict:
+    """C4: SF9 BW125 under AWGN (sigma = sqrt(10^(-SNR/10)/2) per component,
+    unit-power signal; SNR -10 and -15 dB), symbol / bit error rates of the
+    GPU path against the transmitted payloads, and bit-exactness with the
+    CPU oracle / reference on a sample of the same noisy frames."""
+    sf = 9
+    frames = args.frames or DEFAULT_FRAMES[sf]
+    out = {}
+    value = None
+    for snr in (-10.0, -15.0):
+        wl = Workload(sf, args.bw, frames, rank, dev)
+        g = torch.Generator(device=dev)
+        g.manual_seed(0xC4 + int(-snr) + 7919 * rank)
+        sig = float(np.sqrt(10 ** (-snr / 10) / 2))
+        wl.iq.add_(torch.randn(wl.iq.shape, generator=g, device=dev) * sig)
+        mode_b = lphy.MODE_DECHIRP_LORA_DEMODULATE
+        steps = max(3, args.steps // 4)
+        dt = _sync_time(lambda: wl.run(mode_b), steps, 1, world, dev)
+        if value is None:
+            value = world * frames * DATA_SYMS * steps / dt
+        torch.cuda.synchronize()
+        sent = lphy.encode_payloads(wl.payloads)
+        got = wl.syms.cpu().numpy().view(np.uint16).reshape(frames, DATA_SYMS)
+        pay = wl.pay.cpu().numpy().reshape(frames, PAYLOAD)
+        ser = float((got != sent).mean())
+        ber = float(np.unpackbits(pay ^ wl.payloads).mean())
+        chk = wl.check(mode_b)
+        out[f"snr_{int(snr)}dB"] = {"ser": ser, "ber": ber, "frames": frames,
+                                    "frame_error_rate": float((pay != wl.payloads).any(axis=1).mean()),
+                                    "oracle_frames_bit_exact": chk["oracle_frames_bit_exact"]}
+        del wl
+        torch.cuda.empty_cache()
+    return {"metric": baseline["metric"], "value": value, "unit": "data symbols/s",
+            "n_gpus": world, "steps": max(3, args.steps // 4), "warmup": 1,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: device lora_modulate IQ + torch AWGN",
+            "config": {"workload": f"C4 SF9 BW125 AWGN, {frames} frames/GPU", "sf": sf,
+                       "parallelism": f"frames sharded x{world}"},
+            "awgn": out}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -228,6 +340,16 @@ def main():
     if world > 1:
         torch.distributed.init_process_group("nccl", device_id=dev)
     baseline = json.loads((ROOT / "BASELINE.json").read_text())
+    if args.config == "c2":
+        args.sf = 12
+        args.frames = args.frames or 4096
+    elif args.config in ("c3", "c4"):
+        line = (run_c3 if args.config == "c3" else run_c4)(args, baseline, world, rank, dev)
+        if rank == 0:
+            print(json.dumps(line))
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
 
     frames = args.frames or DEFAULT_FRAMES.get(args.sf, 4096)
     wl = Workload(args.sf, args.bw, frames, rank, dev)
@@ -244,10 +366,12 @@ def main():
     # IQ sample once + one u16 per data symbol + the 32-B frame record
     # (its own max-abs pre-scan re-reads the frame, which the
     # PMC traffic below shows)
-    kern_bytes = frames * (wl.fs * 8 + DATA_SYMS * 2 + 32)
-    achieved = kern_bytes / (st["fused"] * 1e-3) / 1e9
+    fused = frames_fused(args.sf)
+    kern_bytes = frames * (wl.fs * 8 + DATA_SYMS * 2 + (32 if fused else 0))
+    kern_ms = st["fused"] if fused else st["unfused_symbols"]
+    achieved = kern_bytes / (kern_ms * 1e-3) / 1e9
     step_gbps = frames * DATA_SYMS * bytes_per_data_symbol(N) / (ms * 1e-3) / 1e9
-    traffic = measured_traffic(f"k_frames<{args.sf}>", frames)
+    traffic = measured_traffic(f"k_frames<{args.sf}>" if fused else f"k_demod<{args.sf}>", frames)
 
     extra = {}
     if not args.no_mode_a:
@@ -306,9 +430,9 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic["bytes"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
-                         "kernel": f"k_frames<{args.sf}>" if frames_fused(args.sf) else f"k_demod<{args.sf}>",
+                         "kernel": f"k_frames<{args.sf}>" if fused else f"k_demod<{args.sf}>",
                          "bytes_per_launch": kern_bytes,
-                         "avg_launch_ms": st["fused"]},
+                         "avg_launch_ms": kern_ms},
             "stage_ms": st,
             "check": check_b,
             "cpu_baseline": cpu,

@@ -832,7 +832,11 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         if (emask) {
             ke = (unsigned)__shfl((int)fk, __ffsll((long long)emask) - 1, 64);
             if ((MODE & 3) != LPHY_MODE_DEMODULATE && ke != m_seq) {
+#ifdef LPHY_ABLATE_FRAME_SCAN  // timing experiments only
+                mx = 1.0f;
+#else
                 mx = wave_maxabs<SF, MODE>(A, w + ke * W, down);
+#endif
                 m_seq = ke;
             }
             if (kind == kUnitEst) {

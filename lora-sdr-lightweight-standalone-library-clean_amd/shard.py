@@ -20,6 +20,23 @@ def frame_range(total: int, world: int, rank: int) -> tuple[int, int]:
     return first, count
 
 
+def balanced_ranges(costs, world: int) -> list[tuple[int, int]]:
+    """Contiguous split of frames with per-frame `costs` into `world` ranges
+    of near-equal total cost (mixed SF balanced by
+    sum(66 N log2 N)); returns (first, count) per rank."""
+    import numpy as np
+    c = np.cumsum(np.asarray(costs, dtype=np.float64))
+    total = float(c[-1]) if c.size else 0.0
+    cuts = [0]
+    for r in range(1, world):
+        cuts.append(int(np.searchsorted(c, total * r / world, side="left")) + 1 if c.size else 0)
+    cuts.append(len(c))
+    cuts = [min(max(x, 0), len(c)) for x in cuts]
+    for i in range(1, len(cuts)):
+        cuts[i] = max(cuts[i], cuts[i - 1])
+    return [(cuts[r], cuts[r + 1] - cuts[r]) for r in range(world)]
+
+
 def gather_payloads(local: torch.Tensor, frames: int, payload: int, total: int,
                     group=None) -> torch.Tensor:
     """All ranks' decoded payloads (uint8, frames*payload each, frame_range
@@ -44,3 +61,23 @@ def gather_payloads(local: torch.Tensor, frames: int, payload: int, total: int,
     if all(c * payload == cap for c in counts):
         return out
     return torch.cat([out[r * cap: r * cap + counts[r] * payload] for r in range(world)])
+
+
+def gather_varlen(local: torch.Tensor, group=None) -> list[torch.Tensor]:
+    """All ranks' uint8 buffers of possibly different lengths (e.g. the
+    payloads of one SF bucket of a mixed-SF batch), in rank order, on every
+    rank: sizes first, then one padded all_gather."""
+    world = dist.get_world_size(group)
+    buf = local.reshape(-1)
+    n = torch.tensor([buf.numel()], dtype=torch.int64, device=local.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(x.item()) for x in sizes]
+    cap = max(sizes) if sizes else 0
+    if buf.numel() != cap:
+        pad = torch.zeros(cap, dtype=torch.uint8, device=local.device)
+        pad[: buf.numel()] = buf
+        buf = pad
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    return [p[:k] for p, k in zip(parts, sizes)]

@@ -72,3 +72,42 @@ def test_frame_range_partitions(total, world):
         assert a + n == b
     assert sum(n for _, n in spans) == total
     assert max(n for _, n in spans) - min(n for _, n in spans) <= 1
+
+
+def _varlen_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        local = torch.arange(3 + 4 * rank, dtype=torch.uint8)
+        parts = shard.gather_varlen(local)
+        q.put((rank, [p.tolist() for p in parts]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_varlen_two_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_varlen_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = [list(range(3)), list(range(7))]
+    assert res == {0: want, 1: want}
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_balanced_ranges_by_cost(world):
+    rng = np.random.default_rng(3)
+    sfs = rng.integers(7, 13, 20000)
+    cost = (1 << sfs) * sfs.astype(np.float64)
+    spans = shard.balanced_ranges(cost, world)
+    assert spans[0][0] == 0 and sum(n for _, n in spans) == sfs.size
+    for (a, n), (b, _) in zip(spans, spans[1:]):
+        assert a + n == b
+    loads = [cost[a:a + n].sum() for a, n in spans]
+    assert max(loads) - min(loads) <= 2.5 * cost.max()  # within a couple of frames
