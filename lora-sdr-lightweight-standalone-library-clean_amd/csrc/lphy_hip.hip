@@ -1189,13 +1189,27 @@ int demod_grid() {
     return grid;
 }
 
+inline int cu_count() {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (cus <= 0) cus = 256;
+    }
+    return cus;
+}
+
+// per_cu > 0 caps the persistent grid at per_cu workgroups per CU (room
+// for a concurrent kernel on another stream)
 template <int SF, int MODE, int OCC>
-void launch_symbols_occ(const DemodArgs& A0, unsigned long long tiles, hipStream_t st) {
+void launch_symbols_occ(const DemodArgs& A0, unsigned long long tiles, hipStream_t st, int per_cu) {
     using G = Geo<SF>;
     constexpr bool WAVE = G::LPS <= 64;
     constexpr int WT = WAVE ? 64 / G::LPS : G::T;      // symbols per worker tile
     constexpr int WPB = WAVE ? kTile / 64 : 1;         // workers per workgroup
-    const unsigned long long g = (unsigned long long)demod_grid<SF, MODE, OCC>();
+    unsigned long long g = (unsigned long long)demod_grid<SF, MODE, OCC>();
+    if (per_cu > 0 && g > (unsigned long long)per_cu * cu_count()) g = (unsigned long long)per_cu * cu_count();
     const unsigned long long wtiles = (A0.frames * A0.total_syms + WT - 1) / WT;
     unsigned long long grid = (wtiles + WPB - 1) / WPB;
     if (grid > g) grid = g;
@@ -1208,14 +1222,14 @@ void launch_symbols_occ(const DemodArgs& A0, unsigned long long tiles, hipStream
 }
 
 template <int SF, int MODE>
-void launch_symbols(const DemodArgs& A, unsigned long long tiles, hipStream_t st) {
+void launch_symbols(const DemodArgs& A, unsigned long long tiles, hipStream_t st, int per_cu) {
     if constexpr (SF <= 10) {
         if (demod_occ(SF) == 3) {
-            launch_symbols_occ<SF, MODE, 3>(A, tiles, st);
+            launch_symbols_occ<SF, MODE, 3>(A, tiles, st, per_cu);
             return;
         }
     }
-    launch_symbols_occ<SF, MODE, 2>(A, tiles, st);
+    launch_symbols_occ<SF, MODE, 2>(A, tiles, st, per_cu);
 }
 
 // Fused path (k_frames).
@@ -1278,13 +1292,13 @@ inline bool frames_fit(unsigned sf, unsigned osr, int est_units, size_t total) {
 
 
 template <int SF, int MODE>
-void launch_symbols_w(const DemodArgs& A, unsigned long long tiles, hipStream_t st) {
-    if (A.win) launch_symbols<SF, MODE | kWinBit>(A, tiles, st);
-    else launch_symbols<SF, MODE>(A, tiles, st);
+void launch_symbols_w(const DemodArgs& A, unsigned long long tiles, hipStream_t st, int per_cu) {
+    if (A.win) launch_symbols<SF, MODE | kWinBit>(A, tiles, st, per_cu);
+    else launch_symbols<SF, MODE>(A, tiles, st, per_cu);
 }
 
 template <int SF>
-int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symbols) {
+int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symbols, int per_cu) {
     using G = Geo<SF>;
     if (prologue) {
         if (A.mode != LPHY_MODE_DEMODULATE)
@@ -1298,9 +1312,9 @@ int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symb
         const unsigned long long tiles = (nsym + G::T - 1) / G::T;
         if (tiles) {
             switch (A.mode) {
-                case LPHY_MODE_DEMODULATE: launch_symbols_w<SF, LPHY_MODE_DEMODULATE>(A, tiles, st); break;
-                case LPHY_MODE_LORA_DEMODULATE: launch_symbols_w<SF, LPHY_MODE_LORA_DEMODULATE>(A, tiles, st); break;
-                default: launch_symbols_w<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>(A, tiles, st); break;
+                case LPHY_MODE_DEMODULATE: launch_symbols_w<SF, LPHY_MODE_DEMODULATE>(A, tiles, st, per_cu); break;
+                case LPHY_MODE_LORA_DEMODULATE: launch_symbols_w<SF, LPHY_MODE_LORA_DEMODULATE>(A, tiles, st, per_cu); break;
+                default: launch_symbols_w<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>(A, tiles, st, per_cu); break;
             }
         }
     }
@@ -1308,43 +1322,43 @@ int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symb
     return 0;
 }
 
-int launch_demod(unsigned sf, const DemodArgs& A, hipStream_t st, bool pro, bool sym) {
+int launch_demod(unsigned sf, const DemodArgs& A, hipStream_t st, bool pro, bool sym, int per_cu = 0) {
     switch (sf) {
 #if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 1
-        case 1: return launch_demod_sf<1>(A, st, pro, sym);
+        case 1: return launch_demod_sf<1>(A, st, pro, sym, per_cu);
 #endif
 #if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 2
-        case 2: return launch_demod_sf<2>(A, st, pro, sym);
+        case 2: return launch_demod_sf<2>(A, st, pro, sym, per_cu);
 #endif
 #if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 3
-        case 3: return launch_demod_sf<3>(A, st, pro, sym);
+        case 3: return launch_demod_sf<3>(A, st, pro, sym, per_cu);
 #endif
 #if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 4
-        case 4: return launch_demod_sf<4>(A, st, pro, sym);
+        case 4: return launch_demod_sf<4>(A, st, pro, sym, per_cu);
 #endif
 #if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 5
-        case 5: return launch_demod_sf<5>(A, st, pro, sym);
+        case 5: return launch_demod_sf<5>(A, st, pro, sym, per_cu);
 #endif
 #if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 6
-        case 6: return launch_demod_sf<6>(A, st, pro, sym);
+        case 6: return launch_demod_sf<6>(A, st, pro, sym, per_cu);
 #endif
 #if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 7
-        case 7: return launch_demod_sf<7>(A, st, pro, sym);
+        case 7: return launch_demod_sf<7>(A, st, pro, sym, per_cu);
 #endif
 #if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 8
-        case 8: return launch_demod_sf<8>(A, st, pro, sym);
+        case 8: return launch_demod_sf<8>(A, st, pro, sym, per_cu);
 #endif
 #if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 9
-        case 9: return launch_demod_sf<9>(A, st, pro, sym);
+        case 9: return launch_demod_sf<9>(A, st, pro, sym, per_cu);
 #endif
 #if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 10
-        case 10: return launch_demod_sf<10>(A, st, pro, sym);
+        case 10: return launch_demod_sf<10>(A, st, pro, sym, per_cu);
 #endif
 #if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 11
-        case 11: return launch_demod_sf<11>(A, st, pro, sym);
+        case 11: return launch_demod_sf<11>(A, st, pro, sym, per_cu);
 #endif
 #if !defined(LPHY_ONLY_SF) || LPHY_ONLY_SF == 12
-        case 12: return launch_demod_sf<12>(A, st, pro, sym);
+        case 12: return launch_demod_sf<12>(A, st, pro, sym, per_cu);
 #endif
         default: return -EINVAL;
     }
@@ -1546,6 +1560,9 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     // one fused launch for prologue + symbols when the frame shape allows it
     // (see k_frames); selecting exactly those two stages runs it alone
     const unsigned both = LPHY_F_STAGE_PROLOGUE | LPHY_F_STAGE_SYMBOLS;
+    // (Measured alternative: the separate kernels pipelined over chunks on
+    // two streams, prologue of chunk c+1 beside the symbol kernel of chunk
+    // c: the co-running kernels slowed each other ~2x, 1.1x slower overall.)
     const bool fused = (all || (stages & both) == both) && !(flags & LPHY_F_UNFUSED) &&
                        fused_enabled() && frames_fit(c->sf, c->osr, A.est_units, total);
     int rc = fused ? launch_frames(c->sf, A, st)
