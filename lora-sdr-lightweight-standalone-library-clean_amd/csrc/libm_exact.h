@@ -303,4 +303,110 @@ LPHY_HD float cabsf_exact(float re, float im) {
 #endif
 }
 
+// logf as glibc 2.35 computes it (the table-driven double-precision
+// evaluation that replaced fdlibm's in glibc 2.28): x = 2^k * z with z in
+// [0x3f330000, 2*0x3f330000), 16 sub-intervals each with a tabulated
+// 1/c and log(c), then a degree-3 polynomial in r = z/c - 1.  Only normal
+// positive inputs reach it from the detector; the special cases follow
+// glibc for completeness.  CONTRACT selects whether the double-precision
+// multiply-adds are fused (x86-64 glibc builds are not; see the host check).
+template <bool CONTRACT>
+LPHY_HD double logf_eval(uint32_t ix) {
+    constexpr uint32_t OFF = 0x3f330000u;
+    constexpr double Ln2 = 0x1.62e42fefa39efp-1;
+    constexpr double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2,
+                     A2 = -0x1.ffffef20a4123p-2;
+    constexpr double invc_t[16] = {
+        0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010b0p+0,
+        0x1.3c995b0b80385p+0, 0x1.30d190c8864a5p+0, 0x1.25e227b0b8ea0p+0,
+        0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0, 0x1.0953f419900a7p+0,
+        0x1.0000000000000p+0, 0x1.e608cfd9a47acp-1, 0x1.ca4b31f026aa0p-1,
+        0x1.b2036576afce6p-1, 0x1.9c2d163a1aa2dp-1, 0x1.886e6037841edp-1,
+        0x1.767dcf5534862p-1};
+    constexpr double logc_t[16] = {
+        -0x1.57bf7808caadep-2, -0x1.2bef0a7c06ddbp-2, -0x1.01eae7f513a67p-2,
+        -0x1.b31d8a68224e9p-3, -0x1.6574f0ac07758p-3, -0x1.1aa2bc79c8100p-3,
+        -0x1.a4e76ce8c0e5ep-4, -0x1.1973c5a611cccp-4, -0x1.252f438e10c1ep-5,
+        0x0.0p+0,              0x1.aa5aa5df25984p-5,  0x1.c5e53aa362eb4p-4,
+        0x1.526e57720db08p-3,  0x1.bc2860d224770p-3,  0x1.1058bc8a07ee1p-2,
+        0x1.4043057b6ee09p-2};
+    uint32_t tmp = ix - OFF;
+    int i = (int)((tmp >> 19) % 16u);
+    int k = (int32_t)tmp >> 23;
+    uint32_t iz = ix - (tmp & 0xff800000u);
+    double invc = invc_t[i], logc = logc_t[i];
+    double z = (double)u2f(iz);
+    double r, y0, y;
+    if (CONTRACT) {
+        r = dfma(z, invc, -1.0);
+        y0 = dfma((double)k, Ln2, logc);
+        double r2 = r * r;
+        y = dfma(A1, r, A2);
+        y = dfma(A0, r2, y);
+        y = dfma(y, r2, y0 + r);
+    } else {
+        r = z * invc - 1.0;
+        y0 = logc + (double)k * Ln2;
+        double r2 = r * r;
+        y = A1 * r + A2;
+        y = A0 * r2 + y;
+        y = y * r2 + (y0 + r);
+    }
+    return y;
+}
+
+template <bool CONTRACT>
+LPHY_HD float logf_exact_t(float x) {
+    uint32_t ix = f2u(x);
+    if (ix == 0x3f800000u) return 0.0f;
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
+        if (ix * 2u == 0u) return u2f(0xff800000u);             // -inf
+        if (ix == 0x7f800000u) return x;                        // +inf
+        if ((ix & 0x80000000u) || ix * 2u >= 0xff000000u) return u2f(0x7fc00000u);
+        ix = f2u(x * 0x1p23f);
+        ix -= 23u << 23;
+    }
+    return (float)logf_eval<CONTRACT>(ix);
+}
+
+LPHY_HD float logf_exact(float x) { return logf_exact_t<false>(x); }
+
+// log10f as glibc 2.35 computes it: fdlibm's e_log10f.c, which splits
+// x = 2^k * m (m in [1,2), or [0.5,1) when k < 0 so the 2^k term is
+// exact), then z = k*log10_2lo + ivln10*logf(m); result z + k*log10_2hi
+// (all single precision).  Used by the osr>1 estimator's detector power,
+// LoRaDetector.hpp:64 (20*log10f(sqrtf(maxValue))).
+template <bool CONTRACT>
+LPHY_HD float log10f_exact_t(float x) {
+    const float two25 = 3.3554432000e+07f;
+    const float ivln10 = u2f(0x3ede5bd9u);
+    const float log10_2hi = u2f(0x3e9a2080u);
+    const float log10_2lo = u2f(0x355427dbu);
+    int32_t hx = (int32_t)f2u(x);
+    int32_t k = 0;
+    if (hx < 0x00800000) {
+        if ((hx & 0x7fffffff) == 0) return u2f(0xff800000u);
+        if (hx < 0) return u2f(0x7fc00000u);
+        k -= 25;
+        x *= two25;
+        hx = (int32_t)f2u(x);
+    }
+    if (hx >= 0x7f800000) return x + x;
+    k += (hx >> 23) - 127;
+    int32_t i = (int32_t)(((uint32_t)k & 0x80000000u) >> 31);
+    hx = (hx & 0x007fffff) | ((0x7f - i) << 23);
+    float y = (float)(k + i);
+    x = u2f((uint32_t)hx);
+    float lx = logf_exact_t<CONTRACT>(x);
+    float z;
+    if (CONTRACT) {
+        z = __builtin_fmaf(y, log10_2lo, ivln10 * lx);
+        return __builtin_fmaf(y, log10_2hi, z);
+    }
+    z = y * log10_2lo + ivln10 * lx;
+    return z + y * log10_2hi;
+}
+
+LPHY_HD float log10f_exact(float x) { return log10f_exact_t<false>(x); }
+
 }  // namespace lphy_libm

@@ -47,6 +47,10 @@ constexpr float kPi = 3.14159265358979323846f;  // lora_phy::PI (phy.hpp:20)
 // (a runtime branch per sample would split the staging block and serialise
 // the 16 independent sincos chains of a lane).
 constexpr int kWinBit = 4;
+// ... and kOsrBit when osr > 1: k_demod then reads every osr-th sample
+// (LoRaDemod.cpp:155, phy.cpp:225); the osr == 1 kernels keep unit-stride
+// addressing.
+constexpr int kOsrBit = 8;
 
 #ifdef LPHY_PROFILE_PHASES
 __device__ unsigned long long g_phase_cycles[4];
@@ -73,6 +77,7 @@ struct DemodArgs {
     int mode;
     int no_scratch;
     int est_units;           // estimate units per frame (est_syms * osr)
+    float power_scale;       // LoRaDetector.hpp:29, (float)(20*log10((double)N))
     // persistent demod workers: symbol stride per step split into whole
     // frames + symbols (host-computed, so the kernel never divides)
     unsigned stride_f, stride_s;
@@ -221,6 +226,15 @@ __device__ __forceinline__ UnitResult unit_result(const cf32* lds, int slot, Arg
     return r;
 }
 
+// Detector power of LoRaDetector.hpp:64, 20*log10(sqrt(maxValue)) - scale in
+// single precision with glibc's log10f.  Only the osr > 1 estimate compares
+// powers (with one phase, p > -1e30 <=> maxValue > 0).
+__device__ __forceinline__ float detector_power(float max_value, float power_scale) {
+    const float fund = sqrtf(max_value);
+    const float db = 20.0f * lphy_libm::log10f_exact(fund);
+    return db - power_scale;
+}
+
 // Running fold of the per-symbol estimates in symbol order
 // (LoRaDemod.cpp:95-128 / phy.cpp:95-135).
 struct EstFold {
@@ -238,6 +252,21 @@ struct EstFold {
         }
         prev_phase = best_phase;
         have_prev = true;
+    }
+    // per-phase selection over the osr phases of one symbol
+    // (LoRaDemod.cpp:93-113 with the lowest-index tie-break, phy.cpp:106-121
+    // without it); units arrive in (symbol, phase) order
+    float best_p = -1e30f, best_f = 0.0f, best_phase = 0.0f;
+    int best_idx = 0, best_t = 0, t = 0;
+    __device__ __forceinline__ void unit(const UnitResult& r, float p, int osr, bool tie_low) {
+        if (r.valid && (p > best_p || (tie_low && p == best_p && r.idx < best_idx))) {
+            best_p = p; best_idx = r.idx; best_f = r.findex; best_t = t; best_phase = r.phase;
+        }
+        if (++t == osr) {
+            add(best_idx, best_f, best_t, best_phase);
+            best_p = -1e30f; best_f = 0.0f; best_phase = 0.0f;
+            best_idx = 0; best_t = 0; t = 0;
+        }
     }
     // offsets of LoRaDemod.cpp:130-140 / phy.cpp:137-147 into m
     __device__ __forceinline__ void finish(lphy_frame_meta& m, int est_syms, int N, int osr) const {
@@ -263,6 +292,7 @@ __global__ __launch_bounds__(kTile) void k_estimate(DemodArgs A) {
     __shared__ cf32 twl[N];
     __shared__ ArgMax red[kTile / 64];
     __shared__ UnitResult units[T];
+    __shared__ float upow[T];
 
     const int tid = threadIdx.x;
     const int U = A.est_units;
@@ -319,23 +349,19 @@ __global__ __launch_bounds__(kTile) void k_estimate(DemodArgs A) {
         for (int e = 0; e < G::E; ++e) lds[G::addr(slot, bin_of<SF>(e, lam))] = v[e];
         ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), red);
         __syncthreads();
-        if (lam == 0) units[slot] = live ? unit_result<SF>(lds, slot, best) : UnitResult{0, 0, 0.0f, 0.0f};
+        if (lam == 0) {
+            units[slot] = live ? unit_result<SF>(lds, slot, best) : UnitResult{0, 0, 0.0f, 0.0f};
+            if (A.osr > 1)
+                upow[slot] = live ? detector_power(best.v > 0.0f ? best.v : 0.0f, A.power_scale) : 0.0f;
+        }
         __syncthreads();
         if (folder) {
             const int first = packed ? tid * U : 0;
             const int nu = packed ? U : ((U - c * T) < T ? (U - c * T) : T);
-            for (int s0 = 0; s0 < nu; s0 += A.osr) {
-                int best_idx = 0, best_t = 0;
-                float best_f = 0.0f, best_phase = 0.0f;  // atan2(0, 0) of an unset bin
-                for (int t2 = 0; t2 < A.osr; ++t2) {
-                    const UnitResult& r = units[first + s0 + t2];
-                    if (r.valid) {
-                        best_idx = r.idx; best_f = r.findex; best_t = t2; best_phase = r.phase;
-                        break;
-                    }
-                }
-                fold.add(best_idx, best_f, best_t, best_phase);
-            }
+            const bool tie_low = A.mode != LPHY_MODE_DEMODULATE;
+            // an unset best bin is (0, 0), whose atan2 is 0
+            for (int k = 0; k < nu; ++k)
+                fold.unit(units[first + k], A.osr > 1 ? upow[first + k] : 0.0f, A.osr, tie_low);
         }
     }
 
@@ -361,6 +387,7 @@ struct SymCtx {
     bool ok, have_sync, live;
 };
 
+template <bool OSR = false>
 __device__ __forceinline__ SymCtx sym_ctx(const DemodArgs& A, unsigned f, unsigned s, bool live,
                                           int N, const lphy_frame_meta& m) {
     SymCtx c;
@@ -369,8 +396,9 @@ __device__ __forceinline__ SymCtx sym_ctx(const DemodArgs& A, unsigned f, unsign
     c.ok = live && m.status == 0;
     c.live = live;
     c.have_sync = m.have_sync != 0;
-    // LoRaDemod.cpp:144-151 with osr == 1, in 32 bits
-    const unsigned step = (unsigned)N, count = (unsigned)A.frame_samples;
+    // LoRaDemod.cpp:144-151 / phy.cpp:208-216, in 32 bits
+    const unsigned osr = OSR ? (unsigned)A.osr : 1u;
+    const unsigned step = (unsigned)N * osr, count = (unsigned)A.frame_samples;
     unsigned base = s * step;
     const int t = m.t_off;
     if (t > 0) {
@@ -383,9 +411,10 @@ __device__ __forceinline__ SymCtx sym_ctx(const DemodArgs& A, unsigned f, unsign
     c.base = base;
     c.rate = m.rate;
     c.scale = m.scale;
-    // LoRaDemod.cpp:152-153 / phy.cpp:217-218 with osr == 1; (float) of the
-    // size_t product equals (float) of the same value held in 32 bits
-    c.start = m.rate * ((float)(s * step) + (float)m.t_off / 1.0f);
+    // LoRaDemod.cpp:152-153 / phy.cpp:217-218; (float) of the size_t product
+    // equals (float) of the same value held in 32 bits; x / 1.0f == x
+    const float toff = OSR ? (float)m.t_off / (float)osr : (float)m.t_off;
+    c.start = m.rate * ((float)(s * (unsigned)N) + toff);
     return c;
 }
 
@@ -425,7 +454,7 @@ __device__ __forceinline__ cf32 rotate_sample(cf32 x, int i, const SymCtx& c,
 template <int SF, int MODE>
 __device__ __forceinline__ void stage_symbol(cf32* lds, const Stage<SF>& stg, const cf32 (&raw)[16],
                                              const cf32* src, const SymCtx& c, int lam,
-                                             const cf32* down, const float* win) {
+                                             const cf32* down, const float* win, int osr = 1) {
     using G = Geo<SF>;
 #pragma unroll
     for (int e = 0; e < G::E; ++e)
@@ -437,7 +466,7 @@ __device__ __forceinline__ void stage_symbol(cf32* lds, const Stage<SF>& stg, co
         for (int e = 0; e < G::E; ++e) {
             const int i = lam + e * G::LPS;
             if (lphy_libm::sincosf_needs_large(c.start + c.rate * (float)i))
-                stg.put(lds, e, rotate_sample<SF, MODE>(src[i], i, c, down, win, true));
+                stg.put(lds, e, rotate_sample<SF, MODE>(src[(unsigned)i * (unsigned)osr], i, c, down, win, true));
         }
     }
 }
@@ -506,13 +535,15 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
     unsigned fw = fw0, sw = worker * WT - fw0 * S;
 
     // prologue of the software pipeline
+    constexpr bool OSR = (MODE & kOsrBit) != 0;
+    const unsigned osr = OSR ? (unsigned)A.osr : 1u;  // sample stride of a symbol
     lphy_frame_meta m = A.meta[f < nframes ? f : 0];
-    SymCtx c = sym_ctx(A, f < nframes ? f : 0, f < nframes ? s : 0, f < nframes, N, m);
+    SymCtx c = sym_ctx<OSR>(A, f < nframes ? f : 0, f < nframes ? s : 0, f < nframes, N, m);
     cf32 raw[16];
     {
         const cf32* src = A.iq + (unsigned long long)c.f * A.frame_samples + c.base;
 #pragma unroll
-        for (int e = 0; e < G::E; ++e) raw[e] = src[lam + e * G::LPS];
+        for (int e = 0; e < G::E; ++e) raw[e] = src[(unsigned)(lam + e * G::LPS) * osr];
     }
 
 #ifdef LPHY_PROFILE_PHASES  // timing experiments only: per-phase clock sums
@@ -531,14 +562,14 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
 
         if constexpr (!WAVE) __syncthreads();  // previous tile's readers done
         stage_symbol<SF, MODE>(lds, stg, raw, A.iq + (unsigned long long)c.f * A.frame_samples + c.base,
-                               c, lam, down, win);
+                               c, lam, down, win, (int)osr);
         team_sync<SF>();
 #ifdef LPHY_PROFILE_PHASES
         const unsigned long long p1 = clock64();
 #endif
 
         // next tile's IQ: in flight during this tile's FFT
-        const SymCtx nc = sym_ctx(A, nlive ? nf : 0, nlive ? ns : 0, nlive, N, nm);
+        const SymCtx nc = sym_ctx<OSR>(A, nlive ? nf : 0, nlive ? ns : 0, nlive, N, nm);
         if (nfw < nframes) {
             const cf32* nsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base;
 #ifdef LPHY_ABLATE_LOAD  // timing experiments only
@@ -547,7 +578,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
             for (int e = 0; e < G::E; ++e) raw[e] = raw[e] * 0.999f + cf32{(float)e, (float)lam};
 #else
 #pragma unroll
-            for (int e = 0; e < G::E; ++e) raw[e] = nsrc[lam + e * G::LPS];
+            for (int e = 0; e < G::E; ++e) raw[e] = nsrc[(unsigned)(lam + e * G::LPS) * osr];
 #endif
         }
 
@@ -1106,6 +1137,7 @@ struct lphy_hip_ctx {
     int device = 0;
     unsigned sf = 0, N = 0, bw_hz = 0, osr = 1;
     int window = 0;
+    float power_scale = 0.0f;
     cf32* d_tw = nullptr;
     cf32* d_down = nullptr;
     float* d_win = nullptr;
@@ -1293,6 +1325,14 @@ inline bool frames_fit(unsigned sf, unsigned osr, int est_units, size_t total) {
 
 template <int SF, int MODE>
 void launch_symbols_w(const DemodArgs& A, unsigned long long tiles, hipStream_t st, int per_cu) {
+    if (A.osr > 1) {
+        // oversampled input: strided symbol loads (no dechirp mode here)
+        if constexpr ((MODE & 3) != LPHY_MODE_DECHIRP_LORA_DEMODULATE) {
+            if (A.win) launch_symbols_occ<SF, MODE | kWinBit | kOsrBit, 2>(A, tiles, st, per_cu);
+            else launch_symbols_occ<SF, MODE | kOsrBit, 2>(A, tiles, st, per_cu);
+        }
+        return;
+    }
     if (A.win) launch_symbols<SF, MODE | kWinBit>(A, tiles, st, per_cu);
     else launch_symbols<SF, MODE>(A, tiles, st, per_cu);
 }
@@ -1465,7 +1505,7 @@ int lphy_hip_ctx_create(lphy_hip_ctx** out, int device, unsigned sf, unsigned bw
     if (sf < 1 || sf > 12) return -EINVAL;
     if (bw_hz != 125000 && bw_hz != 250000 && bw_hz != 500000) return -EINVAL;
     if (osr == 0) osr = 1;
-    if (osr != 1) return -ENOTSUP;  // TODO(osr>1): p comparison needs log10f parity
+    if (osr > 64) return -EINVAL;
     if (window != LPHY_WINDOW_NONE && window != LPHY_WINDOW_HANN) return -EINVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return -ENODEV;
@@ -1477,6 +1517,7 @@ int lphy_hip_ctx_create(lphy_hip_ctx** out, int device, unsigned sf, unsigned bw
     c->bw_hz = bw_hz;
     c->osr = osr;
     c->window = window;
+    c->power_scale = (float)(20.0 * std::log10((double)c->N));  // LoRaDetector.hpp:29
     std::vector<std::complex<float>> tw, down;
     make_twiddles(tw, (int)c->N);
     make_downchirp(down, (int)c->N, (float)bw_hz / 125000.0f);
@@ -1547,6 +1588,7 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     A.total_syms = total;
     A.out_per_frame = lphy_hip_syms_per_frame(c, frame_samples, mode);
     A.osr = (int)c->osr;
+    A.power_scale = c->power_scale;
     A.mode = mode;
     A.no_scratch = (flags & LPHY_F_NO_SCRATCH) ? 1 : 0;
     const size_t est_syms = mode == LPHY_MODE_DEMODULATE ? 2 : (total < 2 ? total : 2);
@@ -1638,6 +1680,7 @@ int lphy_hip_estimate_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     A.frame_samples = frame_samples;
     A.total_syms = frame_samples / step;
     A.osr = (int)c->osr;
+    A.power_scale = c->power_scale;
     A.mode = LPHY_MODE_DEMODULATE;
     A.est_units = (int)(syms * c->osr);
     hipStream_t st = (hipStream_t)stream;

@@ -103,6 +103,14 @@ class Oracle:
         self.lib.orc_lora_encode(_p(payload, _u8p), len(payload), _p(out, _u16p))
         return out
 
+    def estimate_offsets(self, iq, sf, osr=1, hann=False):
+        """phy.cpp:81-148 over the whole buffer -> (cfo, time_offset)."""
+        x = _cf(iq)
+        met = np.zeros(2, np.float32)
+        self.lib.orc_estimate_offsets(sf, osr, int(hann), _p(x, _f32p), len(x) // 2,
+                                      _p(met, _f32p))
+        return met
+
     def dechirp(self, iq, sf, bw_hz=125000):
         x = _cf(np.asarray(iq, np.complex64))
         out = np.zeros_like(x)
@@ -216,6 +224,13 @@ class Reference:
         out = np.zeros_like(x)
         self.lib.ref_fft(_p(x, _f32p), _p(out, _f32p), len(x) // 2)
         return out.view(np.complex64)
+
+    def estimate_offsets(self, iq, sf, osr=1, hann=False, bw_hz=125000):
+        x = _cf(iq)
+        met = np.zeros(2, np.float32)
+        self.lib.ref_estimate_offsets(sf, bw_hz, osr, int(hann), _p(x, _f32p), len(x) // 2,
+                                      _p(met, _f32p))
+        return met
 
     def dechirp(self, iq, sf, bw_hz=125000):
         x = _cf(np.asarray(iq, np.complex64))

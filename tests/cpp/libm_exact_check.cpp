@@ -3,6 +3,8 @@
 //   libm_exact_check sincos <first_u32> <last_u32> [threads]   # float range
 //   libm_exact_check atan2 <count> <seed> [threads]            # random pairs
 //   libm_exact_check cabs <count> <seed> [threads]
+//   libm_exact_check log10 <first_u32> <last_u32> [threads]    # float range
+//   libm_exact_check logf <first_u32> <last_u32> [threads]
 // Prints "mismatches=<k> checked=<n>" and exits non-zero on any mismatch.
 #include "../../lora-sdr-lightweight-standalone-library-clean_amd/csrc/libm_exact.h"
 
@@ -29,7 +31,29 @@ int main(int argc, char** argv) {
     int threads = argc > 4 ? atoi(argv[4]) : 8;
     std::atomic<uint64_t> bad{0}, checked{0};
     std::vector<std::thread> th;
-    if (!strcmp(what, "sincos")) {
+    if (!strcmp(what, "log10") || !strcmp(what, "logf") || !strcmp(what, "log10c")) {
+        uint64_t lo = strtoull(argv[2], 0, 0), hi = strtoull(argv[3], 0, 0);
+        uint64_t span = hi - lo + 1, per = (span + threads - 1) / threads;
+        int which = !strcmp(what, "logf") ? 0 : !strcmp(what, "log10") ? 1 : 2;
+        for (int t = 0; t < threads; ++t) {
+            th.emplace_back([&, t, which] {
+                uint64_t a = lo + t * per, b = std::min(hi + 1, a + per);
+                uint64_t nb = 0, n = 0;
+                for (uint64_t u = a; u < b; ++u) {
+                    float x = fromb((uint32_t)u), g, o;
+                    if (which == 0) { g = logf(x); o = lphy_libm::logf_exact(x); }
+                    else if (which == 1) { g = log10f(x); o = lphy_libm::log10f_exact(x); }
+                    else { g = log10f(x); o = lphy_libm::log10f_exact_t<true>(x); }
+                    ++n;
+                    if (!same(g, o)) {
+                        if (nb < 5) fprintf(stderr, "x=%a glibc=%a ours=%a\n", x, g, o);
+                        ++nb;
+                    }
+                }
+                bad += nb; checked += n;
+            });
+        }
+    } else if (!strcmp(what, "sincos")) {
         uint64_t lo = strtoull(argv[2], 0, 0), hi = strtoull(argv[3], 0, 0);
         uint64_t span = hi - lo + 1, per = (span + threads - 1) / threads;
         for (int t = 0; t < threads; ++t) {

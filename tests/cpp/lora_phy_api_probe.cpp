@@ -84,12 +84,13 @@ struct Ws {
     std::vector<float> win;
     lora_workspace ws{};
     int rc;
-    Ws(unsigned sf, bandwidth bw, window_type w = window_type::window_none, uint8_t sync = 0x12) {
+    Ws(unsigned sf, bandwidth bw, window_type w = window_type::window_none, uint8_t sync = 0x12,
+       unsigned osr = 1) {
         const size_t N = size_t(1) << sf;
         in.resize(N); out.resize(N); win.resize(N);
         ws.fft_in = in.data(); ws.fft_out = out.data(); ws.window = win.data();
         lora_params p{};
-        p.sf = sf; p.bw = bw; p.cr = 1; p.osr = 1; p.window = w; p.sync_word = sync;
+        p.sf = sf; p.bw = bw; p.cr = 1; p.osr = osr; p.window = w; p.sync_word = sync;
         rc = init(&ws, &p);
     }
 };
@@ -102,9 +103,9 @@ std::vector<uint8_t> ramp32() {
 
 void chain(const char* tag, unsigned sf, bandwidth bw, const std::vector<uint8_t>& payload,
            float cfo, int delay, float sigma, window_type w = window_type::window_none,
-           uint8_t sync = 0x12) {
-    Ws s(sf, bw, w, sync);
-    const size_t N = size_t(1) << sf;
+           uint8_t sync = 0x12, unsigned osr = 1) {
+    Ws s(sf, bw, w, sync, osr);
+    const size_t N = (size_t(1) << sf) * osr;  // samples per symbol
     std::vector<uint16_t> syms(2 * payload.size() + 8);
     const ssize_t ns = encode(&s.ws, payload.data(), payload.size(), syms.data(), syms.size());
     std::vector<cf> iq((ns + 2) * N + 64);
@@ -124,26 +125,29 @@ void chain(const char* tag, unsigned sf, bandwidth bw, const std::vector<uint8_t
 
 void legacy(const char* tag, unsigned sf, bandwidth bw, const std::vector<uint8_t>& payload,
             float cfo, int delay, float sigma, float gain, bool scratch,
-            window_type w = window_type::window_none) {
+            window_type w = window_type::window_none, unsigned osr = 1) {
     const size_t N = size_t(1) << sf;
     std::vector<uint16_t> syms(2 * payload.size() + 8);
     const size_t ns = lora_encode(payload.data(), payload.size(), syms.data(), sf);
-    std::vector<cf> iq((ns + 2) * N);
-    const size_t nm = lora_modulate(syms.data(), ns, iq.data(), sf, 1, bw, 1.0f, 0x12);
+    std::vector<cf> iq((ns + 2) * N * osr);
+    const size_t nm = lora_modulate(syms.data(), ns, iq.data(), sf, osr, bw, 1.0f, 0x12);
     iq.resize(nm);
-    if (cfo != 0.0f || delay || sigma > 0.0f) impair(iq, (unsigned)N, cfo, delay, sigma, sf * 977 + delay);
+    if (cfo != 0.0f || delay || sigma > 0.0f) impair(iq, (unsigned)(N * osr), cfo, delay, sigma, sf * 977 + delay);
     for (auto& v : iq) v *= gain;
-    // external dechirp (e2e_chain_test.cpp:80-93 / bit_exact_test.cpp:145-155)
-    std::vector<cf> down(N);
-    float ph = 0.0f;
-    genChirp<float>(down.data(), (int)N, 1, (int)N, 0.0f, true, 1.0f, ph, bw_scale(bw));
-    for (size_t i = 0; i < iq.size(); ++i) iq[i] *= down[i % N];
+    // external dechirp (e2e_chain_test.cpp:80-93 / bit_exact_test.cpp:145-155),
+    // at the chip rate only
+    if (osr == 1) {
+        std::vector<cf> down(N);
+        float ph = 0.0f;
+        genChirp<float>(down.data(), (int)N, 1, (int)N, 0.0f, true, 1.0f, ph, bw_scale(bw));
+        for (size_t i = 0; i < iq.size(); ++i) iq[i] *= down[i % N];
+    }
     static lora_demod_workspace ws;  // ~115 KB: keep off the stack
     std::vector<cf> scr(iq.size());
     lora_demod_init(&ws, sf, w, scratch ? scr.data() : nullptr, scratch ? scr.size() : 0);
     std::vector<uint16_t> got(iq.size() / N + 2);
     uint8_t sw = 0xEE;
-    const ssize_t nd = lora_demodulate(&ws, iq.data(), iq.size(), got.data(), 1, &sw);
+    const ssize_t nd = lora_demodulate(&ws, iq.data(), iq.size(), got.data(), osr, &sw);
     std::vector<uint8_t> pay(got.size());
     const ssize_t nb = nd >= 0 ? lora_decode(got.data(), (size_t)(nd & ~1), pay.data()) : -1;
     char buf[256];
@@ -343,5 +347,15 @@ int main(int argc, char** argv) {
     legacy("legacy_sf9_gain3_noscratch", 9, bandwidth::bw_250, r32, 0, 0, 0.2f, 3.0f, false);
     legacy("legacy_sf12", 12, bandwidth::bw_125, r32, 0, 0, 0, 1.0f, true);
     legacy("legacy_sf8_hann", 8, bandwidth::bw_125, r32, -0.15f, 1, 0.4f, 0.5f, true, window_type::window_hann);
+    // oversampled input (lora_params::osr, lora_demodulate's osr argument)
+    chain("chain_sf7_osr2", 7, bandwidth::bw_125, r32, 0, 0, 0, window_type::window_none, 0x12, 2);
+    chain("chain_sf8_osr4_impaired", 8, bandwidth::bw_125, r32, 0.2f, 37, 0.4f,
+          window_type::window_none, 0x12, 4);
+    chain("chain_sf9_osr2_hann", 9, bandwidth::bw_250, r32, -0.1f, 5, 0.2f,
+          window_type::window_hann, 0x34, 2);
+    legacy("legacy_sf7_osr2", 7, bandwidth::bw_125, r32, 0.1f, 9, 0.3f, 1.0f, true,
+           window_type::window_none, 2);
+    legacy("legacy_sf10_osr3_gain2", 10, bandwidth::bw_125, r32, 0, 100, 0.2f, 2.0f, true,
+           window_type::window_none, 3);
     return 0;
 }

@@ -57,3 +57,14 @@ def test_fft_layout_algebra(bins):
     r = subprocess.run([str(bins / "fft_layout")], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count(": ok") == 12, r.stdout
+
+
+@pytest.mark.parametrize("what", ["logf", "log10"])
+def test_log10f_exact_all_floats(bins, what):
+    """log10f drives the osr>1 estimator's detector power (LoRaDetector.hpp:64);
+    the restatement is checked against glibc for every float bit pattern."""
+    for lo, hi in ((0x00000000, 0x7f800000), (0x7f800001, 0xffffffff)):
+        r = subprocess.run([str(bins / "libm_check"), what, str(lo), str(hi), "8"],
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert "mismatches=0" in r.stdout

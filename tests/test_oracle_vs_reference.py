@@ -101,3 +101,79 @@ def test_encode_decode_roundtrip(oracle, reference):
         syms = oracle.encode(p) ^ rng.integers(0, 2, 2 * n, dtype=np.uint16) << rng.integers(0, 8, 2 * n, dtype=np.uint16)
         np.testing.assert_array_equal(oracle.decode(syms)[1], reference.decode(syms)[1])
         assert oracle.decode(syms)[2] == reference.decode(syms)[2]
+
+
+def _osr_frame(oracle, rng, sf, osr, plen, snr, delay, cfo):
+    """A frame modulated at osr samples per chip, delayed by a fraction of a
+    symbol, with carrier offset and noise."""
+    iq = oracle.modulate(oracle.encode(rng.integers(0, 256, plen, dtype=np.uint8).tobytes()),
+                         sf, osr=osr)
+    if cfo:
+        iq = (iq * np.exp(2j * np.pi * cfo / ((1 << sf) * osr) * np.arange(iq.size))).astype(np.complex64)
+    if delay:
+        iq = np.concatenate([np.zeros(delay, np.complex64), iq[:-delay]])
+    if snr is not None:
+        s = np.sqrt(10 ** (-snr / 10) / 2)
+        iq = (iq + s * (rng.standard_normal(iq.size) + 1j * rng.standard_normal(iq.size))).astype(np.complex64)
+    return iq
+
+
+def _tie_frame(sf, osr, nsym, amp):
+    """Oversampled input whose phases tie on detector power with different
+    argmax bins: phase 0 carries an alternating sequence (peak at N/2),
+    phase 1 a constant one (peak at 0).  LoRaDemod.cpp:102 breaks the tie
+    towards the lower bin, phy.cpp:114 keeps the first phase."""
+    N = 1 << sf
+    x = np.zeros((nsym, N, osr), np.complex64)
+    x[:, :, 0] = amp * np.where(np.arange(N) % 2 == 0, 1.0, -1.0)
+    if osr > 1:
+        x[:, :, 1] = amp
+    return x.reshape(-1)
+
+
+OSR_CASES = [  # sf, osr, payload bytes, snr, delay, cfo, hann
+    (7, 2, 16, None, 0, 0.0, False), (7, 2, 16, -8.0, 37, 0.2, False),
+    (7, 4, 8, None, 301, -0.3, False), (8, 3, 12, 0.0, 5, 0.1, True),
+    (9, 2, 8, -12.0, 0, 0.0, False), (5, 8, 8, None, 17, 0.05, False),
+    (10, 2, 4, None, 700, 0.0, False), (12, 2, 4, -5.0, 0, 0.0, False),
+    (11, 4, 4, None, 33, 0.4, True)]
+
+
+@pytest.mark.parametrize("sf,osr,plen,snr,delay,cfo,hann", OSR_CASES)
+def test_oversampled_paths_bit_exact(oracle, reference, sf, osr, plen, snr, delay, cfo, hann):
+    """osr > 1: the estimate picks the best of osr phases by detector power
+    (log10f), symbols read every osr-th sample after the time shift."""
+    rng = np.random.default_rng(sf * 31 + osr * 7 + delay)
+    for rep in range(2):
+        iq = _osr_frame(oracle, rng, sf, osr, plen, snr, delay, cfo)
+        a = oracle.demodulate(iq, sf, osr=osr, hann=hann)
+        b = reference.demodulate(iq, sf, osr=osr, hann=hann)
+        assert a[0] == b[0] and a[2] == b[2]
+        np.testing.assert_array_equal(a[1], b[1])
+        np.testing.assert_array_equal(_bits(a[3][:2]), _bits(b[3][:2]))
+        nsym = iq.size // ((1 << sf) * osr)
+        for n in (1, 3, nsym):  # estimate_offsets over n whole symbols
+            seg = iq[: n * (1 << sf) * osr]
+            np.testing.assert_array_equal(_bits(oracle.estimate_offsets(seg, sf, osr, hann)),
+                                          _bits(reference.estimate_offsets(seg, sf, osr, hann)))
+        for scratch in (True, False):
+            a = oracle.lora_demodulate(iq, sf, osr=osr, hann=hann, scratch=scratch)
+            b = reference.lora_demodulate(iq, sf, osr=osr, hann=hann, scratch=scratch)
+            assert a[0] == b[0] and a[2] == b[2]
+            np.testing.assert_array_equal(a[1], b[1])
+            np.testing.assert_array_equal(_bits(a[3][:2]), _bits(b[3][:2]))
+
+
+@pytest.mark.parametrize("sf,osr,amp", [(2, 2, 0.5), (7, 2, 0.25), (7, 4, 3.0), (10, 2, 1.0)])
+def test_oversampled_power_tie(oracle, reference, sf, osr, amp):
+    x = _tie_frame(sf, osr, 6, amp)
+    a = oracle.demodulate(x, sf, osr=osr)
+    b = reference.demodulate(x, sf, osr=osr)
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(_bits(a[3][:2]), _bits(b[3][:2]))
+    a1 = oracle.lora_demodulate(x, sf, osr=osr)
+    b1 = reference.lora_demodulate(x, sf, osr=osr)
+    np.testing.assert_array_equal(a1[1], b1[1])
+    np.testing.assert_array_equal(_bits(a1[3][:2]), _bits(b1[3][:2]))
+    # the two tie rules pick different phases here
+    assert _bits(a[3][1]) != _bits(a1[3][1])
