@@ -83,9 +83,13 @@ enum lphy_flags {
     LPHY_F_STAGE_PROLOGUE = 4u,  /* per-frame max-abs + offset estimate   */
     LPHY_F_STAGE_SYMBOLS = 8u,   /* per-symbol rotate + FFT + argmax      */
     LPHY_F_STAGE_FINAL = 16u,    /* per-frame sync word, decode, CRC      */
-    LPHY_F_UNFUSED = 32u         /* separate prologue / symbol launches
+    LPHY_F_UNFUSED = 32u,        /* separate prologue / symbol launches
                                     instead of the fused single launch
                                     (same results; for comparison)       */
+    LPHY_F_EXACT_ROTATION = 64u  /* fused launch: rotate every symbol with
+                                    the per-sample sincos of the reference
+                                    instead of the certified per-frame
+                                    table (same results; for comparison) */
 };
 
 enum lphy_window { LPHY_WINDOW_NONE = 0, LPHY_WINDOW_HANN = 1 };
@@ -161,6 +165,13 @@ int lphy_hip_sync(void* stream);
 
 /* Version / build string (for tests that check the library loaded). */
 const char* lphy_hip_version(void);
+
+/* Symbols the fused kernel recomputed with the exact per-sample rotation
+ * because the certified fast path could not prove its argmax (near-ties,
+ * NaN, shifted windows; every symbol under LPHY_F_EXACT_ROTATION), summed
+ * over launches on `ctx`'s device since the last reset.  Diagnostic only:
+ * synchronises the device.  Returns 0 or -EIO. */
+int lphy_hip_recheck_count(lphy_hip_ctx* ctx, unsigned long long* out, int reset);
 
 #ifdef __cplusplus
 }

@@ -398,4 +398,55 @@ __device__ __forceinline__ ArgMax symbol_argmax(ArgMax a, ArgMax* red) {
     return a;
 }
 
+// Argmax plus the runner-up value: v2 = max |X|^2 over every bin but the
+// winner (ties give v2 == v).  NaN bins are ignored by both (v_min / v_max
+// return the other operand), so an all-NaN symbol ends with v = v2 = 0.
+// Used by the certified fast rotation (k_frames): a symbol whose winner
+// clears the runner-up by more than the rounding bound has the reference's
+// argmax, any other symbol is recomputed with the exact rotation.
+struct ArgMax2 {
+    float v;
+    int i;
+    float v2;
+};
+
+template <int SF>
+__device__ __forceinline__ ArgMax2 local_argmax2(const cf32 (&v)[16], int lam) {
+    using G = Geo<SF>;
+    constexpr BinOrder<SF> BO{};
+    ArgMax2 best{0.0f, 0x7fffffff, 0.0f};
+    const int lane_bin = bin_of<SF>(0, lam);
+#pragma unroll
+    for (int k = 0; k < G::E; ++k) {
+        const int e = BO.e[k];
+        const cf32 sq = v[e] * v[e];
+        const float m2 = sq.x + sq.y;
+        best.v2 = fmaxf(best.v2, fminf(m2, best.v));
+        const bool take = m2 > best.v;
+        best.v = take ? m2 : best.v;
+        best.i = take ? (lane_bin | bin_of<SF>(e, 0)) : best.i;
+    }
+    return best;
+}
+
+// Team reduction (LPS <= 64 only: one wavefront per symbol).
+template <int SF>
+__device__ __forceinline__ ArgMax2 symbol_argmax2(ArgMax2 a) {
+    using G = Geo<SF>;
+    static_assert(G::LPS <= 64, "team inside one wavefront");
+#pragma unroll
+    for (int off = G::LPS / 2; off >= 1; off >>= 1) {
+        ArgMax2 o;
+        o.v = __shfl_xor(a.v, off, 64);
+        o.i = __shfl_xor(a.i, off, 64);
+        o.v2 = __shfl_xor(a.v2, off, 64);
+        a.v2 = fmaxf(fmaxf(a.v2, o.v2), fminf(a.v, o.v));
+        const bool take = (o.v > a.v) | ((o.v == a.v) & (o.i < a.i));
+        a.v = take ? o.v : a.v;
+        a.i = take ? o.i : a.i;
+    }
+    if (!(a.v > 0.0f)) a.i = 0;  // nothing beat maxValue = 0
+    return a;
+}
+
 }  // namespace lphy

@@ -55,6 +55,8 @@ constexpr int kOsrBit = 8;
 #ifdef LPHY_PROFILE_PHASES
 __device__ unsigned long long g_phase_cycles[4];
 #endif
+// symbols recomputed by the exact rotation (lphy_hip_recheck_count)
+__device__ unsigned long long g_rechecks;
 
 // Experiments only: -DLPHY_ONLY_SF=n instantiates the kernels of one SF
 // (the launch switches below); the default build has every SF.
@@ -77,6 +79,7 @@ struct DemodArgs {
     int mode;
     int no_scratch;
     int est_units;           // estimate units per frame (est_syms * osr)
+    int exact_rotation;      // LPHY_F_EXACT_ROTATION: no certified fast path
     float power_scale;       // LoRaDetector.hpp:29, (float)(20*log10((double)N))
     // persistent demod workers: symbol stride per step split into whole
     // frames + symbols (host-computed, so the kernel never divides)
@@ -384,6 +387,7 @@ struct SymCtx {
     unsigned f, s;            // frame, symbol within the frame
     unsigned base;            // first sample of the (shifted) window in the frame
     float start, rate, scale;
+    int toff;                 // the frame's t_off (fast-rotation table offset)
     bool ok, have_sync, live;
 };
 
@@ -411,6 +415,7 @@ __device__ __forceinline__ SymCtx sym_ctx(const DemodArgs& A, unsigned f, unsign
     c.base = base;
     c.rate = m.rate;
     c.scale = m.scale;
+    c.toff = m.t_off;
     // LoRaDemod.cpp:152-153 / phy.cpp:217-218; (float) of the size_t product
     // equals (float) of the same value held in 32 bits; x / 1.0f == x
     const float toff = OSR ? (float)m.t_off / (float)osr : (float)m.t_off;
@@ -754,6 +759,122 @@ __device__ __forceinline__ void stage_mixed(cf32* lds, const Stage<SF>& stg, con
 
 enum : int { kUnitDead = 0, kUnitEst = 1, kUnitSym = 2 };
 
+// ---------------------------------------------------------------------------
+// Certified fast rotation (k_frames symbol units).
+//
+// The reference rotates sample i of symbol s by the glibc sincosf of
+// ph_i = fl(start_s + fl(rate * i)), start_s = rate * (s*N + t_off)
+// (LoRaDemod.cpp:152-158, phy.cpp:217-222): one double-precision sincos per
+// sample, half of the path's arithmetic.  A symbol's output is only the
+// argmax of |FFT|^2, and |FFT(y * e^{j start})| = |FFT(y)|: the common phase
+// start_s drops out of every magnitude.  So symbols are transformed as
+//     q_i = x_i * t_i,   t_i = [down] * e^{j rate i} * [scale] * [win]
+// with t a per-FRAME table (N entries, built once per frame from exact
+// sincos of fl(rate*i)), i.e. one complex multiply per sample instead of a
+// dechirp, a rescale, a sincos and a rotation.
+//
+// Exactness is certified per symbol, not assumed.  With u = 2^-24, A an
+// upper bound of sum_i |y_i| (the symbol's L1 norm), P = |start| + |rate| N,
+// L the number of KISS stages, the reference's bins X and ours X' satisfy
+//   | |X_k| - |X'_k| | <= B = u A (24 + 12 L + 2 |rate| N + P) (1 + 1e-3):
+//   * rotation inputs: the reference's sample differs from the ideal
+//     y_i e^{j(start + rate i)} by <= u(10 + |rate| N + P)|y_i| (dechirp
+//     3u, rescale u, sincos sqrt(2)u, phase roundings u(|rate| i + |ph|),
+//     rotation 3u, window u); ours from e^{j start}-times-ideal by
+//     <= u(10 + |rate| N)|y_i|;
+//   * transform: each KISS stage adds <= 6u (sum of its butterfly's input
+//     magnitudes) to an output; an output depends on one value of every
+//     sub-transform of a level, whose inputs partition the symbol, so both
+//     FFTs are within 6 L u A of the exact map (same float twiddles), and
+//     the input difference passes with gain (1+u)^L.
+// The reference's winner is ours when |X'_best| - 2B > |X'_second| (plus
+// the 2u rounding of |X|^2 on both sides and of the check itself); any
+// symbol that fails it - ties, near-ties, NaN, overflow risk, frames whose
+// time shift is not applied to every symbol - is recomputed with the exact
+// per-sample path.  The check below uses 4B (a factor 2 of slack).
+// ---------------------------------------------------------------------------
+constexpr float kU = 5.9604645e-8f;  // 2^-24
+
+// Table of frame `rec` (rate, scale, t_off): t_i for i = lane, lane+64, ...
+template <int SF, int MODE>
+__device__ __forceinline__ void build_rtab(cf32* tab, float rate, float scale, int t_off,
+                                           const cf32* down, const float* win, int lane) {
+    constexpr int N = 1 << SF;
+    const unsigned t0 = (unsigned)t_off & (N - 1);
+    for (int i = lane; i < N; i += 64) {
+        float sn, cs;
+        lphy_libm::sincosf_exact(rate * (float)i, &sn, &cs);
+        cf32 t = cf32{cs, sn};
+        if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) t = cmul(down[i], t);
+        if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) t = cmul(down[(t0 + (unsigned)i) & (N - 1)], t);
+        if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) t = cscale(t, scale);
+        if constexpr ((MODE & kWinBit) != 0) t = cscale(t, win[i]);
+        tab[i] = t;
+    }
+}
+
+// Whether the fast path may take this symbol unit: the table's dechirp
+// offset (mode 2) must match the symbol's window start.
+template <int SF, int MODE>
+__device__ __forceinline__ bool fast_applies(const SymCtx& c, int t_off) {
+    constexpr int N = 1 << SF;
+    if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+        return (c.base & (N - 1)) == ((unsigned)t_off & (N - 1));
+    return true;
+}
+
+// The certificate of the header comment.  amax bounds max(|Re y|, |Im y|)
+// over the symbol's samples before rotation (modes 1/2: <= 1 after the
+// frame's normalisation; mode 0: measured).
+template <int SF>
+__device__ __forceinline__ bool fast_certified(const ArgMax2& b, const SymCtx& c, float amax) {
+    constexpr int N = 1 << SF, L = (SF + 1) / 2;
+    const float A = (float)N * 1.41421366f * amax * 1.0001f;
+    const float ar = fabsf(c.rate) * (float)N;
+    const float P = fabsf(c.start) + ar;
+    const float B = kU * A * ((24.0f + 12.0f * L) + 2.0f * ar + P) * 1.001f;
+    const float lhs = sqrtf(b.v) * (1.0f - 8.0f * kU) - 4.0f * B;
+    const float rhs = sqrtf(b.v2) * (1.0f + 8.0f * kU);
+    return lhs > rhs && A < 1e18f;
+}
+
+// Fast staging of one tile: symbol units q_i = x_i * t_i from the frame's
+// rotation table (LDS ring for SF <= 8, the lane's registers above), estimate
+// units exactly as stage_mixed (no rotation).  Returns the lane's
+// max(|Re x|, |Im x|) over its symbol samples for mode 0's certificate.
+template <int SF, int MODE, bool MIXED>
+__device__ __forceinline__ float stage_fast(cf32* lds, const Stage<SF>& stg, const cf32 (&raw)[16],
+                                            const SymCtx& c, int lam, const cf32* down,
+                                            const float* win, const cf32* rt,
+                                            const cf32 (&rreg)[16], bool est) {
+    using G = Geo<SF>;
+    constexpr int N = G::N;
+    constexpr bool RLDS = SF <= 8;
+    float amax = 0.0f;
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) {
+        const int i = lam + e * G::LPS;
+        const cf32 x = raw[e];
+        cf32 y;
+        if (MIXED && est) {
+            cf32 p = x;
+            if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) {
+                if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+                    p = cmul(p, down[((unsigned)c.base + (unsigned)i) & (N - 1)]);
+                p = cscale(p, c.scale);
+            }
+            y = c.ok ? p : czero();
+            if constexpr ((MODE & kWinBit) != 0) y = cscale(y, win[i]);
+        } else {
+            y = cmul(x, RLDS ? rt[i] : rreg[e]);
+            if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE)
+                amax = fmaxf(amax, fmaxf(fabsf(x.x), fabsf(x.y)));
+        }
+        stg.put(lds, e, y);
+    }
+    return amax;
+}
+
 template <int SF, int MODE, int OCC>
 __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     using G = Geo<SF>;
@@ -766,6 +887,9 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     // symbols two tiles behind it like every later frame's
     constexpr unsigned PT = (U + WT - 1) / WT + 1;
     constexpr int WPB = kTile / 64;
+    // rotation tables: per-wave LDS ring of two frames up to SF 8, per-lane
+    // registers (built when a team reaches a new frame) for SF 9-10
+    constexpr bool RLDS = SF <= 8;
     const DemodArgs& A = P.A;
     __shared__ cf32 lds[G::T * G::SSTRIDE];
     __shared__ cf32 twl[N];
@@ -773,6 +897,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     __shared__ float wnl[TAB ? N : 1];
     __shared__ UnitResult ures[WPB][U];
     __shared__ float4 ring[WPB][3];  // frame records: rate, scale, t_off, flags
+    __shared__ cf32 rtab[RLDS ? WPB : 1][2][RLDS ? N : 1];
 
     const int tid = threadIdx.x;
     for (int i = tid; i < N; i += kTile) {
@@ -801,6 +926,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     const unsigned nk = (nframes - 1 - w) / W + 1;  // frames of this wave
     const unsigned long long L = (unsigned long long)PT * WT + (unsigned long long)nk * SL;
     const unsigned ntiles = (unsigned)((L + WT - 1) / WT);
+    const bool exact_only = A.exact_rotation != 0;
 
     // unit of this team in tile t; (k, o) = slice and offset for t >= PT
     auto unit_of = [&](unsigned t, unsigned k, unsigned o, unsigned& kind, unsigned& fk,
@@ -855,11 +981,36 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     }
     unsigned m_seq = 0xffffffffu;  // frame whose max-abs `mx` holds
     float mx = 0.0f;
+    cf32 rreg[16];                 // SF 9-10: the team's table ...
+    unsigned rreg_fk = 0xffffffffu;  // ... of this frame
+    unsigned long long rechecks = 0;
 
     for (unsigned t = 0; t < ntiles; ++t) {
+        // SF 9-10: a team entering a new frame builds its table entries
+        if constexpr (!RLDS) {
+            if (kind == kUnitSym && fk != rreg_fk) {
+                const unsigned t0 = (unsigned)c.toff & (N - 1);
+#pragma unroll
+                for (int e = 0; e < G::E; ++e) {
+                    const int i = lam + e * G::LPS;
+                    float sn, cs;
+                    lphy_libm::sincosf_exact(c.rate * (float)i, &sn, &cs);
+                    cf32 tv = cf32{cs, sn};
+                    if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) tv = cmul(down[i], tv);
+                    if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+                        tv = cmul(down[(t0 + (unsigned)i) & (N - 1)], tv);
+                    if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) tv = cscale(tv, c.scale);
+                    if constexpr ((MODE & kWinBit) != 0) tv = cscale(tv, win[i]);
+                    rreg[e] = tv;
+                }
+                rreg_fk = fk;
+            }
+        }
+        const cf32* rt = rtab[RLDS ? wv : 0][RLDS ? (fk & 1) : 0];
         // estimate units in this tile (all of one frame): its max-abs first
         const unsigned long long emask = __ballot(kind == kUnitEst);
         unsigned ke = 0;
+        float amax;
         if (emask) {
             ke = (unsigned)__shfl((int)fk, __ffsll((long long)emask) - 1, 64);
             if ((MODE & 3) != LPHY_MODE_DEMODULATE && ke != m_seq) {
@@ -878,11 +1029,15 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
                 }
                 c.ok = c.live;  // estimate this unit (else stage zeros)
             }
-            stage_mixed<SF, MODE>(lds, stg, raw, A.iq + (unsigned long long)c.f * A.frame_samples + c.base,
-                                  c, lam, down, win, kind != kUnitSym);
+            amax = stage_fast<SF, MODE, true>(lds, stg, raw, c, lam, down, win, rt, rreg, kind != kUnitSym);
         } else {
-            stage_symbol<SF, MODE>(lds, stg, raw, A.iq + (unsigned long long)c.f * A.frame_samples + c.base,
-                                   c, lam, down, win);
+            amax = stage_fast<SF, MODE, false>(lds, stg, raw, c, lam, down, win, rt, rreg, false);
+        }
+        if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) {
+#pragma unroll
+            for (int off = G::LPS / 2; off >= 1; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
+        } else {
+            amax = 1.0f;  // normalised frame: max(|I|,|Q|) <= 1 (see fast_certified)
         }
         team_sync<SF>();
 
@@ -906,7 +1061,8 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
 
         cf32 v[16];
         fft_tile<SF>(v, lds, slot, lam, twl);
-        const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), nullptr);
+        const ArgMax2 b2 = symbol_argmax2<SF>(local_argmax2<SF>(v, lam));
+        ArgMax best{b2.v, b2.i};
         if (emask) {
             // detector outputs of the estimate units (LoRaDetector.hpp:60-71)
             if (kind == kUnitEst) {
@@ -916,6 +1072,31 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             team_sync<SF>();
             if (kind == kUnitEst && lam == 0)
                 ures[wv][su] = c.ok ? unit_result<SF>(lds, slot, best) : UnitResult{0, 0, 0.0f, 0.0f};
+            team_sync<SF>();  // slot reads done before a re-check restages
+        }
+        // symbols the certificate does not cover: exact per-sample rotation
+        const bool redo = kind == kUnitSym && c.ok &&
+                          (exact_only || !fast_applies<SF, MODE>(c, c.toff) ||
+                           !fast_certified<SF>(b2, c, amax));
+        const unsigned long long rmask = __ballot(redo);
+        if (rmask) {
+            // one sample at a time: the re-check is rare, and a serial loop
+            // keeps its sincos temporaries out of the main path's registers
+            const cf32* src = A.iq + (unsigned long long)c.f * A.frame_samples + c.base;
+#pragma unroll 1
+            for (int e = 0; e < G::E; ++e) {
+                const int i = lam + e * G::LPS;
+                const float ph = c.start + c.rate * (float)i;
+                stg.put(lds, e, rotate_sample<SF, MODE>(src[i], i, c, down, win,
+                                                        lphy_libm::sincosf_needs_large(ph)));
+            }
+            team_sync<SF>();
+            cf32 vx[16];
+            fft_tile<SF>(vx, lds, slot, lam, twl);
+            const ArgMax ex = symbol_argmax<SF>(local_argmax<SF>(vx, lam), nullptr);
+            if (redo) best = ex;
+            rechecks += (unsigned long long)__popcll(rmask) / G::LPS;
+            team_sync<SF>();
         }
         if (kind == kUnitSym && lam == 0) {
             // sw0 / sw1 also for frames that are not demodulated (0, as the
@@ -925,7 +1106,8 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         }
         team_sync<SF>();  // slot reads (and ures) done
         // the frame whose last estimate unit was in this tile: fold
-        if (__ballot(kind == kUnitEst && su == U - 1) && lane == 0) {
+        const bool folding = __ballot(kind == kUnitEst && su == U - 1) != 0;
+        if (folding && lane == 0) {
             lphy_frame_meta m{};
             m.scale = 1.0f;
             m.have_sync = 1;
@@ -945,6 +1127,15 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             meta_put_est(&A.meta[w + ke * W], m);
         }
         team_sync<SF>();
+        if constexpr (RLDS) {
+            // the folded frame's rotation table, first read two tiles later
+            // (its slot's previous frame, ke - 2, has no units left)
+            if (folding) {
+                const float4 r = ring[wv][ke % 3];
+                if (__float_as_uint(r.w) & 1u)
+                    build_rtab<SF, MODE>(rtab[wv][ke & 1], r.x, r.y, __float_as_int(r.z), down, win, lane);
+            }
+        }
         k = nkk;
         o = no;
         kind = nkind;
@@ -952,6 +1143,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         su = nsu;
         c = nc;
     }
+    if (lane == 0 && rechecks) atomicAdd(&g_rechecks, rechecks);
 }
 
 // ---------------------------------------------------------------------------
@@ -1591,6 +1783,7 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     A.power_scale = c->power_scale;
     A.mode = mode;
     A.no_scratch = (flags & LPHY_F_NO_SCRATCH) ? 1 : 0;
+    A.exact_rotation = (flags & LPHY_F_EXACT_ROTATION) ? 1 : 0;
     const size_t est_syms = mode == LPHY_MODE_DEMODULATE ? 2 : (total < 2 ? total : 2);
     A.est_units = (int)(est_syms * c->osr);
     // 32-bit symbol / sample bookkeeping in the kernels
@@ -1752,6 +1945,18 @@ int lphy_hip_modulate_batch(lphy_hip_ctx* c, const uint16_t* d_syms, size_t fram
 
 int lphy_hip_sync(void* stream) {
     HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+    return 0;
+}
+
+int lphy_hip_recheck_count(lphy_hip_ctx* c, unsigned long long* out, int reset) {
+    if (!c || !out) return -EINVAL;
+    HIP_OK(hipSetDevice(c->device));
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rechecks), sizeof(*out)));
+    if (reset) {
+        const unsigned long long zero = 0;
+        HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_rechecks), &zero, sizeof(zero)));
+    }
     return 0;
 }
 

@@ -29,6 +29,7 @@ F_STAGE_PROLOGUE = 4
 F_STAGE_SYMBOLS = 8
 F_STAGE_FINAL = 16
 F_UNFUSED = 32  # separate prologue / symbol launches (lphy_hip.h)
+F_EXACT_ROTATION = 64  # fused launch without the certified per-frame rotation table
 WINDOW_NONE = 0
 WINDOW_HANN = 1
 
@@ -96,6 +97,7 @@ def load(path: Path = HIP_SO) -> C.CDLL:
     L.lphy_hip_compensate_host.argtypes = [_vp, _vp, _sz, C.c_float, C.c_float]
     L.lphy_hip_modulate_host.argtypes = [_vp, _vp, _sz, _vp, C.c_float, C.c_uint8]
     L.lphy_hip_sync.argtypes = [_vp]
+    L.lphy_hip_recheck_count.argtypes = [_vp, C.POINTER(C.c_ulonglong), C.c_int]
     L.lphy_hip_version.restype = C.c_char_p
     _LIB = L
     return L
@@ -202,6 +204,13 @@ class Demodulator:
                                              out.ctypes.data, amplitude, sync),
              "lphy_hip_modulate_host")
         return out
+
+    def recheck_count(self, reset: bool = True) -> int:
+        """Symbols the fused kernel re-ran with the exact rotation (device sync)."""
+        n = C.c_ulonglong(0)
+        _chk(self.lib.lphy_hip_recheck_count(self.ctx, C.byref(n), int(reset)),
+             "lphy_hip_recheck_count")
+        return int(n.value)
 
 
 def hamming84_encode_table() -> np.ndarray:
