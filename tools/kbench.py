@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Kernel-level timing driver for experiments (not the bench contract).
+
+Times the fused demodulation launch (PROLOGUE|SYMBOLS -> k_frames, or the
+separate kernels with --unfused) per mode on resident synthetic SF frames,
+with HIP events on the launch stream; optional alternative library builds
+(--so a.so,b.so) are timed one after the other in the same process.
+
+  python tools/kbench.py --sf 7 --frames 65536 --modes 0,2 --reps 10
+"""
+import argparse
+import ctypes
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+PKG = ROOT / "lora-sdr-lightweight-standalone-library-clean_amd"
+sys.path.insert(0, str(PKG))
+import lphy  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--sf", type=int, default=7)
+ap.add_argument("--frames", type=int, default=65536)
+ap.add_argument("--modes", default="0,2")
+ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--so", default="")
+ap.add_argument("--unfused", action="store_true")
+ap.add_argument("--exact", action="store_true")
+ap.add_argument("--check", action="store_true", help="compare outputs across builds")
+a = ap.parse_args()
+
+dev = torch.device("cuda:0")
+sos = [Path(p) for p in a.so.split(",") if p] or [lphy.HIP_SO]
+N = 1 << a.sf
+fs = 66 * N
+rng = np.random.default_rng(0x5EED + a.sf)
+pay = rng.integers(0, 256, (a.frames, 32), dtype=np.uint8)
+syms_in = torch.from_numpy(lphy.encode_payloads(pay).view(np.int16).reshape(-1).copy()).to(dev)
+iq = torch.empty(a.frames * fs * 2, dtype=torch.float32, device=dev)
+flags = lphy.F_DECODE | lphy.F_STAGE_PROLOGUE | lphy.F_STAGE_SYMBOLS
+if a.unfused:
+    flags |= lphy.F_UNFUSED
+if a.exact:
+    flags |= lphy.F_EXACT_ROTATION
+ref = {}
+for so in sos:
+    lphy._LIB = None
+    lphy.load(so)
+    d = lphy.Demodulator(a.sf)
+    st = torch.cuda.current_stream().cuda_stream
+    d.modulate_batch(syms_in, a.frames, 64, iq, 1.0, 0x12, st)
+    out = torch.zeros(a.frames * 64, dtype=torch.int16, device=dev)
+    meta = torch.zeros(a.frames * 32, dtype=torch.uint8, device=dev)
+    pl = torch.zeros(a.frames * 32, dtype=torch.uint8, device=dev)
+    for mode in [int(m) for m in a.modes.split(",")]:
+        d.demod_batch(iq, a.frames, fs, out, meta, mode, flags, payload=pl, stream=st)
+        torch.cuda.synchronize()
+        d.recheck_count(reset=True)
+        ts = []
+        for _ in range(a.reps):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            d.demod_batch(iq, a.frames, fs, out, meta, mode, flags, payload=pl, stream=st)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        rc = d.recheck_count(reset=True)
+        ms = float(np.median(ts))
+        gbs = a.frames * fs * 8 / ms / 1e6
+        line = f"{so.name:28s} SF{a.sf} mode {mode}: {ms:.4f} ms  {a.frames * 64 / ms / 1e6:.3f} Gsym/s  {gbs:.0f} GB/s  rechecks/launch {rc // a.reps}"
+        if a.check:
+            key = mode
+            o = out.cpu().numpy().copy()
+            if key in ref:
+                line += "  same" if np.array_equal(ref[key], o) else "  DIFFERENT"
+            else:
+                ref[key] = o
+        print(line, flush=True)
+    d.close()
