@@ -208,7 +208,14 @@ struct Group {
 
 // All butterflies of one pass on the lane's registers.  v[s*GS + a] is group
 // s, group-local index a.
-template <int SF, int HI, int LO>
+//
+// TRIV (symbol units of the certified fast path only): butterflies whose
+// twiddle index is 0 at compile time skip the product with tw[0] = (1, 0).
+// x * (1, 0) = (re - im*0, im + re*0) equals x up to the sign of an exact
+// zero (and NaN from an infinite component, which the certificate rejects),
+// so every |X|^2 - all a symbol unit keeps - is unchanged.  Estimate units
+// keep the multiply: their bins feed atan2, where the sign of a zero counts.
+template <int SF, int HI, int LO, bool TRIV = false>
 __device__ __forceinline__ void pass_butterflies(cf32 (&v)[16], int lam,
                                                  const cf32* __restrict__ tw) {
     using G = Geo<SF>;
@@ -224,15 +231,17 @@ __device__ __forceinline__ void pass_butterflies(cf32 (&v)[16], int lam,
             for (int a = 0; a < P::GS; ++a) {
                 if (P::digit(a, l) != 0) continue;
                 const int k = low + (a % w) * P::MH;
+                // twiddle index 0 for every lane: MH == 1 makes low == 0
+                const bool one = TRIV && P::MH == 1 && (a % w) == 0;
                 cf32* x = &v[s * P::GS];
                 if (R == 2) {
-                    const cf32 t = cmul(x[a + w], tw[k * fs]);
+                    const cf32 t = one ? x[a + w] : cmul(x[a + w], tw[k * fs]);
                     x[a + w] = csub(x[a], t);
                     x[a] = cadd(x[a], t);
                 } else {
-                    const cf32 s0 = cmul(x[a + w], tw[k * fs]);
-                    const cf32 s1 = cmul(x[a + 2 * w], tw[k * fs * 2]);
-                    const cf32 s2 = cmul(x[a + 3 * w], tw[k * fs * 3]);
+                    const cf32 s0 = one ? x[a + w] : cmul(x[a + w], tw[k * fs]);
+                    const cf32 s1 = one ? x[a + 2 * w] : cmul(x[a + 2 * w], tw[k * fs * 2]);
+                    const cf32 s2 = one ? x[a + 3 * w] : cmul(x[a + 3 * w], tw[k * fs * 3]);
                     const cf32 s5 = csub(x[a], s1);
                     const cf32 a0 = cadd(x[a], s1);
                     const cf32 s3 = cadd(s0, s2);
@@ -258,7 +267,7 @@ __device__ __forceinline__ void lds_st(cf32* lds, int byte_off, cf32 v) {
     *reinterpret_cast<cf32*>(reinterpret_cast<char*>(lds) + byte_off) = v;
 }
 
-template <int SF, int PI, bool LAST>
+template <int SF, int PI, bool LAST, bool TRIV>
 __device__ __forceinline__ void run_pass(cf32 (&v)[16], cf32* lds, int slot, int lam,
                                          const cf32* __restrict__ tw) {
     using G = Geo<SF>;
@@ -275,7 +284,7 @@ __device__ __forceinline__ void run_pass(cf32 (&v)[16], cf32* lds, int slot, int
 #pragma unroll
         for (int e = 0; e < G::E; ++e) v[e] = lds_ld(lds, G::at8(lb8, G::cpart(Gr::pos(e, 0)) << 3));
     }
-    pass_butterflies<SF, HI, LO>(v, lam, tw);
+    pass_butterflies<SF, HI, LO, TRIV>(v, lam, tw);
     if (!LAST) {
         const int lb8 = G::lbase(slot, Gr::pos(0, lam)) << 3;
 #pragma unroll
@@ -284,23 +293,24 @@ __device__ __forceinline__ void run_pass(cf32 (&v)[16], cf32* lds, int slot, int
     }
 }
 
-template <int SF, int PI>
+template <int SF, int PI, bool TRIV>
 __device__ __forceinline__ void run_passes(cf32 (&v)[16], cf32* lds, int slot, int lam,
                                            const cf32* __restrict__ tw) {
     constexpr Passes<SF> PS{};
     if constexpr (PI < PS.n) {
-        run_pass<SF, PI, PI == PS.n - 1>(v, lds, slot, lam, tw);
-        run_passes<SF, PI + 1>(v, lds, slot, lam, tw);
+        run_pass<SF, PI, PI == PS.n - 1, TRIV>(v, lds, slot, lam, tw);
+        run_passes<SF, PI + 1, TRIV>(v, lds, slot, lam, tw);
     }
 }
 
 // Full transform of the symbol staged (natural order) in `slot` of the tile
 // LDS; on return v[e] holds bin bin_of<SF>(e, lam).  Must be called by every
 // thread of the tile (contains barriers).
-template <int SF>
+// TRIV: see pass_butterflies (magnitude-only consumers).
+template <int SF, bool TRIV = false>
 __device__ __forceinline__ void fft_tile(cf32 (&v)[16], cf32* lds, int slot, int lam,
                                          const cf32* __restrict__ tw) {
-    run_passes<SF, 0>(v, lds, slot, lam, tw);
+    run_passes<SF, 0, TRIV>(v, lds, slot, lam, tw);
 }
 
 template <int SF>

@@ -668,45 +668,88 @@ __device__ __forceinline__ void meta_put_est(lphy_frame_meta* dst, const lphy_fr
 
 // Max-abs of frame f by one wavefront (16-byte loads, 8 in flight per
 // lane), same arithmetic as k_maxabs; the result is in every lane.
+//
+// Fast form of the aligned bulk (one v_max3 per sample): max(mx, |re|, |im|)
+// equals the reference's fold for samples without NaN, and the frame's
+// samples are summed alongside (one packed add per sample) so that any NaN
+// - or an overflow to inf, which could make one - sends the whole frame to
+// the per-sample fold above, whose NaN rules (a NaN real part hides the
+// sample) v_max3 does not have.  In mode 2 only the whole symbols are
+// scanned: the zeros the reference's dechirp leaves past them never raise
+// the maximum.
+__device__ __forceinline__ float max3_abs(float m, float a, float b) {
+    float r;
+    asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
+
 template <int SF, int MODE>
 __device__ __forceinline__ float wave_maxabs(const DemodArgs& A, unsigned f, const cf32* down) {
     constexpr int N = 1 << SF;
+    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     const int lane = threadIdx.x & 63;
     const cf32* fr = A.iq + (unsigned long long)f * A.frame_samples;
-    const unsigned count = (unsigned)A.frame_samples;
-    const unsigned dech_end = (unsigned)A.total_syms * N;
+    const unsigned count = DECH ? (unsigned)A.total_syms * N : (unsigned)A.frame_samples;
     float mx = 0.0f;
     auto acc = [&](cf32 x, unsigned i) {
-        if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
-            x = i < dech_end ? cmul(x, down[i & (N - 1)]) : czero();
+        if constexpr (DECH) x = cmul(x, down[i & (N - 1)]);
         maxabs_acc(mx, x);
     };
-    if ((reinterpret_cast<uintptr_t>(fr) & 15) == 0) {
+    // loads in flight per lane (measured at SF7: 16, 24, 32 and 33 - two
+    // rounds per 66-symbol frame - within 1 %; 16 spills least)
+#ifdef LPHY_MAXABS_U
+    constexpr int U = LPHY_MAXABS_U;
+#else
+    constexpr int U = 16;
+#endif
+    // chirp index of sample 2 (b + 64 u + lane) for a round base b = 64 U r:
+    // the 128 U r term vanishes mod N
+    static_assert((128 * U) % N == 0, "chirp phase of the unrolled scan");
+    bool exact = (reinterpret_cast<uintptr_t>(fr) & 15) != 0;
+    if (!exact) {
         const float4* f4 = reinterpret_cast<const float4*>(fr);
         const unsigned n4 = count / 2;
-#ifndef LPHY_MAXABS_U
-#define LPHY_MAXABS_U 16
-#endif
-        constexpr int U = LPHY_MAXABS_U;  // loads in flight per lane
-        unsigned j = lane;
-        for (; j + (U - 1) * 64 < n4; j += U * 64) {
-            float4 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = f4[j + u * 64];
+        float fm = 0.0f;
+        cf32 sum = czero();
+        auto round = [&](const float4 (&v)[U]) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const unsigned i = 2 * (j + u * 64);
-                acc(cf32{v[u].x, v[u].y}, i);
-                acc(cf32{v[u].z, v[u].w}, i + 1);
+                cf32 a = cf32{v[u].x, v[u].y}, b = cf32{v[u].z, v[u].w};
+                if constexpr (DECH) {
+                    const unsigned ci = (2u * (unsigned)lane + 128u * (unsigned)u) & (N - 1);
+                    a = cmul(a, down[ci]);
+                    b = cmul(b, down[(ci + 1) & (N - 1)]);
+                }
+                fm = max3_abs(fm, a.x, a.y);
+                fm = max3_abs(fm, b.x, b.y);
+                sum = sum + a;
+                sum = sum + b;
             }
+        };
+        unsigned base = 0;
+        for (; base + U * 64 <= n4; base += U * 64) {
+            float4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = f4[base + u * 64 + lane];
+            round(v);
         }
-        for (; j < n4; j += 64) {
-            const float4 v = f4[j];
-            acc(cf32{v.x, v.y}, 2 * j);
-            acc(cf32{v.z, v.w}, 2 * j + 1);
+        if (base < n4) {  // last partial round, zero-filled (zeros never raise the max)
+            float4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const unsigned j = base + u * 64 + lane;
+                v[u] = j < n4 ? f4[j] : float4{0.0f, 0.0f, 0.0f, 0.0f};
+            }
+            round(v);
         }
-        if ((count & 1) && lane == 0) acc(fr[count - 1], count - 1);
-    } else {
+        exact = __ballot(!(sum.x == sum.x && sum.y == sum.y)) != 0;
+        if (!exact) {
+            mx = fm;
+            if ((count & 1) && lane == 0) acc(fr[count - 1], count - 1);
+        }
+    }
+    if (exact) {
+        mx = 0.0f;
         for (unsigned i = lane; i < count; i += 64) acc(fr[i], i);
     }
 #pragma unroll
@@ -826,6 +869,10 @@ __device__ __forceinline__ bool fast_applies(const SymCtx& c, int t_off) {
 // The certificate of the header comment.  amax bounds max(|Re y|, |Im y|)
 // over the symbol's samples before rotation (modes 1/2: <= 1 after the
 // frame's normalisation; mode 0: measured).
+//
+// Range guards keep every rounding relative: amax >= 1e-20 (denormal
+// arithmetic stays negligible against B), b.v >= 1e-30 (a normal |X|^2), and
+// a runner-up below 1e-30 is taken as 1e-30.
 template <int SF>
 __device__ __forceinline__ bool fast_certified(const ArgMax2& b, const SymCtx& c, float amax) {
     constexpr int N = 1 << SF, L = (SF + 1) / 2;
@@ -834,8 +881,8 @@ __device__ __forceinline__ bool fast_certified(const ArgMax2& b, const SymCtx& c
     const float P = fabsf(c.start) + ar;
     const float B = kU * A * ((24.0f + 12.0f * L) + 2.0f * ar + P) * 1.001f;
     const float lhs = sqrtf(b.v) * (1.0f - 8.0f * kU) - 4.0f * B;
-    const float rhs = sqrtf(b.v2) * (1.0f + 8.0f * kU);
-    return lhs > rhs && A < 1e18f;
+    const float rhs = sqrtf(fmaxf(b.v2, 1e-30f)) * (1.0f + 8.0f * kU);
+    return lhs > rhs && A < 1e18f && amax >= 1e-20f && b.v >= 1e-30f;
 }
 
 // Fast staging of one tile: symbol units q_i = x_i * t_i from the frame's
@@ -973,14 +1020,36 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     unsigned kind, fk, su;
     unit_of(0, k, o, kind, fk, su);
     SymCtx c = ctx_of(kind, fk, su);
+    // M (modes 1/2): the max-abs scan of a frame runs in the tile before the
+    // one holding its first estimate unit, between that tile's staging and
+    // its IQ prefetch, when no tile data is held in registers (the scan keeps
+    // U = 32-33 loads in flight per lane); tile 0 holds E(0), scanned here
+    unsigned m_seq = 0xffffffffu;  // frame whose max-abs `mx` holds
+    float mx = 0.0f;
+    float mxe = 0.0f;              // max-abs of the frame estimated in this tile
+    auto scan_ahead = [&](unsigned nkind_, unsigned nfk_) {
+        if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) {
+            const unsigned long long nem = __ballot(nkind_ == kUnitEst);
+            if (nem) {
+                const unsigned nke = (unsigned)__shfl((int)nfk_, __ffsll((long long)nem) - 1, 64);
+                if (nke != m_seq) {
+#ifdef LPHY_ABLATE_FRAME_SCAN  // timing experiments only
+                    mx = 1.0f;
+#else
+                    mx = wave_maxabs<SF, MODE>(A, w + nke * W, down);
+#endif
+                    m_seq = nke;
+                }
+            }
+        }
+    };
+    scan_ahead(kind, fk);
     cf32 raw[16];
     {
         const cf32* src = A.iq + (unsigned long long)c.f * A.frame_samples + c.base;
 #pragma unroll
         for (int e = 0; e < G::E; ++e) raw[e] = src[lam + e * G::LPS];
     }
-    unsigned m_seq = 0xffffffffu;  // frame whose max-abs `mx` holds
-    float mx = 0.0f;
     cf32 rreg[16];                 // SF 9-10: the team's table ...
     unsigned rreg_fk = 0xffffffffu;  // ... of this frame
     unsigned long long rechecks = 0;
@@ -1013,17 +1082,10 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         float amax;
         if (emask) {
             ke = (unsigned)__shfl((int)fk, __ffsll((long long)emask) - 1, 64);
-            if ((MODE & 3) != LPHY_MODE_DEMODULATE && ke != m_seq) {
-#ifdef LPHY_ABLATE_FRAME_SCAN  // timing experiments only
-                mx = 1.0f;
-#else
-                mx = wave_maxabs<SF, MODE>(A, w + ke * W, down);
-#endif
-                m_seq = ke;
-            }
+            mxe = mx;  // scanned ahead (frame ke == m_seq)
             if (kind == kUnitEst) {
                 if ((MODE & 3) != LPHY_MODE_DEMODULATE) {
-                    const lphy_frame_meta nm = norm_meta(mx, true, A.no_scratch);
+                    const lphy_frame_meta nm = norm_meta(mxe, true, A.no_scratch);
                     c.scale = nm.scale;
                     c.live = nm.status == 0;
                 }
@@ -1052,6 +1114,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         }
         unsigned nkind, nfk, nsu;
         unit_of(t + 1, nkk, no, nkind, nfk, nsu);
+        if (t + 1 < ntiles) scan_ahead(nkind, nfk);
         const SymCtx nc = ctx_of(nkind, nfk, nsu);
         if (t + 1 < ntiles) {
             const cf32* nsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base;
@@ -1060,7 +1123,11 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         }
 
         cf32 v[16];
-        fft_tile<SF>(v, lds, slot, lam, twl);
+        // tiles of symbol units only: magnitude-only transform (fft_tile TRIV)
+        // (measured alternative: a packed-key max/min tournament for the top
+        // two, 3 % slower than this ordered scan)
+        if (emask) fft_tile<SF>(v, lds, slot, lam, twl);
+        else fft_tile<SF, true>(v, lds, slot, lam, twl);
         const ArgMax2 b2 = symbol_argmax2<SF>(local_argmax2<SF>(v, lam));
         ArgMax best{b2.v, b2.i};
         if (emask) {
@@ -1111,7 +1178,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             lphy_frame_meta m{};
             m.scale = 1.0f;
             m.have_sync = 1;
-            if ((MODE & 3) != LPHY_MODE_DEMODULATE) m = norm_meta(mx, true, A.no_scratch);
+            if ((MODE & 3) != LPHY_MODE_DEMODULATE) m = norm_meta(mxe, true, A.no_scratch);
             if (m.status == 0) {
                 EstFold fold;
 #pragma unroll

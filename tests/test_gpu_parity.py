@@ -188,3 +188,51 @@ def test_fused_no_scratch_mixed(oracle, lphy):
                 assert meta["status"][f] == 0
                 r, osyms, osync, omet = oracle.lora_demodulate(dech, sf)
                 np.testing.assert_array_equal(syms[f], osyms)
+
+
+def test_nonfinite_frames_maxabs(oracle, lphy):
+    """The fused max-abs scan's fast form (v_max3 + NaN sentinel) against the
+    reference's per-sample fold (LoRaDemod.cpp:62-66) on frames carrying a
+    NaN real part beside a large imaginary part (the sample is hidden), a
+    NaN imaginary part (the real part still counts), inf, values whose
+    dechirp overflows, and a NaN in the partial-symbol tail (scanned only
+    without the fused dechirp).  Both normalising modes, fused and separate
+    launches, every output against the oracle."""
+    sf, N = 7, 128
+    base = oracle.modulate(oracle.encode(bytes(range(16))), sf)
+    tail = 5
+    fs = base.size + tail
+    frames = []
+    for k in range(8):
+        x = np.concatenate([base * 0.8, np.zeros(tail, np.complex64)]).astype(np.complex64)
+        if k == 1:
+            x[300] = np.complex64(complex(np.nan, 5.0))
+        elif k == 2:
+            x[301] = np.complex64(complex(3.0, np.nan))
+        elif k == 3:
+            x[4000] = np.complex64(complex(np.inf, 0.25))
+        elif k == 4:
+            x[777] = np.complex64(complex(3.0e38, -3.0e38))
+        elif k == 5:
+            x[fs - 2] = np.complex64(complex(np.nan, 7.0))
+        elif k == 6:
+            x[fs - 1] = np.complex64(complex(9.0, 0.0))
+        elif k == 7:
+            x[40] = np.complex64(complex(-np.inf, np.nan))
+        frames.append(x)
+    iq = np.stack(frames)
+    nf = iq.shape[0]
+    d = lphy.Demodulator(sf)
+    for mode in (lphy.MODE_LORA_DEMODULATE, lphy.MODE_DECHIRP_LORA_DEMODULATE):
+        # the fused dechirp takes whole symbols only (-EINVAL otherwise)
+        x = iq if mode == lphy.MODE_LORA_DEMODULATE else np.ascontiguousarray(iq[:, :base.size])
+        for flags in (0, lphy.F_UNFUSED):
+            syms, _, meta = d.demod_host(x, nf, x.shape[1], mode, flags)
+            for f in range(nf):
+                src = x[f] if mode == lphy.MODE_LORA_DEMODULATE else oracle.dechirp(x[f], sf)
+                r, osyms, osync, omet = oracle.lora_demodulate(src, sf)
+                ctx = f"mode {mode} flags {flags} frame {f}"
+                assert meta["status"][f] == 0, ctx
+                np.testing.assert_array_equal(syms[f], osyms, err_msg=ctx)
+                assert _bits(meta["cfo"][f]) == _bits(omet[0]), ctx
+                assert _bits(meta["time_offset"][f]) == _bits(omet[1]), ctx

@@ -30,6 +30,7 @@ ap.add_argument("--so", default="")
 ap.add_argument("--unfused", action="store_true")
 ap.add_argument("--exact", action="store_true")
 ap.add_argument("--check", action="store_true", help="compare outputs across builds")
+ap.add_argument("--rounds", type=int, default=1, help="interleave the builds this many times")
 a = ap.parse_args()
 
 dev = torch.device("cuda:0")
@@ -46,38 +47,49 @@ if a.unfused:
 if a.exact:
     flags |= lphy.F_EXACT_ROTATION
 ref = {}
+dems = []
 for so in sos:
     lphy._LIB = None
     lphy.load(so)
-    d = lphy.Demodulator(a.sf)
-    st = torch.cuda.current_stream().cuda_stream
-    d.modulate_batch(syms_in, a.frames, 64, iq, 1.0, 0x12, st)
-    out = torch.zeros(a.frames * 64, dtype=torch.int16, device=dev)
-    meta = torch.zeros(a.frames * 32, dtype=torch.uint8, device=dev)
-    pl = torch.zeros(a.frames * 32, dtype=torch.uint8, device=dev)
-    for mode in [int(m) for m in a.modes.split(",")]:
-        d.demod_batch(iq, a.frames, fs, out, meta, mode, flags, payload=pl, stream=st)
-        torch.cuda.synchronize()
-        d.recheck_count(reset=True)
-        ts = []
-        for _ in range(a.reps):
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record()
+    dems.append((so, lphy.Demodulator(a.sf)))
+st = torch.cuda.current_stream().cuda_stream
+dems[0][1].modulate_batch(syms_in, a.frames, 64, iq, 1.0, 0x12, st)
+out = torch.zeros(a.frames * 64, dtype=torch.int16, device=dev)
+meta = torch.zeros(a.frames * 32, dtype=torch.uint8, device=dev)
+pl = torch.zeros(a.frames * 32, dtype=torch.uint8, device=dev)
+modes = [int(m) for m in a.modes.split(",")]
+times = {}
+rcs = {}
+for r in range(a.rounds):
+    for so, d in dems:
+        for mode in modes:
             d.demod_batch(iq, a.frames, fs, out, meta, mode, flags, payload=pl, stream=st)
-            e1.record()
             torch.cuda.synchronize()
-            ts.append(e0.elapsed_time(e1))
-        rc = d.recheck_count(reset=True)
-        ms = float(np.median(ts))
+            d.recheck_count(reset=True)
+            ts = []
+            for _ in range(a.reps):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                d.demod_batch(iq, a.frames, fs, out, meta, mode, flags, payload=pl, stream=st)
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            rcs[(so, mode)] = d.recheck_count(reset=True) // a.reps
+            times.setdefault((so, mode), []).append(float(np.median(ts)))
+            if a.check and r == 0:
+                o = out.cpu().numpy().copy()
+                if mode in ref:
+                    if not np.array_equal(ref[mode], o):
+                        print(f"{so.name} mode {mode}: OUTPUT DIFFERS from {sos[0].name}", flush=True)
+                else:
+                    ref[mode] = o
+for so, d in dems:
+    for mode in modes:
+        v = times[(so, mode)]
+        ms = float(np.median(v))
         gbs = a.frames * fs * 8 / ms / 1e6
-        line = f"{so.name:28s} SF{a.sf} mode {mode}: {ms:.4f} ms  {a.frames * 64 / ms / 1e6:.3f} Gsym/s  {gbs:.0f} GB/s  rechecks/launch {rc // a.reps}"
-        if a.check:
-            key = mode
-            o = out.cpu().numpy().copy()
-            if key in ref:
-                line += "  same" if np.array_equal(ref[key], o) else "  DIFFERENT"
-            else:
-                ref[key] = o
-        print(line, flush=True)
+        print(f"{so.name:28s} SF{a.sf} mode {mode}: {ms:.4f} ms (min {min(v):.4f})  "
+              f"{a.frames * 64 / ms / 1e6:.3f} Gsym/s  {gbs:.0f} GB/s  rechecks/launch {rcs[(so, mode)]}",
+              flush=True)
     d.close()
