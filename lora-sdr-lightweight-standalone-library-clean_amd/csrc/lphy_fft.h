@@ -161,13 +161,19 @@ struct PassGeo {
 
 // Synchronisation of the lanes that share a symbol ("team" of LPS lanes).
 // Up to LPS = 64 a team lives inside one wavefront: its LDS exchanges only
-// need this wave's LDS operations drained and no compiler motion across the
-// point (a wave's LDS instructions execute in order).  Larger teams span
+// need no compiler motion across the point (a wave's LDS instructions
+// execute in order, so a read issued after a write sees it).  Larger teams span
 // wavefronts and need the workgroup barrier.
 template <int SF>
 __device__ __forceinline__ void team_sync() {
     if constexpr (Geo<SF>::LPS <= 64) {
+#ifdef LPHY_TEAM_WAIT  // experiments: drain the wave's LDS queue (7 % slower)
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+#else
+        // a wave's LDS operations execute in issue order, so a team inside
+        // one wavefront only needs compiler motion across the point stopped
+        asm volatile("" ::: "memory");
+#endif
         __builtin_amdgcn_wave_barrier();
     } else {
         __syncthreads();

@@ -1022,8 +1022,12 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     SymCtx c = ctx_of(kind, fk, su);
     // M (modes 1/2): the max-abs scan of a frame runs in the tile before the
     // one holding its first estimate unit, between that tile's staging and
-    // its IQ prefetch, when no tile data is held in registers (the scan keeps
-    // U = 32-33 loads in flight per lane); tile 0 holds E(0), scanned here
+    // its IQ prefetch, when no tile data is held in registers; tile 0 holds
+    // E(0), scanned here.  (Measured alternative, 1.4x slower at SF7: the
+    // scan streamed one chunk per tile through a per-wave LDS buffer by
+    // LDS-DMA, issued after staging and folded a tile later - never behind
+    // the estimates, yet the chunk traffic and its folds cost more than the
+    // blocking scan's exposed latency.)
     unsigned m_seq = 0xffffffffu;  // frame whose max-abs `mx` holds
     float mx = 0.0f;
     float mxe = 0.0f;              // max-abs of the frame estimated in this tile
