@@ -160,6 +160,27 @@ int lphy_hip_modulate_host(lphy_hip_ctx* ctx, const uint16_t* h_syms,
                            size_t nsyms, float* h_iq, float amplitude,
                            uint8_t sync);
 
+/* Streaming ingestion.  Reads the reference receive
+ * runner's input format - float32 (I, Q) pairs back to back, from a file or
+ * stdin (runners/rx_runner.cpp:61-79) - from file descriptor `fd` until EOF
+ * (or `max_frames` frames when non-zero) as consecutive frames of
+ * `frame_samples` samples, and demodulates them (lphy_hip_demod_batch,
+ * `mode`, `flags`) in chunks of `chunk_frames`: the read of one chunk into
+ * pinned host memory and its H2D copy (copy stream) overlap the
+ * demodulation of the previous one (compute stream).  Results land in the
+ * caller's host arrays in stream order (frame f at h_syms +
+ * f*lphy_hip_syms_per_frame, h_bytes + f*(syms/2) with LPHY_F_DECODE,
+ * h_meta + f), sized for the frames the stream can hold.  Synchronous.
+ * *frames_out = whole frames demodulated; *tail_bytes (optional) = bytes of
+ * a trailing partial frame, which is not demodulated (the runner rejects a
+ * partial symbol count, rx_runner.cpp:87-91).  Returns 0, -EINVAL, -EIO
+ * (read or HIP error) or a lphy_hip_demod_batch shape error. */
+int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_samples,
+                          size_t chunk_frames, int mode, unsigned flags,
+                          size_t max_frames, uint16_t* h_syms, uint8_t* h_bytes,
+                          lphy_frame_meta* h_meta, size_t* frames_out,
+                          size_t* tail_bytes);
+
 /* Wait for all work queued on `stream`. */
 int lphy_hip_sync(void* stream);
 

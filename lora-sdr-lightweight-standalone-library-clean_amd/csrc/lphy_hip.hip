@@ -1761,6 +1761,10 @@ extern "C" {
 
 const char* lphy_hip_version(void) { return "lphy_hip 0.1 gfx950"; }
 
+// Internal (not in include/lphy_hip.h): the context's HIP device, for the
+// streaming ingestion in lphy_stream.hip.
+int lphy_hip_ctx_device(const lphy_hip_ctx* c) { return c ? c->device : -1; }
+
 int lphy_hip_ctx_create(lphy_hip_ctx** out, int device, unsigned sf, unsigned bw_hz,
                         unsigned osr, int window) {
     if (!out) return -EINVAL;

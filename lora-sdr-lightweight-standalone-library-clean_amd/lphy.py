@@ -60,7 +60,7 @@ EXPORTS = (
     "lphy_hip_demod_batch", "lphy_hip_decode_batch", "lphy_hip_estimate_batch",
     "lphy_hip_compensate", "lphy_hip_modulate_batch", "lphy_hip_demod_host",
     "lphy_hip_decode_host", "lphy_hip_estimate_host", "lphy_hip_compensate_host",
-    "lphy_hip_modulate_host", "lphy_hip_sync", "lphy_hip_version",
+    "lphy_hip_modulate_host", "lphy_hip_demod_stream", "lphy_hip_sync", "lphy_hip_version",
 )
 
 _LIB = None
@@ -96,6 +96,8 @@ def load(path: Path = HIP_SO) -> C.CDLL:
     L.lphy_hip_estimate_host.argtypes = [_vp, _vp, _sz, _vp]
     L.lphy_hip_compensate_host.argtypes = [_vp, _vp, _sz, C.c_float, C.c_float]
     L.lphy_hip_modulate_host.argtypes = [_vp, _vp, _sz, _vp, C.c_float, C.c_uint8]
+    L.lphy_hip_demod_stream.argtypes = [_vp, C.c_int, _sz, _sz, C.c_int, C.c_uint, _sz, _vp, _vp,
+                                        _vp, C.POINTER(_sz), C.POINTER(_sz)]
     L.lphy_hip_sync.argtypes = [_vp]
     L.lphy_hip_recheck_count.argtypes = [_vp, C.POINTER(C.c_ulonglong), C.c_int]
     L.lphy_hip_version.restype = C.c_char_p
@@ -159,6 +161,31 @@ class Demodulator:
         _chk(self.lib.lphy_hip_decode_batch(self.ctx, _ptr(syms), frames, syms_per_frame,
                                             _ptr(payload), _ptr(meta), stream),
              "lphy_hip_decode_batch")
+
+    # --- streaming ingestion (lphy_hip_demod_stream) --------------------
+    def demod_stream(self, fd: int, frame_samples: int, mode: int, flags: int = 0,
+                     chunk_frames: int = 4096, max_frames: int = 0, capacity: int = 0):
+        """Demodulate the float32 I/Q frames read from `fd` until EOF (or
+        max_frames).  `capacity` bounds the frames the result arrays hold
+        (default: max_frames).  Returns (symbols, payload, meta, tail_bytes)
+        for the whole frames read."""
+        cap = capacity or max_frames
+        if cap <= 0:
+            raise ValueError("capacity or max_frames required")
+        if not max_frames:
+            max_frames = cap
+        per = self.syms_per_frame(frame_samples, mode)
+        syms = np.zeros(max(cap * per, 1), np.uint16)
+        payload = np.zeros(max(cap * (per // 2), 1), np.uint8)
+        meta = np.zeros(cap, META_DTYPE)
+        nout, tail = _sz(0), _sz(0)
+        _chk(self.lib.lphy_hip_demod_stream(self.ctx, fd, frame_samples, chunk_frames, mode, flags,
+                                            max_frames, syms.ctypes.data, payload.ctypes.data,
+                                            meta.ctypes.data, C.byref(nout), C.byref(tail)),
+             "lphy_hip_demod_stream")
+        n = nout.value
+        return (syms[: n * per].reshape(n, per), payload[: n * (per // 2)].reshape(n, per // 2),
+                meta[:n], tail.value)
 
     # --- host convenience ----------------------------------------------
     def demod_host(self, iq: np.ndarray, frames: int, frame_samples: int, mode: int,
