@@ -2,13 +2,20 @@
  * @file lora_phy/phy.hpp
  * lora_phy:: C++17 API of the MI355X LoRa PHY (liblora_phy_amd.so).
  *
- * Source- and ABI-compatible replacement for the reference header
- * /root/reference/include/lora_phy/phy.hpp:
+ * Replacement for the reference header /root/reference/include/lora_phy/
+ * phy.hpp, source- and ABI/layout-compatible for its public API:
  *   - the same free functions with the same signatures and negative-errno
  *     returns (reference phy.hpp:104-161, 195-224);
  *   - the same caller-owned structs with the same field sets, sizes and
  *     offsets (lora_workspace 66,136 B, lora_demod_workspace 115,064 B on
- *     x86-64; tests/test_abi.py compares them against the reference build).
+ *     x86-64; tests/test_abi_cpu.py compares them against the reference
+ *     build).
+ * Not carried over: the reference's internal FFT / detector classes
+ * (kissfft.hh, LoRaDetector.hpp).  lora_demod_workspace keeps their storage
+ * as opaque bytes (fft / detector are void*), so code that reaches into
+ * those objects does not compile against this header.  The codec helpers
+ * (LoRaCodes.hpp) and the chirp generator (ChirpGenerator.hpp) are shipped
+ * beside it.
  * Demodulation, offset estimation, compensation, decoding and modulation run
  * on the GPU through the C ABI in lphy_hip.h; the structs here only carry
  * configuration and results between calls, as in the reference.

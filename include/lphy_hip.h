@@ -163,14 +163,16 @@ int lphy_hip_modulate_host(lphy_hip_ctx* ctx, const uint16_t* h_syms,
 /* Streaming ingestion.  Reads the reference receive
  * runner's input format - float32 (I, Q) pairs back to back, from a file or
  * stdin (runners/rx_runner.cpp:61-79) - from file descriptor `fd` until EOF
- * (or `max_frames` frames when non-zero) as consecutive frames of
+ * or `max_frames` frames, whichever comes first, as consecutive frames of
  * `frame_samples` samples, and demodulates them (lphy_hip_demod_batch,
  * `mode`, `flags`) in chunks of `chunk_frames`: the read of one chunk into
  * pinned host memory and its H2D copy (copy stream) overlap the
  * demodulation of the previous one (compute stream).  Results land in the
  * caller's host arrays in stream order (frame f at h_syms +
  * f*lphy_hip_syms_per_frame, h_bytes + f*(syms/2) with LPHY_F_DECODE,
- * h_meta + f), sized for the frames the stream can hold.  Synchronous.
+ * h_meta + f).  `max_frames` is their capacity in frames and is required
+ * (0 gives -EINVAL): reading stops there and the rest of the stream is left
+ * unread on `fd` for a later call.  Synchronous.
  * *frames_out = whole frames demodulated; *tail_bytes (optional) = bytes of
  * a trailing partial frame, which is not demodulated (the runner rejects a
  * partial symbol count, rx_runner.cpp:87-91).  Returns 0, -EINVAL, -EIO

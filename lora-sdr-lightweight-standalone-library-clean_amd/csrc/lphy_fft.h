@@ -46,6 +46,58 @@ __device__ __forceinline__ cf32 cmul(cf32 a, cf32 b) {
     asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(P), "v"(Q));
     return r;
 }
+// The reference's std::complex<float> product is GCC's inline formula plus a
+// call to __mulsc3 when BOTH parts come out NaN (built without
+// -fcx-limited-range): C99 Annex G.5.1's recovery of infinities, which boxes
+// an infinite factor to +-1 / +-0, zeroes NaNs of the other factor and
+// recomputes times infinity.  cmul_x is that product.  Only the exact paths
+// use it directly; the hot paths run cmul and detect the case afterwards
+// (see fft_has_nan): a (NaN, NaN) product anywhere reaches at least one bin
+// of the transform as NaN, and without one cmul == cmul_x bit for bit.
+__device__ __attribute__((noinline)) cf32 cmul_recover(float a, float b, float c, float d) {
+    const float ac = a * c, bd = b * d, ad = a * d, bc = b * c;
+    cf32 r = cf32{ac - bd, ad + bc};
+    bool recalc = false;
+    if (__builtin_isinf(a) || __builtin_isinf(b)) {
+        a = __builtin_copysignf(__builtin_isinf(a) ? 1.0f : 0.0f, a);
+        b = __builtin_copysignf(__builtin_isinf(b) ? 1.0f : 0.0f, b);
+        if (__builtin_isnan(c)) c = __builtin_copysignf(0.0f, c);
+        if (__builtin_isnan(d)) d = __builtin_copysignf(0.0f, d);
+        recalc = true;
+    }
+    if (__builtin_isinf(c) || __builtin_isinf(d)) {
+        c = __builtin_copysignf(__builtin_isinf(c) ? 1.0f : 0.0f, c);
+        d = __builtin_copysignf(__builtin_isinf(d) ? 1.0f : 0.0f, d);
+        if (__builtin_isnan(a)) a = __builtin_copysignf(0.0f, a);
+        if (__builtin_isnan(b)) b = __builtin_copysignf(0.0f, b);
+        recalc = true;
+    }
+    if (!recalc && (__builtin_isinf(ac) || __builtin_isinf(bd) || __builtin_isinf(ad) ||
+                    __builtin_isinf(bc))) {
+        if (__builtin_isnan(a)) a = __builtin_copysignf(0.0f, a);
+        if (__builtin_isnan(b)) b = __builtin_copysignf(0.0f, b);
+        if (__builtin_isnan(c)) c = __builtin_copysignf(0.0f, c);
+        if (__builtin_isnan(d)) d = __builtin_copysignf(0.0f, d);
+        recalc = true;
+    }
+    if (recalc) {
+        const float inf = __builtin_inff();
+        r.x = inf * (a * c - b * d);
+        r.y = inf * (a * d + b * c);
+    }
+    return r;
+}
+__device__ __forceinline__ cf32 cmul_x(cf32 a, cf32 b) {
+    const cf32 r = cmul(a, b);
+    if (__builtin_expect(__builtin_isnan(r.x) && __builtin_isnan(r.y), 0))
+        return cmul_recover(a.x, a.y, b.x, b.y);
+    return r;
+}
+template <bool AG>
+__device__ __forceinline__ cf32 cmul_t(cf32 a, cf32 b) {
+    if constexpr (AG) return cmul_x(a, b);
+    else return cmul(a, b);
+}
 // KISS radix-4 cross terms with scratch[4] = (s4.y, -s4.x) folded into the
 // operand modifiers (kissfft.hh:178-183): a + (b.y, -b.x) and a - (b.y, -b.x).
 __device__ __forceinline__ cf32 cadd_rot(cf32 a, cf32 b) {
@@ -221,7 +273,7 @@ struct Group {
 // zero (and NaN from an infinite component, which the certificate rejects),
 // so every |X|^2 - all a symbol unit keeps - is unchanged.  Estimate units
 // keep the multiply: their bins feed atan2, where the sign of a zero counts.
-template <int SF, int HI, int LO, bool TRIV = false>
+template <int SF, int HI, int LO, bool TRIV = false, bool AG = false>
 __device__ __forceinline__ void pass_butterflies(cf32 (&v)[16], int lam,
                                                  const cf32* __restrict__ tw) {
     using G = Geo<SF>;
@@ -241,13 +293,13 @@ __device__ __forceinline__ void pass_butterflies(cf32 (&v)[16], int lam,
                 const bool one = TRIV && P::MH == 1 && (a % w) == 0;
                 cf32* x = &v[s * P::GS];
                 if (R == 2) {
-                    const cf32 t = one ? x[a + w] : cmul(x[a + w], tw[k * fs]);
+                    const cf32 t = one ? x[a + w] : cmul_t<AG>(x[a + w], tw[k * fs]);
                     x[a + w] = csub(x[a], t);
                     x[a] = cadd(x[a], t);
                 } else {
-                    const cf32 s0 = one ? x[a + w] : cmul(x[a + w], tw[k * fs]);
-                    const cf32 s1 = one ? x[a + 2 * w] : cmul(x[a + 2 * w], tw[k * fs * 2]);
-                    const cf32 s2 = one ? x[a + 3 * w] : cmul(x[a + 3 * w], tw[k * fs * 3]);
+                    const cf32 s0 = one ? x[a + w] : cmul_t<AG>(x[a + w], tw[k * fs]);
+                    const cf32 s1 = one ? x[a + 2 * w] : cmul_t<AG>(x[a + 2 * w], tw[k * fs * 2]);
+                    const cf32 s2 = one ? x[a + 3 * w] : cmul_t<AG>(x[a + 3 * w], tw[k * fs * 3]);
                     const cf32 s5 = csub(x[a], s1);
                     const cf32 a0 = cadd(x[a], s1);
                     const cf32 s3 = cadd(s0, s2);
@@ -273,7 +325,7 @@ __device__ __forceinline__ void lds_st(cf32* lds, int byte_off, cf32 v) {
     *reinterpret_cast<cf32*>(reinterpret_cast<char*>(lds) + byte_off) = v;
 }
 
-template <int SF, int PI, bool LAST, bool TRIV>
+template <int SF, int PI, bool LAST, bool TRIV, bool AG>
 __device__ __forceinline__ void run_pass(cf32 (&v)[16], cf32* lds, int slot, int lam,
                                          const cf32* __restrict__ tw) {
     using G = Geo<SF>;
@@ -290,7 +342,7 @@ __device__ __forceinline__ void run_pass(cf32 (&v)[16], cf32* lds, int slot, int
 #pragma unroll
         for (int e = 0; e < G::E; ++e) v[e] = lds_ld(lds, G::at8(lb8, G::cpart(Gr::pos(e, 0)) << 3));
     }
-    pass_butterflies<SF, HI, LO, TRIV>(v, lam, tw);
+    pass_butterflies<SF, HI, LO, TRIV, AG>(v, lam, tw);
     if (!LAST) {
         const int lb8 = G::lbase(slot, Gr::pos(0, lam)) << 3;
 #pragma unroll
@@ -299,13 +351,13 @@ __device__ __forceinline__ void run_pass(cf32 (&v)[16], cf32* lds, int slot, int
     }
 }
 
-template <int SF, int PI, bool TRIV>
+template <int SF, int PI, bool TRIV, bool AG>
 __device__ __forceinline__ void run_passes(cf32 (&v)[16], cf32* lds, int slot, int lam,
                                            const cf32* __restrict__ tw) {
     constexpr Passes<SF> PS{};
     if constexpr (PI < PS.n) {
-        run_pass<SF, PI, PI == PS.n - 1, TRIV>(v, lds, slot, lam, tw);
-        run_passes<SF, PI + 1, TRIV>(v, lds, slot, lam, tw);
+        run_pass<SF, PI, PI == PS.n - 1, TRIV, AG>(v, lds, slot, lam, tw);
+        run_passes<SF, PI + 1, TRIV, AG>(v, lds, slot, lam, tw);
     }
 }
 
@@ -313,10 +365,26 @@ __device__ __forceinline__ void run_passes(cf32 (&v)[16], cf32* lds, int slot, i
 // LDS; on return v[e] holds bin bin_of<SF>(e, lam).  Must be called by every
 // thread of the tile (contains barriers).
 // TRIV: see pass_butterflies (magnitude-only consumers).
-template <int SF, bool TRIV = false>
+// AG: every product with the reference's Annex G recovery (cmul_x).
+template <int SF, bool TRIV = false, bool AG = false>
 __device__ __forceinline__ void fft_tile(cf32 (&v)[16], cf32* lds, int slot, int lam,
                                          const cf32* __restrict__ tw) {
-    run_passes<SF, 0, TRIV>(v, lds, slot, lam, tw);
+    run_passes<SF, 0, TRIV, AG>(v, lds, slot, lam, tw);
+}
+
+// Whether any of the lane's bins has a NaN part: the trigger for re-running
+// a transform (and the products staged into it) with cmul_x.  Sums the
+// detector's |X|^2 values (>= 0 or NaN, so the sum is NaN exactly when one
+// of them is); written like local_argmax so the compiler shares them.
+template <int SF>
+__device__ __forceinline__ bool fft_has_nan(const cf32 (&v)[16]) {
+    float s = 0.0f;
+#pragma unroll
+    for (int e = 0; e < Geo<SF>::E; ++e) {
+        const cf32 sq = v[e] * v[e];
+        s += sq.x + sq.y;
+    }
+    return s != s;
 }
 
 template <int SF>

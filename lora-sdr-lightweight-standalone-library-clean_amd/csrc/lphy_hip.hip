@@ -102,7 +102,7 @@ __device__ __forceinline__ cf32 est_sample(const DemodArgs& A, const cf32* fr,
                                              const lphy_frame_meta& m) {
     cf32 x = fr[idx];
     if (A.mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
-        x = idx < A.total_syms * (unsigned long long)N ? cmul(x, A.down[idx & (N - 1)])
+        x = idx < A.total_syms * (unsigned long long)N ? cmul_x(x, A.down[idx & (N - 1)])
                                                        : czero();
     if (A.mode != LPHY_MODE_DEMODULATE && m.normalised) x = cscale(x, m.scale);
     if (A.win) x = cscale(x, A.win[i]);
@@ -118,6 +118,12 @@ __device__ __forceinline__ void maxabs_acc(float& mx, cf32 x) {
     if (m > mx) mx = m;
 }
 
+// Internal frame status between the launches of one lphy_hip_demod_batch:
+// the frame holds a non-finite value where the reference's Annex G complex
+// product (cmul_x) could differ from the hot kernels' plain one, and is
+// re-run exactly by k_post.  Never left in a record after the call.
+constexpr int kStatusFixup = 0x7f5a0001;
+
 // Normalisation decision of LoRaDemod.cpp:60-78 from the frame's max-abs.
 __device__ __forceinline__ lphy_frame_meta norm_meta(float mx, bool have_sync, int no_scratch) {
     lphy_frame_meta m{};
@@ -128,6 +134,13 @@ __device__ __forceinline__ lphy_frame_meta norm_meta(float mx, bool have_sync, i
         m.normalised = 1;
         m.scale = 1.0f / mx;
     }
+    return m;
+}
+// The same in the hot kernels, whose scans return NaN for a frame with a
+// non-finite sample: that frame goes to the exact re-run.
+__device__ __forceinline__ lphy_frame_meta norm_meta_hot(float mx, bool have_sync, int no_scratch) {
+    lphy_frame_meta m = norm_meta(mx, have_sync, no_scratch);
+    if (!(mx <= 3.40282347e38f)) m.status = kStatusFixup;
     return m;
 }
 
@@ -147,8 +160,10 @@ __global__ __launch_bounds__(kTile) void k_maxabs(DemodArgs A) {
     const unsigned long long dech_end = A.total_syms * N;  // whole symbols
     const bool dech = A.mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     float mx = 0.0f;
+    bool bad = false;  // a non-finite [dechirped] sample: exact re-run (k_post)
     auto acc = [&](cf32 x, unsigned long long i) {
         if (dech) x = i < dech_end ? cmul(x, A.down[i & (N - 1)]) : czero();
+        bad |= !(__builtin_isfinite(x.x) && __builtin_isfinite(x.y));
         maxabs_acc(mx, x);
     };
     if ((reinterpret_cast<uintptr_t>(fr) & 15) == 0) {
@@ -181,13 +196,18 @@ __global__ __launch_bounds__(kTile) void k_maxabs(DemodArgs A) {
         const float o = __shfl_xor(mx, off, 64);
         mx = o > mx ? o : mx;
     }
+    if (__ballot(bad)) mx = __builtin_nanf("");
     if ((tid & 63) == 0) wmax[tid >> 6] = mx;
     __syncthreads();
     if (tid == 0) {
         mx = wmax[0];
+        bool nf = !(mx == mx);
 #pragma unroll
-        for (int w = 1; w < kTile / 64; ++w) mx = wmax[w] > mx ? wmax[w] : mx;
-        A.meta[f] = norm_meta(mx, A.total_syms >= 2, A.no_scratch);
+        for (int w = 1; w < kTile / 64; ++w) {
+            nf |= !(wmax[w] == wmax[w]);
+            mx = wmax[w] > mx ? wmax[w] : mx;
+        }
+        A.meta[f] = norm_meta_hot(nf ? __builtin_nanf("") : mx, A.total_syms >= 2, A.no_scratch);
     }
 }
 
@@ -203,6 +223,7 @@ struct UnitResult {
     int valid;   // p > best_p reachable (maxValue > 0)
     float findex;
     float phase;
+    int nan;     // a NaN bin (k_frames: the frame goes to the exact re-run)
 };
 
 // Detector outputs of one estimate unit from its FFT bins, which the team
@@ -226,6 +247,7 @@ __device__ __forceinline__ UnitResult unit_result(const cf32* lds, int slot, Arg
     r.valid = mv > 0.0f;  // osr == 1: p > -1e30 <=> maxValue > 0
     r.findex = fi;
     r.phase = lphy_libm::atan2f_exact(bin.y, bin.x);
+    r.nan = 0;
     return r;
 }
 
@@ -346,7 +368,7 @@ __global__ __launch_bounds__(kTile) void k_estimate(DemodArgs A) {
         }
         __syncthreads();
         cf32 v[16];
-        fft_tile<SF>(v, lds, slot, lam, twl);
+        fft_tile<SF, false, true>(v, lds, slot, lam, twl);
         // keep the bins for the interpolation and the phase
 #pragma unroll
         for (int e = 0; e < G::E; ++e) lds[G::addr(slot, bin_of<SF>(e, lam))] = v[e];
@@ -424,18 +446,18 @@ __device__ __forceinline__ SymCtx sym_ctx(const DemodArgs& A, unsigned f, unsign
 }
 
 // One rotated input sample (LoRaDemod.cpp:152-163, phy.cpp:217-229).
-template <int SF, int MODE>
+template <int SF, int MODE, bool AG = false>
 __device__ __forceinline__ cf32 rotate_sample(cf32 x, int i, const SymCtx& c,
                                               const cf32* down, const float* win, bool large) {
     constexpr int N = 1 << SF;
     if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) {
-        x = cmul(x, down[i]);  // phy.cpp:219-220: down-chirp of the window
+        x = cmul_t<AG>(x, down[i]);  // phy.cpp:219-220: down-chirp of the window
     } else {
         if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) {
             // the external dechirp ran on the unshifted buffer
             // (e2e_chain_test.cpp:88-93): chirp index of the absolute sample
             // (frames hold whole symbols in this mode)
-            x = cmul(x, down[((unsigned)c.base + (unsigned)i) & (N - 1)]);
+            x = cmul_t<AG>(x, down[((unsigned)c.base + (unsigned)i) & (N - 1)]);
         }
         // LoRaDemod.cpp:74-76; scale == 1.0f exactly when no rescale was
         // needed and x * 1.0f == x, so the multiply is unconditional
@@ -450,9 +472,26 @@ __device__ __forceinline__ cf32 rotate_sample(cf32 x, int i, const SymCtx& c,
     if (large) lphy_libm::sincosf_large(ph, &sn, &cs);
     else lphy_libm::sincosf_fast(ph, &sn, &cs);
 #endif
-    x = cmul(x, cf32{cs, sn});
+    x = cmul_t<AG>(x, cf32{cs, sn});
     if constexpr ((MODE & kWinBit) != 0) x = cscale(x, win[i]);
     return x;
+}
+
+// Exact restaging of the team's symbol from its IQ in memory, one sample at
+// a time (rare paths: the certificate's re-check, and the Annex G re-run of
+// a transform that produced a NaN bin).
+template <int SF, int MODE, bool AG>
+__device__ __forceinline__ void restage_symbol(cf32* lds, const Stage<SF>& stg, const cf32* src,
+                                               const SymCtx& c, int lam, const cf32* down,
+                                               const float* win, unsigned osr = 1) {
+    using G = Geo<SF>;
+#pragma unroll 1
+    for (int e = 0; e < G::E; ++e) {
+        const int i = lam + e * G::LPS;
+        const float ph = c.start + c.rate * (float)i;
+        stg.put(lds, e, rotate_sample<SF, MODE, AG>(src[(unsigned)i * osr], i, c, down, win,
+                                                    lphy_libm::sincosf_needs_large(ph)));
+    }
 }
 
 // Stage the team's symbol (rotated, natural order) into its LDS slot.
@@ -597,6 +636,9 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
 #else
         fft_tile<SF>(v, lds, slot, lam, twl);
 #endif
+        // a NaN bin may hide a (NaN, NaN) product, where the reference's
+        // Annex G product differs: the frame goes to the exact re-run
+        if (fft_has_nan<SF>(v) && c.ok) A.meta[c.f].status = kStatusFixup;
 #ifdef LPHY_PROFILE_PHASES
         const unsigned long long p2 = clock64();
 #endif
@@ -691,8 +733,10 @@ __device__ __forceinline__ float wave_maxabs(const DemodArgs& A, unsigned f, con
     const cf32* fr = A.iq + (unsigned long long)f * A.frame_samples;
     const unsigned count = DECH ? (unsigned)A.total_syms * N : (unsigned)A.frame_samples;
     float mx = 0.0f;
+    bool bad = false;  // non-finite [dechirped] sample
     auto acc = [&](cf32 x, unsigned i) {
         if constexpr (DECH) x = cmul(x, down[i & (N - 1)]);
+        bad |= !(__builtin_isfinite(x.x) && __builtin_isfinite(x.y));
         maxabs_acc(mx, x);
     };
     // loads in flight per lane (measured at SF7: 16, 24, 32 and 33 - two
@@ -742,14 +786,12 @@ __device__ __forceinline__ float wave_maxabs(const DemodArgs& A, unsigned f, con
             }
             round(v);
         }
-        exact = __ballot(!(sum.x == sum.x && sum.y == sum.y)) != 0;
-        if (!exact) {
-            mx = fm;
-            if ((count & 1) && lane == 0) acc(fr[count - 1], count - 1);
-        }
-    }
-    if (exact) {
-        mx = 0.0f;
+        // a NaN or inf sample (or an inf - inf) ends in the sum as NaN, or
+        // in the maximum as inf: the frame goes to the exact re-run
+        bad = !(sum.x == sum.x && sum.y == sum.y) || !(fm <= 3.40282347e38f);
+        mx = fm;
+        if ((count & 1) && lane == 0) acc(fr[count - 1], count - 1);
+    } else {
         for (unsigned i = lane; i < count; i += 64) acc(fr[i], i);
     }
 #pragma unroll
@@ -757,47 +799,8 @@ __device__ __forceinline__ float wave_maxabs(const DemodArgs& A, unsigned f, con
         const float o = __shfl_xor(mx, off, 64);
         mx = o > mx ? o : mx;
     }
-    return mx;
-}
-
-// Staging of a tile that mixes estimate units (no rotation; mode 0: raw
-// samples, modes 1/2: [dechirped,] normalised; zero when the frame is not
-// estimated) with symbol units (as stage_symbol).  est_sample() semantics.
-template <int SF, int MODE>
-__device__ __forceinline__ void stage_mixed(cf32* lds, const Stage<SF>& stg, const cf32 (&raw)[16],
-                                            const cf32* src, const SymCtx& c, int lam,
-                                            const cf32* down, const float* win, bool est) {
-    using G = Geo<SF>;
-    constexpr int N = G::N;
-#pragma unroll
-    for (int e = 0; e < G::E; ++e) {
-        const int i = lam + e * G::LPS;
-        cf32 x = raw[e];
-        cf32 pre;  // input of the rotation
-        if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) {
-            pre = cmul(x, down[i]);
-        } else {
-            if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
-                x = cmul(x, down[((unsigned)c.base + (unsigned)i) & (N - 1)]);
-            x = cscale(x, c.scale);
-            pre = x;
-        }
-        const float ph = c.start + c.rate * (float)i;
-        float sn, cs;
-        lphy_libm::sincosf_fast(ph, &sn, &cs);
-        cf32 y = cmul(pre, cf32{cs, sn});
-        y = est ? (c.ok ? x : czero()) : y;
-        if constexpr ((MODE & kWinBit) != 0) y = cscale(y, win[i]);
-        stg.put(lds, e, y);
-    }
-    if (!est && (lphy_libm::sincosf_needs_large(c.start + c.rate * (float)lam) ||
-                 lphy_libm::sincosf_needs_large(c.start + c.rate * (float)(lam + (G::E - 1) * G::LPS)))) {
-        for (int e = 0; e < G::E; ++e) {
-            const int i = lam + e * G::LPS;
-            if (lphy_libm::sincosf_needs_large(c.start + c.rate * (float)i))
-                stg.put(lds, e, rotate_sample<SF, MODE>(src[i], i, c, down, win, true));
-        }
-    }
+    // NaN: the caller's norm_meta_hot routes the frame to k_post
+    return __ballot(bad) ? __builtin_nanf("") : mx;
 }
 
 enum : int { kUnitDead = 0, kUnitEst = 1, kUnitSym = 2 };
@@ -1089,7 +1092,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             mxe = mx;  // scanned ahead (frame ke == m_seq)
             if (kind == kUnitEst) {
                 if ((MODE & 3) != LPHY_MODE_DEMODULATE) {
-                    const lphy_frame_meta nm = norm_meta(mxe, true, A.no_scratch);
+                    const lphy_frame_meta nm = norm_meta_hot(mxe, true, A.no_scratch);
                     c.scale = nm.scale;
                     c.live = nm.status == 0;
                 }
@@ -1141,8 +1144,12 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
                 for (int e = 0; e < G::E; ++e) lds[G::addr(slot, bin_of<SF>(e, lam))] = v[e];
             }
             team_sync<SF>();
-            if (kind == kUnitEst && lam == 0)
+            // a NaN bin may hide an Annex G product: exact re-run (k_post)
+            const unsigned long long nanm = __ballot(kind == kUnitEst && c.ok && fft_has_nan<SF>(v));
+            if (kind == kUnitEst && lam == 0) {
                 ures[wv][su] = c.ok ? unit_result<SF>(lds, slot, best) : UnitResult{0, 0, 0.0f, 0.0f};
+                ures[wv][su].nan = ((nanm >> (slot * G::LPS)) & ((G::LPS == 64) ? ~0ull : ((1ull << G::LPS) - 1))) != 0;
+            }
             team_sync<SF>();  // slot reads done before a re-check restages
         }
         // symbols the certificate does not cover: exact per-sample rotation
@@ -1153,17 +1160,13 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         if (rmask) {
             // one sample at a time: the re-check is rare, and a serial loop
             // keeps its sincos temporaries out of the main path's registers
-            const cf32* src = A.iq + (unsigned long long)c.f * A.frame_samples + c.base;
-#pragma unroll 1
-            for (int e = 0; e < G::E; ++e) {
-                const int i = lam + e * G::LPS;
-                const float ph = c.start + c.rate * (float)i;
-                stg.put(lds, e, rotate_sample<SF, MODE>(src[i], i, c, down, win,
-                                                        lphy_libm::sincosf_needs_large(ph)));
-            }
+            restage_symbol<SF, MODE, false>(lds, stg, A.iq + (unsigned long long)c.f * A.frame_samples + c.base,
+                                            c, lam, down, win);
             team_sync<SF>();
             cf32 vx[16];
             fft_tile<SF>(vx, lds, slot, lam, twl);
+            // NaN bins: possibly an Annex G product, exact re-run of the frame
+            if (redo && fft_has_nan<SF>(vx) && lam == 0) A.meta[c.f].status = kStatusFixup;
             const ArgMax ex = symbol_argmax<SF>(local_argmax<SF>(vx, lam), nullptr);
             if (redo) best = ex;
             rechecks += (unsigned long long)__popcll(rmask) / G::LPS;
@@ -1182,16 +1185,19 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             lphy_frame_meta m{};
             m.scale = 1.0f;
             m.have_sync = 1;
-            if ((MODE & 3) != LPHY_MODE_DEMODULATE) m = norm_meta(mxe, true, A.no_scratch);
+            if ((MODE & 3) != LPHY_MODE_DEMODULATE) m = norm_meta_hot(mxe, true, A.no_scratch);
             if (m.status == 0) {
                 EstFold fold;
+                bool nan = false;
 #pragma unroll
                 for (unsigned u = 0; u < U; ++u) {
                     const UnitResult r = ures[wv][u];
+                    nan |= r.nan != 0;
                     if (r.valid) fold.add(r.idx, r.findex, 0, r.phase);
                     else fold.add(0, 0.0f, 0, 0.0f);
                 }
                 fold.finish(m, (int)U, N, 1);
+                if (nan) m.status = kStatusFixup;
             }
             ring[wv][ke % 3] = float4{m.rate, m.scale, __int_as_float(m.t_off),
                                       __uint_as_float((m.status == 0 ? 1u : 0u) | 2u)};
@@ -1267,9 +1273,7 @@ struct FinalArgs {
     int set_sync;
 };
 
-__global__ void k_finalize(FinalArgs A) {
-    const unsigned long long f = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= A.frames) return;
+__device__ __forceinline__ void finalize_frame(const FinalArgs& A, unsigned long long f) {
     lphy_frame_meta m = A.meta[f];
     if (m.status != 0) return;
     if (A.set_sync && m.have_sync)
@@ -1295,6 +1299,162 @@ __global__ void k_finalize(FinalArgs A) {
         }
     }
     A.meta[f] = m;
+}
+
+__global__ void k_finalize(FinalArgs A) {
+    const unsigned long long f = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < A.frames) finalize_frame(A, f);
+}
+
+// ---------------------------------------------------------------------------
+// Exact re-run of one frame by a whole 256-thread workgroup (k_post): the
+// reference's arithmetic with its Annex G complex products (cmul_x)
+// everywhere - max-abs (LoRaDemod.cpp:60-78), estimate (LoRaDemod.cpp:80-140
+// / phy.cpp:81-148), every symbol (LoRaDemod.cpp:142-176 / phy.cpp:204-238).
+// Frames get here only when a hot kernel met a non-finite value (status
+// kStatusFixup), so this path favours plainness over speed.
+// ---------------------------------------------------------------------------
+template <int SF>
+struct PostShared {
+    cf32 lds[Geo<SF>::T * Geo<SF>::SSTRIDE];
+    ArgMax red[kTile / 64];
+    UnitResult units[Geo<SF>::T];
+    float upow[Geo<SF>::T];
+    float wmax[kTile / 64];
+    lphy_frame_meta m;
+    uint16_t sw[2];
+    unsigned list[kTile];
+    unsigned count;
+};
+
+template <int SF, int MODE>
+__device__ void exact_frame(const DemodArgs& A, unsigned f, PostShared<SF>& sh) {
+    using G = Geo<SF>;
+    constexpr int N = G::N, T = G::T;
+    const int tid = threadIdx.x;
+    const int slot = tid / G::LPS, lam = tid % G::LPS;
+    const cf32* fr = A.iq + (unsigned long long)f * A.frame_samples;
+    const unsigned long long step = (unsigned long long)N * A.osr;
+    const bool have_sync = A.total_syms >= 2;
+    // (1) normalisation (modes 1, 2)
+    if (MODE != LPHY_MODE_DEMODULATE) {
+        const unsigned long long count = MODE == LPHY_MODE_DECHIRP_LORA_DEMODULATE
+                                             ? A.total_syms * N : A.frame_samples;
+        float mx = 0.0f;
+        for (unsigned long long i = tid; i < count; i += kTile) {
+            cf32 x = fr[i];
+            if (MODE == LPHY_MODE_DECHIRP_LORA_DEMODULATE) x = cmul_x(x, A.down[i & (N - 1)]);
+            maxabs_acc(mx, x);
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const float o = __shfl_xor(mx, off, 64);
+            mx = o > mx ? o : mx;
+        }
+        if ((tid & 63) == 0) sh.wmax[tid >> 6] = mx;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        lphy_frame_meta m{};
+        m.scale = 1.0f;
+        m.have_sync = have_sync;
+        if (MODE != LPHY_MODE_DEMODULATE) {
+            float mx = sh.wmax[0];
+            for (int w = 1; w < kTile / 64; ++w) mx = sh.wmax[w] > mx ? sh.wmax[w] : mx;
+            m = norm_meta(mx, have_sync, A.no_scratch);
+        }
+        sh.m = m;
+        sh.sw[0] = sh.sw[1] = 0;
+    }
+    __syncthreads();
+    // (2) estimate: units (symbol, osr phase) in chunks of T, folded in
+    // order by thread 0 (the separate k_estimate's unpacked path)
+    EstFold fold;
+    const int U = A.est_units;
+    const bool tie_low = MODE != LPHY_MODE_DEMODULATE;
+    for (int c0 = 0; c0 < U && sh.m.status == 0; c0 += T) {
+        const lphy_frame_meta m = sh.m;
+        const int u = c0 + slot;
+        const bool live = u < U;
+        const int s = live ? u / A.osr : 0, t = live ? u % A.osr : 0;
+        const Stage<SF> st(slot, lam);
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) {
+            const int i = lam + e * G::LPS;
+            cf32 x = czero();
+            if (live) x = est_sample(A, fr, (unsigned long long)s * step + t + (unsigned long long)i * A.osr, i, N, m);
+            st.put(sh.lds, e, x);
+        }
+        __syncthreads();
+        cf32 v[16];
+        fft_tile<SF, false, true>(v, sh.lds, slot, lam, A.tw);
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) sh.lds[G::addr(slot, bin_of<SF>(e, lam))] = v[e];
+        const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), sh.red);
+        __syncthreads();
+        if (lam == 0) {
+            sh.units[slot] = live ? unit_result<SF>(sh.lds, slot, best) : UnitResult{0, 0, 0.0f, 0.0f, 0};
+            sh.upow[slot] = live && A.osr > 1 ? detector_power(best.v > 0.0f ? best.v : 0.0f, A.power_scale) : 0.0f;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const int nu = U - c0 < T ? U - c0 : T;
+            for (int k = 0; k < nu; ++k) fold.unit(sh.units[k], A.osr > 1 ? sh.upow[k] : 0.0f, A.osr, tie_low);
+        }
+        __syncthreads();
+    }
+    if (tid == 0 && sh.m.status == 0) fold.finish(sh.m, U / A.osr, N, A.osr);
+    __syncthreads();
+    // (3) symbols, T per tile, exact per-sample rotation
+    const lphy_frame_meta m = sh.m;
+    const unsigned S = (unsigned)A.total_syms;
+    for (unsigned s0 = 0; s0 < S; s0 += T) {
+        const unsigned s = s0 + slot;
+        const bool live = s < S;
+        const SymCtx c = sym_ctx<true>(A, f, live ? s : 0, live, N, m);
+        if (A.win)
+            restage_symbol<SF, MODE | kWinBit, true>(sh.lds, Stage<SF>(slot, lam), fr + c.base, c, lam,
+                                                     A.down, A.win, (unsigned)A.osr);
+        else
+            restage_symbol<SF, MODE, true>(sh.lds, Stage<SF>(slot, lam), fr + c.base, c, lam,
+                                           A.down, nullptr, (unsigned)A.osr);
+        __syncthreads();
+        cf32 v[16];
+        fft_tile<SF, false, true>(v, sh.lds, slot, lam, A.tw);
+        const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), sh.red);
+        if (lam == 0 && live) {
+            if (c.have_sync && s < 2) sh.sw[s] = c.ok ? (uint16_t)best.i : (uint16_t)0;
+            else if (c.ok) A.syms[(unsigned long long)f * A.out_per_frame + (c.have_sync ? s - 2 : s)] = (uint16_t)best.i;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        lphy_frame_meta r = sh.m;
+        r.sw0 = sh.sw[0];
+        r.sw1 = sh.sw[1];
+        A.meta[f] = r;
+    }
+    __syncthreads();
+}
+
+// After the symbol kernels: the exact re-run of the frames they flagged,
+// then (fin) the per-frame finalisation, one thread per frame.
+template <int SF, int MODE>
+__global__ __launch_bounds__(kTile) void k_post(DemodArgs A, FinalArgs F, int fix, int fin) {
+    __shared__ PostShared<SF> sh;
+    const unsigned long long f = (unsigned long long)blockIdx.x * kTile + threadIdx.x;
+    if (fix) {
+        const bool flagged = f < A.frames && A.meta[f].status == kStatusFixup;
+        if (__syncthreads_or(flagged)) {
+            if (threadIdx.x == 0) sh.count = 0;
+            __syncthreads();
+            if (flagged) sh.list[atomicAdd(&sh.count, 1u)] = (unsigned)f;
+            __syncthreads();
+            const unsigned n = sh.count;
+            for (unsigned k = 0; k < n; ++k) exact_frame<SF, MODE>(A, sh.list[k], sh);
+        }
+    }
+    if (fin && f < A.frames) finalize_frame(F, f);
 }
 
 // ---------------------------------------------------------------------------
@@ -1380,7 +1540,7 @@ __global__ void k_comp_rotate(cf32* out, const cf32* in, unsigned long long coun
     const float ph = rate * (float)n;
     float sn, cs;
     lphy_libm::sincosf_exact(ph, &sn, &cs);
-    out[n] = cmul(in[n], cf32{cs, sn});
+    out[n] = cmul_x(in[n], cf32{cs, sn});  // samples[n] *= complex (phy.cpp:163)
 }
 
 __global__ void k_comp_shift(cf32* out, const cf32* in, unsigned long long count,
@@ -1408,10 +1568,9 @@ struct lphy_hip_ctx {
     std::mutex mu;
     void* d_stage = nullptr;
     size_t stage_bytes = 0;
-    // device scratch of the producer / compensation kernels (grown on demand
-    // with a synchronous hipMalloc; never on the demodulation path)
-    void* d_scratch = nullptr;
-    size_t scratch_bytes = 0;
+    // (the producer / compensation kernels take their scratch per call from
+    // the stream-ordered allocator, so concurrent calls on different streams
+    // or threads never share it)
 };
 
 namespace {
@@ -1723,6 +1882,36 @@ int launch_frames(unsigned sf, const DemodArgs& A, hipStream_t st) {
     }
 }
 
+template <int SF>
+int launch_post_sf(int mode, const DemodArgs& A, const FinalArgs& F, bool fix, bool fin, hipStream_t st) {
+    const dim3 grid((unsigned)((A.frames + kTile - 1) / kTile));
+    switch (mode) {
+        case LPHY_MODE_DEMODULATE:
+            hipLaunchKernelGGL((k_post<SF, LPHY_MODE_DEMODULATE>), grid, dim3(kTile), 0, st, A, F, (int)fix, (int)fin);
+            break;
+        case LPHY_MODE_LORA_DEMODULATE:
+            hipLaunchKernelGGL((k_post<SF, LPHY_MODE_LORA_DEMODULATE>), grid, dim3(kTile), 0, st, A, F, (int)fix, (int)fin);
+            break;
+        default:
+            hipLaunchKernelGGL((k_post<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>), grid, dim3(kTile), 0, st, A, F, (int)fix,
+                               (int)fin);
+            break;
+    }
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int launch_post(unsigned sf, int mode, const DemodArgs& A, const FinalArgs& F, bool fix, bool fin,
+                hipStream_t st) {
+    switch (sf) {
+#define CASE(S) case S: return launch_post_sf<S>(mode, A, F, fix, fin, st);
+        CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6)
+        CASE(7) CASE(8) CASE(9) CASE(10) CASE(11) CASE(12)
+#undef CASE
+        default: return -EINVAL;
+    }
+}
+
 bool fused_enabled() {
     static int env = -1;
     if (env < 0) {
@@ -1744,16 +1933,24 @@ int ensure_stage(lphy_hip_ctx* c, size_t bytes) {
 
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
-int ensure_scratch(lphy_hip_ctx* c, size_t bytes, hipStream_t st) {
-    if (c->scratch_bytes >= bytes) return 0;
-    HIP_OK(hipStreamSynchronize(st));  // previous users of the old buffer
-    if (c->d_scratch) (void)hipFree(c->d_scratch);
-    c->d_scratch = nullptr;
-    c->scratch_bytes = 0;
-    HIP_OK(hipMalloc(&c->d_scratch, bytes));
-    c->scratch_bytes = bytes;
-    return 0;
-}
+// Per-call device scratch, allocated and released in the order of `st`
+// (hipMallocAsync / hipFreeAsync): its lifetime is exactly the call's
+// kernels on that stream.
+struct StreamScratch {
+    void* p = nullptr;
+    hipStream_t st;
+    explicit StreamScratch(hipStream_t s) : st(s) {}
+    int get(size_t bytes) {
+        if (hipMallocAsync(&p, bytes, st) != hipSuccess) {
+            p = nullptr;
+            return -ENOMEM;
+        }
+        return 0;
+    }
+    ~StreamScratch() {
+        if (p) (void)hipFreeAsync(p, st);
+    }
+};
 
 }  // namespace
 
@@ -1815,7 +2012,6 @@ void lphy_hip_ctx_destroy(lphy_hip_ctx* c) {
     if (c->d_down) (void)hipFree(c->d_down);
     if (c->d_win) (void)hipFree(c->d_win);
     if (c->d_stage) (void)hipFree(c->d_stage);
-    if (c->d_scratch) (void)hipFree(c->d_scratch);
     delete c;
 }
 
@@ -1879,7 +2075,11 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
                    : launch_demod(c->sf, A, st, all || (stages & LPHY_F_STAGE_PROLOGUE),
                                   all || (stages & LPHY_F_STAGE_SYMBOLS));
     if (rc) return rc;
-    if (!all && !(stages & LPHY_F_STAGE_FINAL)) return 0;
+    // exact re-run of flagged frames (part of the symbols stage) and the
+    // per-frame finalisation, in one launch
+    const bool fix = all || (stages & LPHY_F_STAGE_SYMBOLS);
+    const bool fin = all || (stages & LPHY_F_STAGE_FINAL);
+    if (!fix && !fin) return 0;
     FinalArgs F{};
     F.syms = d_syms;
     F.bytes = d_bytes;
@@ -1890,9 +2090,7 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     F.shift = c->sf > 4 ? (int)c->sf - 4 : 0;
     F.decode = (flags & LPHY_F_DECODE) ? 1 : 0;
     F.set_sync = 1;
-    hipLaunchKernelGGL(k_finalize, dim3((unsigned)((frames + 255) / 256)), dim3(256), 0, st, F);
-    HIP_OK(hipGetLastError());
-    return 0;
+    return launch_post(c->sf, mode, A, F, fix, fin, st);
 }
 
 #ifdef LPHY_PROFILE_PHASES
@@ -1974,9 +2172,9 @@ int lphy_hip_compensate(lphy_hip_ctx* c, float* d_iq, size_t count, float cfo,
     hipStream_t st = (hipStream_t)stream;
     // phy.cpp:159-160
     const float rate = -2.0f * kPi * cfo / (static_cast<float>(c->N) * static_cast<float>(c->osr));
-    int rc = ensure_scratch(c, count * sizeof(cf32), st);
-    if (rc) return rc;
-    cf32* tmp = static_cast<cf32*>(c->d_scratch);
+    StreamScratch scratch(st);
+    if (int rc = scratch.get(count * sizeof(cf32))) return rc;
+    cf32* tmp = static_cast<cf32*>(scratch.p);
     const unsigned blocks = (unsigned)((count + 255) / 256);
     cf32* x = reinterpret_cast<cf32*>(d_iq);
     hipLaunchKernelGGL(k_comp_rotate, dim3(blocks), dim3(256), 0, st, tmp, x, (unsigned long long)count, rate);
@@ -2009,9 +2207,9 @@ int lphy_hip_modulate_batch(lphy_hip_ctx* c, const uint16_t* d_syms, size_t fram
     A.ampl = std::max(-1.0f, std::min(1.0f, amplitude));  // LoRaMod.cpp:18
     A.sync = sync;
     const size_t nph = frames * (nsyms + 2);
-    int rc = ensure_scratch(c, nph * sizeof(float), st);
-    if (rc) return rc;
-    A.phase0 = static_cast<float*>(c->d_scratch);
+    StreamScratch scratch(st);
+    if (int rc = scratch.get(nph * sizeof(float))) return rc;
+    A.phase0 = static_cast<float*>(scratch.p);
     hipLaunchKernelGGL(k_mod_phase, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, A);
     hipLaunchKernelGGL(k_mod_samples, dim3((unsigned)((nph + 63) / 64)), dim3(64), 0, st, A);
     HIP_OK(hipGetLastError());

@@ -77,7 +77,10 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
                                      size_t max_frames, uint16_t* h_syms, uint8_t* h_bytes,
                                      lphy_frame_meta* h_meta, size_t* frames_out,
                                      size_t* tail_bytes) {
-    if (!ctx || fd < 0 || frame_samples == 0 || chunk_frames == 0 || !h_meta || !frames_out)
+    // max_frames is the capacity of h_syms / h_bytes / h_meta in frames: the
+    // C ABI takes no other size, so an unbounded read could overrun them
+    if (!ctx || fd < 0 || frame_samples == 0 || chunk_frames == 0 || max_frames == 0 || !h_meta ||
+        !frames_out)
         return -EINVAL;
     if (mode < 0 || mode > 2) return -EINVAL;
     if ((flags & LPHY_F_DECODE) && !h_bytes) return -EINVAL;
@@ -131,7 +134,7 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
         Slot& s = sl[chunk % NSLOT];
         if ((rc = harvest(s)) != 0) goto done;  // slot free (its H2D and demod are done)
         size_t want = chunk_bytes;
-        if (max_frames && max_frames - next < chunk_frames) want = (max_frames - next) * frame_bytes;
+        if (max_frames - next < chunk_frames) want = (max_frames - next) * frame_bytes;
         if (want == 0) break;
         const long long got = read_full(fd, s.pin_iq, want);
         if (got < 0) { rc = -EIO; goto done; }

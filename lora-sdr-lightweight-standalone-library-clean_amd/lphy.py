@@ -118,6 +118,25 @@ def _ptr(a) -> int | None:
     return a.data_ptr()  # torch tensor
 
 
+def _dev_buf(t, name: str, device: int, nbytes: int, itemsize: int | None = None) -> int:
+    """Pointer of a device tensor after checking what the C ABI cannot: it
+    lives on the context's HIP device, is contiguous, has the element size
+    the kernels write (when given) and holds at least `nbytes`.  A wrong
+    buffer would otherwise become a silent out-of-bounds device access."""
+    if t is None or isinstance(t, np.ndarray) or not hasattr(t, "data_ptr"):
+        raise ValueError(f"{name}: expected a device tensor, got {type(t).__name__}")
+    if t.device.type != "cuda" or (t.device.index or 0) != device:
+        raise ValueError(f"{name}: tensor on {t.device}, context on cuda:{device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: tensor must be contiguous")
+    if itemsize is not None and t.element_size() != itemsize:
+        raise ValueError(f"{name}: {itemsize}-byte elements expected, got {t.dtype}")
+    have = t.numel() * t.element_size()
+    if have < nbytes:
+        raise ValueError(f"{name}: {have} bytes, the call writes/reads {nbytes}")
+    return t.data_ptr()
+
+
 class Demodulator:
     """One (sf, bw, osr, window) configuration on one HIP device."""
 
@@ -125,6 +144,7 @@ class Demodulator:
                  window: int = WINDOW_NONE, device: int = 0):
         self.lib = load()
         self.sf, self.N, self.bw_hz, self.osr = sf, 1 << sf, bw_hz, osr
+        self.device = device
         h = _vp()
         _chk(self.lib.lphy_hip_ctx_create(C.byref(h), device, sf, bw_hz, osr, window),
              "lphy_hip_ctx_create")
@@ -147,33 +167,47 @@ class Demodulator:
     # --- device batch API (torch tensors) --------------------------------
     def demod_batch(self, iq, frames, frame_samples, syms, meta, mode, flags=0,
                     payload=None, stream=None):
-        _chk(self.lib.lphy_hip_demod_batch(self.ctx, _ptr(iq), frames, frame_samples,
-                                           _ptr(syms), _ptr(payload), _ptr(meta), mode,
-                                           flags, stream),
+        per = self.syms_per_frame(frame_samples, mode)
+        dv = self.device
+        p_iq = _dev_buf(iq, "iq", dv, frames * frame_samples * 8, None)
+        p_syms = _dev_buf(syms, "syms", dv, frames * per * 2, 2)
+        p_meta = _dev_buf(meta, "meta", dv, frames * 32, None)
+        p_pay = None
+        if flags & F_DECODE:
+            p_pay = _dev_buf(payload, "payload", dv, frames * (per // 2), 1)
+        _chk(self.lib.lphy_hip_demod_batch(self.ctx, p_iq, frames, frame_samples,
+                                           p_syms, p_pay, p_meta, mode, flags, stream),
              "lphy_hip_demod_batch")
 
     def modulate_batch(self, syms, frames, nsyms, iq, amplitude=1.0, sync=0x12, stream=None):
-        _chk(self.lib.lphy_hip_modulate_batch(self.ctx, _ptr(syms), frames, nsyms, _ptr(iq),
+        dv = self.device
+        p_syms = _dev_buf(syms, "syms", dv, frames * nsyms * 2, 2) if nsyms else None
+        p_iq = _dev_buf(iq, "iq", dv, frames * (nsyms + 2) * self.N * self.osr * 8, None)
+        _chk(self.lib.lphy_hip_modulate_batch(self.ctx, p_syms, frames, nsyms, p_iq,
                                               amplitude, sync, stream),
              "lphy_hip_modulate_batch")
 
     def decode_batch(self, syms, frames, syms_per_frame, payload, meta, stream=None):
-        _chk(self.lib.lphy_hip_decode_batch(self.ctx, _ptr(syms), frames, syms_per_frame,
-                                            _ptr(payload), _ptr(meta), stream),
+        dv = self.device
+        p_syms = _dev_buf(syms, "syms", dv, frames * syms_per_frame * 2, 2)
+        p_pay = _dev_buf(payload, "payload", dv, frames * (syms_per_frame // 2), 1)
+        p_meta = _dev_buf(meta, "meta", dv, frames * 32, None)
+        _chk(self.lib.lphy_hip_decode_batch(self.ctx, p_syms, frames, syms_per_frame,
+                                            p_pay, p_meta, stream),
              "lphy_hip_decode_batch")
 
     # --- streaming ingestion (lphy_hip_demod_stream) --------------------
     def demod_stream(self, fd: int, frame_samples: int, mode: int, flags: int = 0,
                      chunk_frames: int = 4096, max_frames: int = 0, capacity: int = 0):
-        """Demodulate the float32 I/Q frames read from `fd` until EOF (or
-        max_frames).  `capacity` bounds the frames the result arrays hold
-        (default: max_frames).  Returns (symbols, payload, meta, tail_bytes)
-        for the whole frames read."""
+        """Demodulate the float32 I/Q frames read from `fd` until EOF or
+        max_frames.  The result arrays hold `capacity` frames (default:
+        max_frames); at most min(max_frames, capacity) frames are read.
+        Returns (symbols, payload, meta, tail_bytes) for the whole frames
+        read."""
         cap = capacity or max_frames
         if cap <= 0:
             raise ValueError("capacity or max_frames required")
-        if not max_frames:
-            max_frames = cap
+        max_frames = min(max_frames, cap) if max_frames else cap
         per = self.syms_per_frame(frame_samples, mode)
         syms = np.zeros(max(cap * per, 1), np.uint16)
         payload = np.zeros(max(cap * (per // 2), 1), np.uint8)

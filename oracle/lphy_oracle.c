@@ -26,11 +26,52 @@
 
 typedef struct { float re, im; } cpx;
 
+/* C99 Annex G recovery of a product whose two parts both came out NaN:
+ * what GCC's out-of-line __mulsc3 does (libgcc2.c, the published Annex G.5.1
+ * algorithm).  The reference is built with -O2 and no -fcx-limited-range, so
+ * every std::complex<float> product (operator*, operator*=) calls it in that
+ * case: inf components are "boxed" to +-1 and NaNs in the other factor set
+ * to +-0, then the product is recomputed and scaled by infinity. */
+static cpx cmul_recover(float a, float b, float c, float d) {
+    const float ac = a * c, bd = b * d, ad = a * d, bc = b * c;
+    cpx r = {ac - bd, ad + bc};
+    int recalc = 0;
+    if (isinf(a) || isinf(b)) {
+        a = copysignf(isinf(a) ? 1.0f : 0.0f, a);
+        b = copysignf(isinf(b) ? 1.0f : 0.0f, b);
+        if (isnan(c)) c = copysignf(0.0f, c);
+        if (isnan(d)) d = copysignf(0.0f, d);
+        recalc = 1;
+    }
+    if (isinf(c) || isinf(d)) {
+        c = copysignf(isinf(c) ? 1.0f : 0.0f, c);
+        d = copysignf(isinf(d) ? 1.0f : 0.0f, d);
+        if (isnan(a)) a = copysignf(0.0f, a);
+        if (isnan(b)) b = copysignf(0.0f, b);
+        recalc = 1;
+    }
+    if (!recalc && (isinf(ac) || isinf(bd) || isinf(ad) || isinf(bc))) {
+        /* overflow to inf inside the product: NaN operands become 0 */
+        if (isnan(a)) a = copysignf(0.0f, a);
+        if (isnan(b)) b = copysignf(0.0f, b);
+        if (isnan(c)) c = copysignf(0.0f, c);
+        if (isnan(d)) d = copysignf(0.0f, d);
+        recalc = 1;
+    }
+    if (recalc) {
+        r.re = INFINITY * (a * c - b * d);
+        r.im = INFINITY * (a * d + b * c);
+    }
+    return r;
+}
+
 static inline cpx cmul(cpx a, cpx b) {
-    /* GCC's inline complex<float> product (finite operands) */
+    /* GCC's inline complex<float> product, then the __mulsc3 call when both
+     * parts are NaN (see cmul_recover) */
     cpx r;
     r.re = a.re * b.re - a.im * b.im;
     r.im = a.re * b.im + a.im * b.re;
+    if (isnan(r.re) && isnan(r.im)) r = cmul_recover(a.re, a.im, b.re, b.im);
     return r;
 }
 static inline cpx cadd(cpx a, cpx b) { cpx r = {a.re + b.re, a.im + b.im}; return r; }

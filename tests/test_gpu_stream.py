@@ -110,6 +110,9 @@ def test_stream_argument_errors(lphy):
                                      meta.ctypes.data, C.byref(n), C.byref(t)) == -22
     assert lib.lphy_hip_demod_stream(d.ctx, 0, 66 * 128, 0, 0, 0, 4, syms.ctypes.data, None,
                                      meta.ctypes.data, C.byref(n), C.byref(t)) == -22
+    # no capacity: the C ABI cannot bound the writes into the caller's arrays
+    assert lib.lphy_hip_demod_stream(d.ctx, 0, 66 * 128, 4, 0, 0, 0, syms.ctypes.data, None,
+                                     meta.ctypes.data, C.byref(n), C.byref(t)) == -22
     # LPHY_F_DECODE without a payload array
     assert lib.lphy_hip_demod_stream(d.ctx, 0, 66 * 128, 4, 0, lphy.F_DECODE, 4, syms.ctypes.data,
                                      None, meta.ctypes.data, C.byref(n), C.byref(t)) == -22

@@ -177,3 +177,54 @@ def test_oversampled_power_tie(oracle, reference, sf, osr, amp):
     np.testing.assert_array_equal(_bits(a1[3][:2]), _bits(b1[3][:2]))
     # the two tie rules pick different phases here
     assert _bits(a[3][1]) != _bits(a1[3][1])
+
+
+# Non-finite samples: GCC's std::complex<float> product calls __mulsc3 when
+# both result parts are NaN (C99 Annex G recovery of infinities), in the
+# dechirp, the rotation and every KISS butterfly.  The oracle restates it.
+NONFINITE = [(complex(-np.inf, np.nan)), complex(np.inf, 0.25), complex(np.inf, np.inf),
+             complex(np.nan, 3.0), complex(0.5, np.nan), complex(-np.inf, -np.inf),
+             complex(3e38, 3e38), complex(np.nan, np.inf)]
+
+
+def _nan_bits_equal(a, b):
+    a = np.asarray(a, np.float32).reshape(-1)
+    b = np.asarray(b, np.float32).reshape(-1)
+    na, nb = np.isnan(a), np.isnan(b)
+    np.testing.assert_array_equal(na, nb)
+    np.testing.assert_array_equal(a[~na].view(np.uint32), b[~nb].view(np.uint32))
+
+
+def _nonfinite_frames(oracle, sf, rng):
+    base = _frame(oracle, rng, sf, 125000, 8)
+    out = []
+    for v in NONFINITE:
+        for pos in (3, (1 << sf) + 5, base.size - 7):
+            x = base.copy()
+            x[pos] = v
+            out.append(x)
+    return out
+
+
+@pytest.mark.parametrize("sf", [2, 7, 8])
+def test_nonfinite_samples_bit_exact(oracle, reference, sf):
+    rng = np.random.default_rng(900 + sf)
+    for iq in _nonfinite_frames(oracle, sf, rng):
+        a = oracle.demodulate(iq, sf)
+        b = reference.demodulate(iq, sf)
+        assert a[0] == b[0] and a[2] == b[2]
+        np.testing.assert_array_equal(a[1], b[1])
+        _nan_bits_equal(a[3][:2], b[3][:2])
+        x = oracle.dechirp(iq, sf, 125000)
+        _nan_bits_equal(x.view(np.float32), reference.dechirp(iq, sf, 125000).view(np.float32))
+        for inp in (x, iq):
+            a = oracle.lora_demodulate(inp, sf)
+            b = reference.lora_demodulate(inp, sf)
+            assert a[0] == b[0] and a[2] == b[2]
+            np.testing.assert_array_equal(a[1], b[1])
+            _nan_bits_equal(a[3][:2], b[3][:2])
+        # FFT bins bit for bit, except that a NaN's sign/payload follows the
+        # host's operand order (x86 keeps the first NaN operand); NaN
+        # positions must agree
+        fa, fb = oracle.fft(iq[: 1 << sf]), reference.fft(iq[: 1 << sf])
+        _nan_bits_equal(fa.view(np.float32), fb.view(np.float32))
