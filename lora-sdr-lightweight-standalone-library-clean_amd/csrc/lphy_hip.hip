@@ -1933,22 +1933,37 @@ int ensure_stage(lphy_hip_ctx* c, size_t bytes) {
 
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
-// Per-call device scratch, allocated and released in the order of `st`
-// (hipMallocAsync / hipFreeAsync): its lifetime is exactly the call's
-// kernels on that stream.
+// Per-call device scratch.  On a caller's stream it is allocated and
+// released in that stream's order (hipMallocAsync / hipFreeAsync), so its
+// lifetime is exactly the call's kernels.  On the null stream the stream-
+// ordered pool is not used (a transcript run once read a recycled block
+// there): a plain hipMalloc, and the release waits for the stream.  The
+// *_host entry points lend a slice of their staging buffer instead (they
+// hold c->mu and synchronise before returning).
 struct StreamScratch {
     void* p = nullptr;
     hipStream_t st;
-    explicit StreamScratch(hipStream_t s) : st(s) {}
+    bool owned = false, pooled = false;
+    explicit StreamScratch(hipStream_t s, void* lent = nullptr) : p(lent), st(s) {}
     int get(size_t bytes) {
-        if (hipMallocAsync(&p, bytes, st) != hipSuccess) {
+        if (p) return 0;  // lent by the caller
+        pooled = st != nullptr;
+        const hipError_t e = pooled ? hipMallocAsync(&p, bytes, st) : hipMalloc(&p, bytes);
+        if (e != hipSuccess) {
             p = nullptr;
             return -ENOMEM;
         }
+        owned = true;
         return 0;
     }
     ~StreamScratch() {
-        if (p) (void)hipFreeAsync(p, st);
+        if (!owned) return;
+        if (pooled) {
+            (void)hipFreeAsync(p, st);
+        } else {
+            (void)hipStreamSynchronize(st);
+            (void)hipFree(p);
+        }
     }
 };
 
@@ -2164,38 +2179,38 @@ int lphy_hip_estimate_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     return 0;
 }
 
-int lphy_hip_compensate(lphy_hip_ctx* c, float* d_iq, size_t count, float cfo,
-                        float time_offset, void* stream) {
-    if (!c || !d_iq) return -EINVAL;
-    if (count == 0) return 0;
-    HIP_OK(hipSetDevice(c->device));
-    hipStream_t st = (hipStream_t)stream;
+namespace {
+// compensate_offsets (phy.cpp:150-180) on device samples.  The rotation is
+// elementwise and runs in place; only a time shift needs scratch (`lent`,
+// when given, is count complex values the caller owns).
+int compensate_impl(lphy_hip_ctx* c, float* d_iq, size_t count, float cfo, float time_offset,
+                    hipStream_t st, void* lent) {
     // phy.cpp:159-160
     const float rate = -2.0f * kPi * cfo / (static_cast<float>(c->N) * static_cast<float>(c->osr));
-    StreamScratch scratch(st);
-    if (int rc = scratch.get(count * sizeof(cf32))) return rc;
-    cf32* tmp = static_cast<cf32*>(scratch.p);
     const unsigned blocks = (unsigned)((count + 255) / 256);
     cf32* x = reinterpret_cast<cf32*>(d_iq);
-    hipLaunchKernelGGL(k_comp_rotate, dim3(blocks), dim3(256), 0, st, tmp, x, (unsigned long long)count, rate);
-    const float r = std::round(time_offset);
-    long long off = (r >= -2147483648.0f && r < 2147483648.0f) ? (long long)(int)r : (long long)(int)0x80000000u;
-    if (off != 0 && (unsigned long long)(off > 0 ? off : -off) < count) {
-        hipLaunchKernelGGL(k_comp_shift, dim3(blocks), dim3(256), 0, st, x, tmp, (unsigned long long)count, off);
-    } else {
-        HIP_OK(hipMemcpyAsync(x, tmp, count * sizeof(cf32), hipMemcpyDeviceToDevice, st));
+    const float r = std::round(time_offset);  // phy.cpp:167, x86 cvttss2si
+    const long long off = (r >= -2147483648.0f && r < 2147483648.0f) ? (long long)(int)r
+                                                                     : (long long)(int)0x80000000u;
+    if (off == 0 || (unsigned long long)(off > 0 ? off : -off) >= count) {
+        hipLaunchKernelGGL(k_comp_rotate, dim3(blocks), dim3(256), 0, st, x, x,
+                           (unsigned long long)count, rate);
+        HIP_OK(hipGetLastError());
+        return 0;
     }
+    StreamScratch scratch(st, lent);
+    if (int rc = scratch.get(count * sizeof(cf32))) return rc;
+    cf32* tmp = static_cast<cf32*>(scratch.p);
+    hipLaunchKernelGGL(k_comp_rotate, dim3(blocks), dim3(256), 0, st, tmp, x, (unsigned long long)count, rate);
+    hipLaunchKernelGGL(k_comp_shift, dim3(blocks), dim3(256), 0, st, x, tmp, (unsigned long long)count, off);
     HIP_OK(hipGetLastError());
     return 0;
 }
 
-int lphy_hip_modulate_batch(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames,
-                            size_t nsyms, float* d_iq, float amplitude, uint8_t sync,
-                            void* stream) {
-    if (!c || !d_iq || (nsyms && !d_syms)) return -EINVAL;
-    if (frames == 0) return 0;
-    HIP_OK(hipSetDevice(c->device));
-    hipStream_t st = (hipStream_t)stream;
+// lora_modulate (LoRaMod.cpp:8-43) for `frames` frames; `lent` (optional)
+// holds frames * (nsyms + 2) floats of per-symbol start phases.
+int modulate_impl(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames, size_t nsyms,
+                  float* d_iq, float amplitude, uint8_t sync, hipStream_t st, void* lent) {
     ModArgs A{};
     A.syms = d_syms;
     A.iq = reinterpret_cast<cf32*>(d_iq);
@@ -2207,13 +2222,32 @@ int lphy_hip_modulate_batch(lphy_hip_ctx* c, const uint16_t* d_syms, size_t fram
     A.ampl = std::max(-1.0f, std::min(1.0f, amplitude));  // LoRaMod.cpp:18
     A.sync = sync;
     const size_t nph = frames * (nsyms + 2);
-    StreamScratch scratch(st);
+    StreamScratch scratch(st, lent);
     if (int rc = scratch.get(nph * sizeof(float))) return rc;
     A.phase0 = static_cast<float*>(scratch.p);
     hipLaunchKernelGGL(k_mod_phase, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, A);
     hipLaunchKernelGGL(k_mod_samples, dim3((unsigned)((nph + 63) / 64)), dim3(64), 0, st, A);
     HIP_OK(hipGetLastError());
     return 0;
+}
+}  // namespace
+
+int lphy_hip_compensate(lphy_hip_ctx* c, float* d_iq, size_t count, float cfo,
+                        float time_offset, void* stream) {
+    if (!c || !d_iq) return -EINVAL;
+    if (count == 0) return 0;
+    HIP_OK(hipSetDevice(c->device));
+    return compensate_impl(c, d_iq, count, cfo, time_offset, (hipStream_t)stream, nullptr);
+}
+
+int lphy_hip_modulate_batch(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames,
+                            size_t nsyms, float* d_iq, float amplitude, uint8_t sync,
+                            void* stream) {
+    if (!c || !d_iq || (nsyms && !d_syms)) return -EINVAL;
+    if (frames == 0) return 0;
+    HIP_OK(hipSetDevice(c->device));
+    return modulate_impl(c, d_syms, frames, nsyms, d_iq, amplitude, sync, (hipStream_t)stream,
+                         nullptr);
 }
 
 int lphy_hip_sync(void* stream) {
@@ -2319,11 +2353,12 @@ int lphy_hip_compensate_host(lphy_hip_ctx* c, float* h_iq, size_t count, float c
     if (count == 0) return 0;
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_OK(hipSetDevice(c->device));
-    int rc = ensure_stage(c, align_up(count * sizeof(cf32)));
+    const size_t iq_b = align_up(count * sizeof(cf32));
+    int rc = ensure_stage(c, 2 * iq_b);
     if (rc) return rc;
     float* d = (float*)c->d_stage;
     HIP_OK(hipMemcpy(d, h_iq, count * sizeof(cf32), hipMemcpyHostToDevice));
-    rc = lphy_hip_compensate(c, d, count, cfo, time_offset, nullptr);
+    rc = compensate_impl(c, d, count, cfo, time_offset, nullptr, (char*)c->d_stage + iq_b);
     if (rc) return rc;
     HIP_OK(hipDeviceSynchronize());
     HIP_OK(hipMemcpy(h_iq, d, count * sizeof(cf32), hipMemcpyDeviceToHost));
@@ -2337,13 +2372,14 @@ int lphy_hip_modulate_host(lphy_hip_ctx* c, const uint16_t* h_syms, size_t nsyms
     HIP_OK(hipSetDevice(c->device));
     const size_t samples = (nsyms + 2) * (size_t)c->N * c->osr;
     const size_t sym_b = align_up(std::max<size_t>(1, nsyms) * sizeof(uint16_t));
-    int rc = ensure_stage(c, sym_b + align_up(samples * sizeof(cf32)));
+    const size_t iq_b = align_up(samples * sizeof(cf32));
+    int rc = ensure_stage(c, sym_b + iq_b + align_up((nsyms + 2) * sizeof(float)));
     if (rc) return rc;
     char* base = (char*)c->d_stage;
     uint16_t* d_syms = (uint16_t*)base;
     float* d_iq = (float*)(base + sym_b);
     if (nsyms) HIP_OK(hipMemcpy(d_syms, h_syms, nsyms * sizeof(uint16_t), hipMemcpyHostToDevice));
-    rc = lphy_hip_modulate_batch(c, d_syms, 1, nsyms, d_iq, amplitude, sync, nullptr);
+    rc = modulate_impl(c, d_syms, 1, nsyms, d_iq, amplitude, sync, nullptr, base + sym_b + iq_b);
     if (rc) return rc;
     HIP_OK(hipDeviceSynchronize());
     HIP_OK(hipMemcpy(h_iq, d_iq, samples * sizeof(cf32), hipMemcpyDeviceToHost));

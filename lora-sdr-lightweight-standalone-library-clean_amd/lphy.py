@@ -80,6 +80,15 @@ def load(path: Path = HIP_SO) -> C.CDLL:
         return _LIB
     if not path.exists():
         raise FileNotFoundError(f"{path} missing: build with __graft_entry__.build()")
+    # One HIP runtime per process: torch ships its own libamdhip64 (SONAME
+    # libamdhip64.so.7) and asks for it by the unversioned name.  Loaded
+    # first, it also satisfies our NEEDED libamdhip64.so.7; loaded after
+    # /opt/rocm's copy, a second runtime instance appears and torch then
+    # sees no device.  So bring torch's in before ours when torch exists.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(str(path))
     L.lphy_hip_ctx_create.argtypes = [C.POINTER(_vp), C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_int]
     L.lphy_hip_ctx_destroy.argtypes = [_vp]

@@ -611,6 +611,34 @@ ssize_t orc_demodulate(unsigned sf, unsigned bw_hz, unsigned osr, int hann,
 }
 
 /* ---------------------------------------------------------------------- */
+/* phy.cpp:150-180: rotate by e^{j rate n}, then shift by round(time_offset) */
+/* ---------------------------------------------------------------------- */
+void orc_compensate_offsets(unsigned sf, unsigned osr, float cfo,
+                            float time_offset, float* iq_f, size_t count) {
+    if (!iq_f || count == 0) return;
+    if (!osr) osr = 1;
+    cpx* x = (cpx*)iq_f;
+    const size_t N = (size_t)1 << sf;
+    const float rate = -2.0f * ORC_PI * cfo / ((float)N * (float)osr);
+    for (size_t n = 0; n < count; ++n) {
+        const float ph = rate * (float)n;
+        float sn, cs;
+        sincosf(ph, &sn, &cs); /* std::cos / std::sin (phy.cpp:163-164) */
+        cpx rot = {cs, sn};
+        x[n] = cmul(x[n], rot);
+    }
+    const int off = round_to_int(time_offset);
+    if (off > 0 && (size_t)off < count) {
+        memmove(x + off, x, (count - (size_t)off) * sizeof(cpx));
+        memset(x, 0, (size_t)off * sizeof(cpx));
+    } else if (off < 0 && off != (int)0x80000000u && (size_t)(-off) < count) {
+        const size_t o = (size_t)(-off);
+        memmove(x, x + o, (count - o) * sizeof(cpx));
+        memset(x + count - o, 0, o * sizeof(cpx));
+    }
+}
+
+/* ---------------------------------------------------------------------- */
 /* CPU timing harness (bench.py cpu_baseline, kind "port")                  */
 /* ---------------------------------------------------------------------- */
 typedef struct {

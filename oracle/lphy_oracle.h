@@ -70,6 +70,10 @@ ssize_t orc_demodulate(unsigned sf, unsigned bw_hz, unsigned osr, int hann,
 void orc_estimate_offsets(unsigned sf, unsigned osr, int hann,
                           const float* iq, size_t count, float* metrics_out);
 
+/* phy.cpp:150-180, in place, with ws->metrics = {cfo, time_offset} */
+void orc_compensate_offsets(unsigned sf, unsigned osr, float cfo,
+                            float time_offset, float* iq, size_t count);
+
 /* phy.cpp:245-261 (crc_ok written to *crc_out when the call gets that far) */
 ssize_t orc_decode(const uint16_t* syms, size_t n, uint8_t* out, size_t cap,
                    uint8_t* crc_out);

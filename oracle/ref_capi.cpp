@@ -191,6 +191,17 @@ void ref_estimate_offsets(unsigned sf, unsigned bw_hz, unsigned osr,
     delete r;
 }
 
+// phy.cpp:150-180 with ws->metrics = {cfo, time_offset}; samples in place.
+void ref_compensate_offsets(unsigned sf, unsigned osr, float cfo,
+                            float time_offset, float* iq, size_t count) {
+    auto* r = new ref_ws;
+    ref_ws_init(*r, sf, 125000, osr, 0, 0x12);
+    r->ws.metrics.cfo = cfo;
+    r->ws.metrics.time_offset = time_offset;
+    compensate_offsets(&r->ws, reinterpret_cast<cf*>(iq), count);
+    delete r;
+}
+
 // phy.cpp:245-261.  crc_out = ws->metrics.crc_ok.
 ssize_t ref_decode(unsigned sf, const uint16_t* syms, size_t n, uint8_t* out,
                    size_t cap, uint8_t* crc_out) {

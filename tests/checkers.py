@@ -77,6 +77,8 @@ class Oracle:
                                            C.c_size_t, _f32p]
         L.orc_decode.argtypes = [_u16p, C.c_size_t, _u8p, C.c_size_t, _u8p]
         L.orc_decode.restype = C.c_ssize_t
+        L.orc_compensate_offsets.argtypes = [C.c_uint, C.c_uint, C.c_float, C.c_float,
+                                             _f32p, C.c_size_t]
         L.orc_bench.argtypes = [C.c_int, C.c_uint, C.c_uint, _f32p, C.c_size_t,
                                 C.c_size_t, _u8p, C.c_int]
         L.orc_bench.restype = C.c_double
@@ -110,6 +112,12 @@ class Oracle:
         self.lib.orc_estimate_offsets(sf, osr, int(hann), _p(x, _f32p), len(x) // 2,
                                       _p(met, _f32p))
         return met
+
+    def compensate_offsets(self, iq, sf, cfo, time_offset, osr=1):
+        """phy.cpp:150-180 on a copy -> compensated complex64 samples."""
+        x = _cf(np.array(iq, np.complex64))
+        self.lib.orc_compensate_offsets(sf, osr, cfo, time_offset, _p(x, _f32p), len(x) // 2)
+        return x.view(np.complex64)
 
     def dechirp(self, iq, sf, bw_hz=125000):
         x = _cf(np.asarray(iq, np.complex64))
@@ -214,6 +222,8 @@ class Reference:
                                            _f32p, C.c_size_t, _f32p]
         L.ref_decode.argtypes = [C.c_uint, _u16p, C.c_size_t, _u8p, C.c_size_t, _u8p]
         L.ref_decode.restype = C.c_ssize_t
+        L.ref_compensate_offsets.argtypes = [C.c_uint, C.c_uint, C.c_float, C.c_float,
+                                             _f32p, C.c_size_t]
         for n in ("ref_bench_modeA", "ref_bench_modeB"):
             getattr(L, n).argtypes = [C.c_uint, C.c_uint, _f32p, C.c_size_t,
                                       C.c_size_t, _u8p, C.c_int]
@@ -231,6 +241,11 @@ class Reference:
         self.lib.ref_estimate_offsets(sf, bw_hz, osr, int(hann), _p(x, _f32p), len(x) // 2,
                                       _p(met, _f32p))
         return met
+
+    def compensate_offsets(self, iq, sf, cfo, time_offset, osr=1):
+        x = _cf(np.array(iq, np.complex64))
+        self.lib.ref_compensate_offsets(sf, osr, cfo, time_offset, _p(x, _f32p), len(x) // 2)
+        return x.view(np.complex64)
 
     def dechirp(self, iq, sf, bw_hz=125000):
         x = _cf(np.asarray(iq, np.complex64))

@@ -228,3 +228,19 @@ def test_nonfinite_samples_bit_exact(oracle, reference, sf):
         # positions must agree
         fa, fb = oracle.fft(iq[: 1 << sf]), reference.fft(iq[: 1 << sf])
         _nan_bits_equal(fa.view(np.float32), fb.view(np.float32))
+
+
+COMP_CASES = [  # sf, osr, cfo, time_offset
+    (7, 1, 0.37, 95.54), (7, 1, -0.21, -12.4), (8, 1, 0.0, 0.0), (9, 2, 0.45, 300.2),
+    (12, 1, -0.5, 1e9), (7, 1, 3.0, -2.6e9), (5, 4, 0.1, float("nan")), (10, 1, 1e-4, 0.49)]
+
+
+@pytest.mark.parametrize("sf,osr,cfo,toff", COMP_CASES)
+def test_compensate_offsets_bit_exact(oracle, reference, sf, osr, cfo, toff):
+    """phy.cpp:150-180: rotation by -2 pi cfo n / (N osr), then the integer
+    shift by round(time_offset) (no shift when it is out of range or NaN)."""
+    rng = np.random.default_rng(sf * 13 + osr)
+    x = _iq(rng, 7 * (1 << sf) * osr, scale=2.0)
+    x[3] = complex(np.inf, 0.5)  # Annex G product inside the rotation
+    _nan_bits_equal(oracle.compensate_offsets(x, sf, cfo, toff, osr).view(np.float32),
+                    reference.compensate_offsets(x, sf, cfo, toff, osr).view(np.float32))
