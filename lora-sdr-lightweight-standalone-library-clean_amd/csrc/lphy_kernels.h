@@ -1,0 +1,1768 @@
+// lphy_kernels.h — device code of the MI355X LoRa PHY demodulator and the
+// per-SF launch templates.  Included by lphy_sf.hip, which is compiled once
+// per spreading factor (-DLPHY_SF=n) so the kernel instantiations build in
+// parallel; lphy_hip.hip (host side, C ABI) reaches them through the
+// per-SF SfOps tables declared below.
+//
+// Hot path: per frame a prologue (whole-frame max|I|,|Q| for
+// lora_demodulate's normalisation, LoRaDemod.cpp:60-78, and the two-symbol
+// CFO/timing estimate, LoRaDemod.cpp:80-136 / phy.cpp:81-148), then per
+// symbol CFO rotation -> KISS-identical FFT -> |X|^2 argmax
+// (LoRaDemod.cpp:142-176 / phy.cpp:204-238), then per frame Hamming(8,4)
+// decode + sx1272 CRC (LoRaDecoder.cpp:7-21, phy.cpp:245-261).
+//
+// Kernels:
+//   k_prologue   one 256-thread workgroup per frame: max-abs reduction,
+//                estimate FFTs (tile machinery of lphy_fft.h), offsets.
+//   k_demod<SF>  256-thread tiles of T = 256/(N/16) symbols; each symbol is
+//                staged to LDS with coalesced cf32 loads while the rotation
+//                (glibc-exact sincosf in FP64) is applied, transformed by
+//                LPS = N/16 lanes holding 16 complex each, and reduced by
+//                cross-lane argmax.  No MFMA: the path is HBM/VALU bound.
+//   k_finalize   one thread per frame: sync word, decode, CRC.
+//   k_modulate*  bit-exact lora_modulate (producer for synthetic IQ).
+//
+// All device arithmetic is built with -ffp-contract=off (see
+// __graft_entry__.build); every product/sum is evaluated in the reference's
+// operand order so that symbol indices, sync words and decoded bytes are
+// bit-identical to the reference's CPU path.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/lphy_hip.h"
+#include "libm_exact.h"
+#include "lphy_fft.h"
+
+
+using namespace lphy;
+
+namespace lphy {
+// ---------------------------------------------------------------------------
+// Per-launch parameters (shared by every translation unit)
+// ---------------------------------------------------------------------------
+struct DemodArgs {
+    const cf32* iq;        // frames * frame_samples
+    const cf32* tw;        // N twiddles (KISS, forward)
+    const cf32* down;      // N down-chirp samples (genChirp, down=true)
+    const float* win;        // N window coefficients or nullptr
+    uint16_t* syms;          // output symbols
+    lphy_frame_meta* meta;   // per-frame meta (prologue -> demod hand-off)
+    unsigned long long frames;
+    unsigned long long frame_samples;
+    unsigned long long total_syms;  // symbols per frame = frame_samples / step
+    unsigned long long out_per_frame;
+    int osr;
+    int mode;
+    int no_scratch;
+    int est_units;           // estimate units per frame (est_syms * osr)
+    int exact_rotation;      // LPHY_F_EXACT_ROTATION: no certified fast path
+    float power_scale;       // LoRaDetector.hpp:29, (float)(20*log10((double)N))
+    unsigned long long* counters;  // ctx counters: [0] rechecks, [1..4] phase clocks
+    // persistent demod workers: symbol stride per step split into whole
+    // frames + symbols (host-computed, so the kernel never divides)
+    unsigned stride_f, stride_s;
+};
+
+struct FinalArgs {
+    const uint16_t* syms;
+    uint8_t* bytes;
+    lphy_frame_meta* meta;
+    unsigned long long frames;
+    unsigned long long nsyms;     // symbols per frame to decode
+    unsigned long long sym_stride;
+    int shift;                    // sf > 4 ? sf - 4 : 0
+    int decode;
+    int set_sync;
+};
+
+// Per-SF launch entry points (one table per lphy_sf.hip instance)
+struct SfOps {
+    int (*demod)(const DemodArgs&, hipStream_t, bool prologue, bool symbols, int per_cu);
+    int (*frames)(const DemodArgs&, hipStream_t);
+    int (*post)(int mode, const DemodArgs&, const FinalArgs&, bool fix, bool fin, hipStream_t);
+    int (*estimate)(const DemodArgs&, hipStream_t);
+};
+extern const SfOps sf_ops_1, sf_ops_2, sf_ops_3, sf_ops_4, sf_ops_5, sf_ops_6,
+    sf_ops_7, sf_ops_8, sf_ops_9, sf_ops_10, sf_ops_11, sf_ops_12;
+}  // namespace lphy
+
+namespace {
+
+constexpr float kPi = 3.14159265358979323846f;  // lora_phy::PI (phy.hpp:20)
+// Kernel MODE template argument: the lphy_mode in bits 0-1, plus kWinBit when
+// a window is applied, so the per-sample window multiply is compile-time
+// (a runtime branch per sample would split the staging block and serialise
+// the 16 independent sincos chains of a lane).
+constexpr int kWinBit = 4;
+// ... and kOsrBit when osr > 1: k_demod then reads every osr-th sample
+// (LoRaDemod.cpp:155, phy.cpp:225); the osr == 1 kernels keep unit-stride
+// addressing.
+constexpr int kOsrBit = 8;
+
+#ifdef LPHY_PROFILE_PHASES
+#endif
+
+// Experiments only: -DLPHY_ONLY_SF=n instantiates the kernels of one SF
+// (the launch switches below); the default build has every SF.
+
+// ---------------------------------------------------------------------------
+// Per-launch parameters
+// ---------------------------------------------------------------------------
+
+
+// (int)std::round(x) as the x86-64 reference evaluates it: cvttss2si on the
+// rounded value, INT_MIN for NaN / out of range.
+__device__ __forceinline__ int round_to_int(float x) {
+    const float r = roundf(x);
+    if (!(r >= -2147483648.0f && r < 2147483648.0f)) return (int)0x80000000u;
+    return (int)r;
+}
+
+// Input sample for the estimate (no rotation): raw (mode 0) or
+// [dechirped,] [normalised] (modes 1, 2).  idx is the absolute sample index
+// in the frame, i the index inside the symbol (window / mode-0 chirp).
+__device__ __forceinline__ cf32 est_sample(const DemodArgs& A, const cf32* fr,
+                                             unsigned long long idx, int i, int N,
+                                             const lphy_frame_meta& m) {
+    cf32 x = fr[idx];
+    if (A.mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+        x = idx < A.total_syms * (unsigned long long)N ? cmul_x(x, A.down[idx & (N - 1)])
+                                                       : czero();
+    if (A.mode != LPHY_MODE_DEMODULATE && m.normalised) x = cscale(x, m.scale);
+    if (A.win) x = cscale(x, A.win[i]);
+    return x;
+}
+
+// max(|I|,|Q|) accumulation of LoRaDemod.cpp:62-66 for one sample:
+// std::max(r, im) keeps r when im is NaN and yields NaN (never > mx) when r
+// is NaN, so a NaN real part hides the whole sample.
+__device__ __forceinline__ void maxabs_acc(float& mx, cf32 x) {
+    const float r = fabsf(x.x), im = fabsf(x.y);
+    const float m = (r < im) ? im : r;
+    if (m > mx) mx = m;
+}
+
+// Internal frame status between the launches of one lphy_hip_demod_batch:
+// the frame holds a non-finite value where the reference's Annex G complex
+// product (cmul_x) could differ from the hot kernels' plain one, and is
+// re-run exactly by k_post.  Never left in a record after the call.
+constexpr int kStatusFixup = 0x7f5a0001;
+
+// Normalisation decision of LoRaDemod.cpp:60-78 from the frame's max-abs.
+__device__ __forceinline__ lphy_frame_meta norm_meta(float mx, bool have_sync, int no_scratch) {
+    lphy_frame_meta m{};
+    m.scale = 1.0f;
+    m.have_sync = have_sync;
+    if (mx > 1.0f) {
+        if (no_scratch) m.status = -ERANGE;  // LoRaDemod.cpp:69-71
+        m.normalised = 1;
+        m.scale = 1.0f / mx;
+    }
+    return m;
+}
+// The same in the hot kernels, whose scans return NaN for a frame with a
+// non-finite sample: that frame goes to the exact re-run.
+__device__ __forceinline__ lphy_frame_meta norm_meta_hot(float mx, bool have_sync, int no_scratch) {
+    lphy_frame_meta m = norm_meta(mx, have_sync, no_scratch);
+    if (!(mx <= 3.40282347e38f)) m.status = kStatusFixup;
+    return m;
+}
+
+// ---------------------------------------------------------------------------
+// Stage 1a (modes 1, 2): per-frame max(|I|,|Q|) of the [dechirped] frame and
+// the normalisation decision (LoRaDemod.cpp:60-78).  A pure streaming
+// reduction: one workgroup per frame, 16-byte loads, 8 in flight per lane.
+// ---------------------------------------------------------------------------
+template <int SF>
+__global__ __launch_bounds__(kTile) void k_maxabs(DemodArgs A) {
+    constexpr int N = 1 << SF;
+    __shared__ float wmax[kTile / 64];
+    const unsigned long long f = blockIdx.x;
+    const int tid = threadIdx.x;
+    const cf32* fr = A.iq + f * A.frame_samples;
+    const unsigned long long count = A.frame_samples;
+    const unsigned long long dech_end = A.total_syms * N;  // whole symbols
+    const bool dech = A.mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    float mx = 0.0f;
+    bool bad = false;  // a non-finite [dechirped] sample: exact re-run (k_post)
+    auto acc = [&](cf32 x, unsigned long long i) {
+        if (dech) x = i < dech_end ? cmul(x, A.down[i & (N - 1)]) : czero();
+        bad |= !(__builtin_isfinite(x.x) && __builtin_isfinite(x.y));
+        maxabs_acc(mx, x);
+    };
+    if ((reinterpret_cast<uintptr_t>(fr) & 15) == 0) {
+        const float4* f4 = reinterpret_cast<const float4*>(fr);
+        const unsigned long long n4 = count / 2;
+        constexpr int U = 8;
+        unsigned long long j = tid;
+        for (; j + (U - 1) * kTile < n4; j += U * kTile) {
+            float4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = f4[j + u * kTile];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const unsigned long long i = 2 * (j + u * kTile);
+                acc(cf32{v[u].x, v[u].y}, i);
+                acc(cf32{v[u].z, v[u].w}, i + 1);
+            }
+        }
+        for (; j < n4; j += kTile) {
+            const float4 v = f4[j];
+            acc(cf32{v.x, v.y}, 2 * j);
+            acc(cf32{v.z, v.w}, 2 * j + 1);
+        }
+        if ((count & 1) && tid == 0) acc(fr[count - 1], count - 1);
+    } else {
+        for (unsigned long long i = tid; i < count; i += kTile) acc(fr[i], i);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float o = __shfl_xor(mx, off, 64);
+        mx = o > mx ? o : mx;
+    }
+    if (__ballot(bad)) mx = __builtin_nanf("");
+    if ((tid & 63) == 0) wmax[tid >> 6] = mx;
+    __syncthreads();
+    if (tid == 0) {
+        mx = wmax[0];
+        bool nf = !(mx == mx);
+#pragma unroll
+        for (int w = 1; w < kTile / 64; ++w) {
+            nf |= !(wmax[w] == wmax[w]);
+            mx = wmax[w] > mx ? wmax[w] : mx;
+        }
+        A.meta[f] = norm_meta_hot(nf ? __builtin_nanf("") : mx, A.total_syms >= 2, A.no_scratch);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Stage 1b: offset estimate (LoRaDemod.cpp:80-140 / phy.cpp:81-148).
+// Units = (symbol, osr phase) FFTs; a 256-thread tile packs T units, i.e.
+// T/U whole frames when a frame has U <= T units (8 frames per workgroup at
+// SF7), otherwise loops over one frame's units.  Per frame, one thread folds
+// the unit results in symbol order exactly like the reference loop.
+// ---------------------------------------------------------------------------
+struct UnitResult {
+    int idx;
+    int valid;   // p > best_p reachable (maxValue > 0)
+    float findex;
+    float phase;
+    int nan;     // a NaN bin (k_frames: the frame goes to the exact re-run)
+};
+
+// Detector outputs of one estimate unit from its FFT bins, which the team
+// has written back to its LDS slot (LoRaDetector.hpp:60-71).
+template <int SF>
+__device__ __forceinline__ UnitResult unit_result(const cf32* lds, int slot, ArgMax best) {
+    using G = Geo<SF>;
+    constexpr int N = G::N;
+    UnitResult r;
+    const int idx = best.i;
+    const float mv = best.v > 0.0f ? best.v : 0.0f;
+    const float fund = sqrtf(mv);
+    const cf32 lb = lds[G::addr(slot, idx > 0 ? idx - 1 : N - 1)];
+    const cf32 rb = lds[G::addr(slot, idx < N - 1 ? idx + 1 : 0)];
+    const float left = lphy_libm::cabsf_exact(lb.x, lb.y);
+    const float right = lphy_libm::cabsf_exact(rb.x, rb.y);
+    const double demon = (2.0 * (double)fund) - (double)right - (double)left;
+    const float fi = demon == 0.0 ? 0.0f : (float)(0.5 * (double)(right - left) / demon);
+    const cf32 bin = lds[G::addr(slot, idx)];
+    r.idx = idx;
+    r.valid = mv > 0.0f;  // osr == 1: p > -1e30 <=> maxValue > 0
+    r.findex = fi;
+    r.phase = lphy_libm::atan2f_exact(bin.y, bin.x);
+    r.nan = 0;
+    return r;
+}
+
+// Detector power of LoRaDetector.hpp:64, 20*log10(sqrt(maxValue)) - scale in
+// single precision with glibc's log10f.  Only the osr > 1 estimate compares
+// powers (with one phase, p > -1e30 <=> maxValue > 0).
+__device__ __forceinline__ float detector_power(float max_value, float power_scale) {
+    const float fund = sqrtf(max_value);
+    const float db = 20.0f * lphy_libm::log10f_exact(fund);
+    return db - power_scale;
+}
+
+// Running fold of the per-symbol estimates in symbol order
+// (LoRaDemod.cpp:95-128 / phy.cpp:95-135).
+struct EstFold {
+    float sum_index = 0.0f, phase_diff = 0.0f, prev_phase = 0.0f;
+    bool have_prev = false;
+    unsigned sum_t = 0;
+    __device__ __forceinline__ void add(int best_idx, float best_f, int best_t, float best_phase) {
+        sum_t += (unsigned)best_t;
+        sum_index += (float)best_idx + best_f;
+        if (have_prev) {
+            float d = best_phase - prev_phase;
+            while (d > kPi) d -= 2.0f * kPi;
+            while (d < -kPi) d += 2.0f * kPi;
+            phase_diff += d;
+        }
+        prev_phase = best_phase;
+        have_prev = true;
+    }
+    // per-phase selection over the osr phases of one symbol
+    // (LoRaDemod.cpp:93-113 with the lowest-index tie-break, phy.cpp:106-121
+    // without it); units arrive in (symbol, phase) order
+    float best_p = -1e30f, best_f = 0.0f, best_phase = 0.0f;
+    int best_idx = 0, best_t = 0, t = 0;
+    __device__ __forceinline__ void unit(const UnitResult& r, float p, int osr, bool tie_low) {
+        if (r.valid && (p > best_p || (tie_low && p == best_p && r.idx < best_idx))) {
+            best_p = p; best_idx = r.idx; best_f = r.findex; best_t = t; best_phase = r.phase;
+        }
+        if (++t == osr) {
+            add(best_idx, best_f, best_t, best_phase);
+            best_p = -1e30f; best_f = 0.0f; best_phase = 0.0f;
+            best_idx = 0; best_t = 0; t = 0;
+        }
+    }
+    // offsets of LoRaDemod.cpp:130-140 / phy.cpp:137-147 into m
+    __device__ __forceinline__ void finish(lphy_frame_meta& m, int est_syms, int N, int osr) const {
+        const float avg_index = sum_index / (float)est_syms;
+        const float cfo_coarse = avg_index / (float)N;
+        float cfo_fine = 0.0f;
+        if (est_syms > 1)
+            cfo_fine = (phase_diff / (float)(est_syms - 1)) / (2.0f * kPi * (float)N);
+        m.cfo = cfo_coarse + cfo_fine;
+        const float frac = avg_index - floorf(avg_index + 0.5f);
+        const float avg_t = (float)sum_t / (float)est_syms;
+        m.time_offset = avg_t - frac * (float)N * (float)osr;
+        m.t_off = round_to_int(m.time_offset);
+        m.rate = -2.0f * kPi * m.cfo / (float)N;
+    }
+};
+
+template <int SF>
+__global__ __launch_bounds__(kTile) void k_estimate(DemodArgs A) {
+    using G = Geo<SF>;
+    constexpr int N = G::N, T = G::T;
+    __shared__ cf32 lds[T * G::SSTRIDE];
+    __shared__ cf32 twl[N];
+    __shared__ ArgMax red[kTile / 64];
+    __shared__ UnitResult units[T];
+    __shared__ float upow[T];
+
+    const int tid = threadIdx.x;
+    const int U = A.est_units;
+    const bool packed = U <= T;
+    const int FPT = packed ? T / U : 1;
+    const unsigned long long fbase = (unsigned long long)blockIdx.x * FPT;
+    const unsigned long long step = (unsigned long long)N * A.osr;
+    for (int i = tid; i < N; i += kTile) twl[i] = A.tw[i];
+
+    // fold state of frame (fbase + tid), held by thread tid < FPT
+    EstFold fold;
+    lphy_frame_meta mine{};
+    const bool folder = tid < FPT && fbase + tid < A.frames;
+    if (folder) {
+        if (A.mode == LPHY_MODE_DEMODULATE) {
+            mine.scale = 1.0f;
+            mine.have_sync = A.total_syms >= 2;
+        } else {
+            mine = A.meta[fbase + tid];
+        }
+    }
+
+    const int slot = tid / G::LPS, lam = tid % G::LPS;
+    const int chunks = packed ? 1 : (U + T - 1) / T;
+    for (int c = 0; c < chunks; ++c) {
+        int fl, u;
+        if (packed) { fl = slot / U; u = slot % U; }
+        else        { fl = 0; u = c * T + slot; }
+        const unsigned long long f = fbase + fl;
+        bool live = (packed ? fl < FPT : u < U) && f < A.frames;
+        lphy_frame_meta m{};
+        if (live) {
+            if (A.mode == LPHY_MODE_DEMODULATE) m.scale = 1.0f;
+            else m = A.meta[f];
+            live = m.status == 0;
+        }
+        const int s = live ? u / A.osr : 0, t = live ? u % A.osr : 0;
+        const cf32* fr = A.iq + f * A.frame_samples;
+        __syncthreads();  // previous chunk's readers are done with lds / units
+        // stage natural-order samples sym[t + i*osr] (LoRaDemod.cpp:86-92)
+        const Stage<SF> st(slot, lam);
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) {
+            const int i = lam + e * G::LPS;
+            cf32 x = czero();
+            if (live) x = est_sample(A, fr, (unsigned long long)s * step + t + (unsigned long long)i * A.osr, i, N, m);
+            st.put(lds, e, x);
+        }
+        __syncthreads();
+        cf32 v[16];
+        fft_tile<SF, false, true>(v, lds, slot, lam, twl);
+        // keep the bins for the interpolation and the phase
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) lds[G::addr(slot, bin_of<SF>(e, lam))] = v[e];
+        ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), red);
+        __syncthreads();
+        if (lam == 0) {
+            units[slot] = live ? unit_result<SF>(lds, slot, best) : UnitResult{0, 0, 0.0f, 0.0f};
+            if (A.osr > 1)
+                upow[slot] = live ? detector_power(best.v > 0.0f ? best.v : 0.0f, A.power_scale) : 0.0f;
+        }
+        __syncthreads();
+        if (folder) {
+            const int first = packed ? tid * U : 0;
+            const int nu = packed ? U : ((U - c * T) < T ? (U - c * T) : T);
+            const bool tie_low = A.mode != LPHY_MODE_DEMODULATE;
+            // an unset best bin is (0, 0), whose atan2 is 0
+            for (int k = 0; k < nu; ++k)
+                fold.unit(units[first + k], A.osr > 1 ? upow[first + k] : 0.0f, A.osr, tie_low);
+        }
+    }
+
+    if (folder && mine.status == 0) {
+        lphy_frame_meta m = mine;
+        fold.finish(m, U / A.osr, N, A.osr);
+        A.meta[fbase + tid] = m;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Stage 2: per-symbol demodulation.  Persistent grid; each 256-thread
+// workgroup stages the twiddles (and, up to N = 1024, the down-chirp and the
+// window) in LDS once, then loops over tiles of T symbols.
+// ---------------------------------------------------------------------------
+// Per-tile context of the symbol a team (LPS lanes) works on.  Frame and
+// symbol indices are 32-bit (lphy_hip_demod_batch checks frames*symbols and
+// frame_samples fit) and advance incrementally: no division per tile.
+struct SymCtx {
+    unsigned f, s;            // frame, symbol within the frame
+    unsigned base;            // first sample of the (shifted) window in the frame
+    float start, rate, scale;
+    int toff;                 // the frame's t_off (fast-rotation table offset)
+    bool ok, have_sync, live;
+};
+
+template <bool OSR = false>
+__device__ __forceinline__ SymCtx sym_ctx(const DemodArgs& A, unsigned f, unsigned s, bool live,
+                                          int N, const lphy_frame_meta& m) {
+    SymCtx c;
+    c.f = f;
+    c.s = s;
+    c.ok = live && m.status == 0;
+    c.live = live;
+    c.have_sync = m.have_sync != 0;
+    // LoRaDemod.cpp:144-151 / phy.cpp:208-216, in 32 bits
+    const unsigned osr = OSR ? (unsigned)A.osr : 1u;
+    const unsigned step = (unsigned)N * osr, count = (unsigned)A.frame_samples;
+    unsigned base = s * step;
+    const int t = m.t_off;
+    if (t > 0) {
+        if ((unsigned long long)base + (unsigned)t + step <= count) base += (unsigned)t;
+    } else if (t < 0) {
+        const unsigned long long off = (t == (int)0x80000000u) ? (unsigned long long)(long long)t
+                                                               : (unsigned long long)(-(long long)t);
+        if (off <= base) base -= (unsigned)off;
+    }
+    c.base = base;
+    c.rate = m.rate;
+    c.scale = m.scale;
+    c.toff = m.t_off;
+    // LoRaDemod.cpp:152-153 / phy.cpp:217-218; (float) of the size_t product
+    // equals (float) of the same value held in 32 bits; x / 1.0f == x
+    const float toff = OSR ? (float)m.t_off / (float)osr : (float)m.t_off;
+    c.start = m.rate * ((float)(s * (unsigned)N) + toff);
+    return c;
+}
+
+// One rotated input sample (LoRaDemod.cpp:152-163, phy.cpp:217-229).
+template <int SF, int MODE, bool AG = false>
+__device__ __forceinline__ cf32 rotate_sample(cf32 x, int i, const SymCtx& c,
+                                              const cf32* down, const float* win, bool large) {
+    constexpr int N = 1 << SF;
+    if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) {
+        x = cmul_t<AG>(x, down[i]);  // phy.cpp:219-220: down-chirp of the window
+    } else {
+        if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) {
+            // the external dechirp ran on the unshifted buffer
+            // (e2e_chain_test.cpp:88-93): chirp index of the absolute sample
+            // (frames hold whole symbols in this mode)
+            x = cmul_t<AG>(x, down[((unsigned)c.base + (unsigned)i) & (N - 1)]);
+        }
+        // LoRaDemod.cpp:74-76; scale == 1.0f exactly when no rescale was
+        // needed and x * 1.0f == x, so the multiply is unconditional
+        x = cscale(x, c.scale);
+    }
+    const float ph = c.start + c.rate * (float)i;
+    float sn, cs;
+#ifdef LPHY_ABLATE_SINCOS  // timing experiments only (tools/ubench/demod_ablate)
+    sn = ph; cs = 1.0f - ph;
+    (void)large;
+#else
+    if (large) lphy_libm::sincosf_large(ph, &sn, &cs);
+    else lphy_libm::sincosf_fast(ph, &sn, &cs);
+#endif
+    x = cmul_t<AG>(x, cf32{cs, sn});
+    if constexpr ((MODE & kWinBit) != 0) x = cscale(x, win[i]);
+    return x;
+}
+
+// Exact restaging of the team's symbol from its IQ in memory, one sample at
+// a time (rare paths: the certificate's re-check, and the Annex G re-run of
+// a transform that produced a NaN bin).
+template <int SF, int MODE, bool AG>
+__device__ __forceinline__ void restage_symbol(cf32* lds, const Stage<SF>& stg, const cf32* src,
+                                               const SymCtx& c, int lam, const cf32* down,
+                                               const float* win, unsigned osr = 1) {
+    using G = Geo<SF>;
+#pragma unroll 1
+    for (int e = 0; e < G::E; ++e) {
+        const int i = lam + e * G::LPS;
+        const float ph = c.start + c.rate * (float)i;
+        stg.put(lds, e, rotate_sample<SF, MODE, AG>(src[(unsigned)i * osr], i, c, down, win,
+                                                    lphy_libm::sincosf_needs_large(ph)));
+    }
+}
+
+// Stage the team's symbol (rotated, natural order) into its LDS slot.
+template <int SF, int MODE>
+__device__ __forceinline__ void stage_symbol(cf32* lds, const Stage<SF>& stg, const cf32 (&raw)[16],
+                                             const cf32* src, const SymCtx& c, int lam,
+                                             const cf32* down, const float* win, int osr = 1) {
+    using G = Geo<SF>;
+#pragma unroll
+    for (int e = 0; e < G::E; ++e)
+        stg.put(lds, e, rotate_sample<SF, MODE>(raw[e], lam + e * G::LPS, c, down, win, false));
+    // rare: |phase| >= 120 rad (large CFO x long frame).  The angle is
+    // monotone in i, so the lane's first and last samples bound it.
+    if (lphy_libm::sincosf_needs_large(c.start + c.rate * (float)lam) ||
+        lphy_libm::sincosf_needs_large(c.start + c.rate * (float)(lam + (G::E - 1) * G::LPS))) {
+        for (int e = 0; e < G::E; ++e) {
+            const int i = lam + e * G::LPS;
+            if (lphy_libm::sincosf_needs_large(c.start + c.rate * (float)i))
+                stg.put(lds, e, rotate_sample<SF, MODE>(src[(unsigned)i * (unsigned)osr], i, c, down, win, true));
+        }
+    }
+}
+
+__device__ __forceinline__ void store_symbol(const DemodArgs& A, const SymCtx& c, uint16_t idx) {
+    if (c.have_sync && c.s < 2) {
+        if (c.s == 0) A.meta[c.f].sw0 = idx;
+        else A.meta[c.f].sw1 = idx;
+    } else {
+        const unsigned o = c.have_sync ? c.s - 2 : c.s;
+        A.syms[(unsigned long long)c.f * A.out_per_frame + o] = idx;
+    }
+}
+
+// Stage 2: per-symbol demodulation, persistent grid.  The workgroup stages
+// the twiddles (and, up to N = 1024, the down-chirp and window) in LDS once.
+//  * SF <= 10 (a symbol's LPS <= 64 lanes sit in one wavefront): every
+//    wavefront is an independent worker with its own LDS slots and no
+//    workgroup barrier in its loop; it software-pipelines the next tile's
+//    frame record (during staging) and IQ (during the FFT).
+//  * SF 11-12: workgroup tiles with barriers (a symbol spans wavefronts).
+template <int SF, int MODE, int OCC>
+__global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
+    using G = Geo<SF>;
+    constexpr int N = G::N;
+    constexpr bool TAB = N <= 1024;  // chirp + window tables in LDS
+    constexpr bool WAVE = G::LPS <= 64;
+    constexpr int WT = WAVE ? 64 / G::LPS : G::T;  // symbols per worker tile
+    __shared__ cf32 lds[G::T * G::SSTRIDE];
+    __shared__ cf32 twl[N];
+    __shared__ cf32 dnl[TAB ? N : 1];
+    __shared__ float wnl[TAB ? N : 1];
+    __shared__ ArgMax red[kTile / 64];
+
+    const int tid = threadIdx.x;
+    for (int i = tid; i < N; i += kTile) {
+        twl[i] = A.tw[i];
+        if constexpr (TAB) {
+            if ((MODE & 3) != LPHY_MODE_LORA_DEMODULATE) dnl[i] = A.down[i];
+            if (A.win) wnl[i] = A.win[i];
+        }
+    }
+    __syncthreads();
+    const cf32* down = TAB ? dnl : A.down;
+    const float* win = A.win ? (TAB ? wnl : A.win) : nullptr;
+
+    const int slot = tid / G::LPS, lam = tid % G::LPS;
+    const unsigned S = (unsigned)A.total_syms;
+    const unsigned nframes = (unsigned)A.frames;
+    const int wslot = WAVE ? slot % WT : slot;  // symbol slot inside the worker tile
+    unsigned worker;
+    if constexpr (WAVE) worker = blockIdx.x * (kTile / 64) + (tid >> 6);
+    else worker = blockIdx.x;
+    const Stage<SF> stg(slot, lam);
+
+    // this team's first symbol and its (frame, symbol) coordinates
+    const unsigned g0 = worker * WT + wslot;
+    unsigned f = g0 / S, s = g0 - f * S;
+    auto step = [&](unsigned& ff, unsigned& ss) {
+        ss += A.stride_s;
+        ff += A.stride_f;
+        if (ss >= S) { ss -= S; ++ff; }
+    };
+    // the worker's tile loop ends when its first team passes the last frame
+    const unsigned fw0 = (worker * WT) / S;
+    unsigned fw = fw0, sw = worker * WT - fw0 * S;
+
+    // prologue of the software pipeline
+    constexpr bool OSR = (MODE & kOsrBit) != 0;
+    const unsigned osr = OSR ? (unsigned)A.osr : 1u;  // sample stride of a symbol
+    lphy_frame_meta m = A.meta[f < nframes ? f : 0];
+    SymCtx c = sym_ctx<OSR>(A, f < nframes ? f : 0, f < nframes ? s : 0, f < nframes, N, m);
+    cf32 raw[16];
+    {
+        const cf32* src = A.iq + (unsigned long long)c.f * A.frame_samples + c.base;
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) raw[e] = src[(unsigned)(lam + e * G::LPS) * osr];
+    }
+
+#ifdef LPHY_PROFILE_PHASES  // timing experiments only: per-phase clock sums
+    unsigned long long ph_stage = 0, ph_fft = 0, ph_tail = 0;
+#endif
+    while (fw < nframes) {
+#ifdef LPHY_PROFILE_PHASES
+        const unsigned long long p0 = clock64();
+#endif
+        // next tile: coordinates and frame record (in flight during staging)
+        unsigned nf = f, ns = s, nfw = fw, nsw = sw;
+        step(nf, ns);
+        step(nfw, nsw);
+        const bool nlive = nf < nframes;
+        const lphy_frame_meta nm = A.meta[nlive ? nf : 0];
+
+        if constexpr (!WAVE) __syncthreads();  // previous tile's readers done
+        stage_symbol<SF, MODE>(lds, stg, raw, A.iq + (unsigned long long)c.f * A.frame_samples + c.base,
+                               c, lam, down, win, (int)osr);
+        team_sync<SF>();
+#ifdef LPHY_PROFILE_PHASES
+        const unsigned long long p1 = clock64();
+#endif
+
+        // next tile's IQ: in flight during this tile's FFT
+        const SymCtx nc = sym_ctx<OSR>(A, nlive ? nf : 0, nlive ? ns : 0, nlive, N, nm);
+        if (nfw < nframes) {
+            const cf32* nsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base;
+#ifdef LPHY_ABLATE_LOAD  // timing experiments only
+            (void)nsrc;
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) raw[e] = raw[e] * 0.999f + cf32{(float)e, (float)lam};
+#else
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) raw[e] = nsrc[(unsigned)(lam + e * G::LPS) * osr];
+#endif
+        }
+
+        cf32 v[16];
+#ifdef LPHY_ABLATE_FFT  // timing experiments only
+        {
+            const Stage<SF> st2(slot, lam);
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) v[e] = lds_ld(lds, G::at8(st2.lb8, G::cpart(e * G::LPS) << 3));
+        }
+#else
+        fft_tile<SF>(v, lds, slot, lam, twl);
+#endif
+        // a NaN bin may hide a (NaN, NaN) product, where the reference's
+        // Annex G product differs: the frame goes to the exact re-run
+        if (fft_has_nan<SF>(v) && c.ok) A.meta[c.f].status = kStatusFixup;
+#ifdef LPHY_PROFILE_PHASES
+        const unsigned long long p2 = clock64();
+#endif
+        const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), red);
+        if (c.ok && lam == 0) store_symbol(A, c, (uint16_t)best.i);
+        if constexpr (WAVE) team_sync<SF>();  // slot reads done before restaging
+        c = nc;
+        f = nf; s = ns; fw = nfw; sw = nsw;
+#ifdef LPHY_PROFILE_PHASES
+        const unsigned long long p3 = clock64();
+        ph_stage += p1 - p0; ph_fft += p2 - p1; ph_tail += p3 - p2;
+#endif
+    }
+#ifdef LPHY_PROFILE_PHASES
+    if ((tid & 63) == 0) {
+        atomicAdd(&A.counters[1], ph_stage);
+        atomicAdd(&A.counters[2], ph_fft);
+        atomicAdd(&A.counters[3], ph_tail);
+    }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// Fused single launch (LPS <= 64 i.e. SF <= 10, two estimate symbols, osr 1).
+// Every wavefront owns the frames f = w, w + W, w + 2W, ... (W waves in the
+// grid) and runs their whole chain itself, so no data crosses wavefronts:
+//   M  max(|I|,|Q|) scan of the frame (LoRaDemod.cpp:60-78), wave-wide
+//   E  the two estimate FFTs (LoRaDemod.cpp:80-140 / phy.cpp:81-148) and the
+//      fold into the frame's offsets
+//   D  the frame's symbols (rotation, FFT, argmax)
+// The wave works through a stream of "units" in tiles of WT = 64/LPS, one
+// unit per team of LPS lanes:
+//   [E(0) x2, pad, one spacer tile] then per frame k (a "slice"):
+//   [D(k) x PE, E(k+1) x2, D(k) x (S - PE)],   PE = S + 1 - 2 WT
+// so the estimate of frame k+1 shares tiles with symbols of frame k and no
+// team idles, and E(k+1) leads D(k+1) by 2 WT units (two tiles: what the
+// one-tile-ahead IQ prefetch needs).  M(k+1) runs right before the tile
+// holding E(k+1)'s first unit, one slice before D(k+1) re-reads the frame
+// (Infinity-Cache distance).  Measured alternatives, all slower at SF7 than
+// this blocking 16-deep scan (2.3 ms per 65,536 frames): M streamed in row
+// chunks held in registers across the FFT (spills, 1.35x), M streamed by
+// LDS-DMA into a per-wave ring (1.15x), scan-only workgroups beside the
+// symbol waves (1.3-5x: they need ~25 % of the slots to stay ahead).
+// Frame records pass between teams through a 3-slot ring per wave in LDS.  Compared with separate launches this
+// removes a whole-batch pass (the prologue kernels) and overlaps the
+// HBM-bound max-abs scans of some waves with the VALU-bound transforms of
+// the others.
+// ---------------------------------------------------------------------------
+struct FrameArgs {
+    DemodArgs A;
+    unsigned waves;  // wavefronts in the grid
+};
+
+// Per-frame record of the public meta array written by E: every field but
+// sw0 / sw1, which the D tasks of symbols 0 and 1 write (disjoint bytes, so
+// the two L2 write-backs cannot clobber each other).
+__device__ __forceinline__ void meta_put_est(lphy_frame_meta* dst, const lphy_frame_meta& m) {
+    float4* d16 = reinterpret_cast<float4*>(dst);
+    d16[0] = float4{m.cfo, m.time_offset, m.rate, m.scale};
+    int* d8 = reinterpret_cast<int*>(dst);
+    d8[4] = m.t_off;
+    d8[5] = m.status;
+    uint8_t* b = reinterpret_cast<uint8_t*>(dst);
+    b[28] = m.sync_word;
+    b[29] = m.crc_ok;
+    b[30] = m.normalised;
+    b[31] = m.have_sync;
+}
+
+// Max-abs of frame f by one wavefront (16-byte loads, 8 in flight per
+// lane), same arithmetic as k_maxabs; the result is in every lane.
+//
+// Fast form of the aligned bulk (one v_max3 per sample): max(mx, |re|, |im|)
+// equals the reference's fold for samples without NaN, and the frame's
+// samples are summed alongside (one packed add per sample) so that any NaN
+// - or an overflow to inf, which could make one - sends the whole frame to
+// the per-sample fold above, whose NaN rules (a NaN real part hides the
+// sample) v_max3 does not have.  In mode 2 only the whole symbols are
+// scanned: the zeros the reference's dechirp leaves past them never raise
+// the maximum.
+__device__ __forceinline__ float max3_abs(float m, float a, float b) {
+    float r;
+    asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
+
+template <int SF, int MODE>
+__device__ __forceinline__ float wave_maxabs(const DemodArgs& A, unsigned f, const cf32* down) {
+    constexpr int N = 1 << SF;
+    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    const int lane = threadIdx.x & 63;
+    const cf32* fr = A.iq + (unsigned long long)f * A.frame_samples;
+    const unsigned count = DECH ? (unsigned)A.total_syms * N : (unsigned)A.frame_samples;
+    float mx = 0.0f;
+    bool bad = false;  // non-finite [dechirped] sample
+    auto acc = [&](cf32 x, unsigned i) {
+        if constexpr (DECH) x = cmul(x, down[i & (N - 1)]);
+        bad |= !(__builtin_isfinite(x.x) && __builtin_isfinite(x.y));
+        maxabs_acc(mx, x);
+    };
+    // loads in flight per lane (measured at SF7: 16, 24, 32 and 33 - two
+    // rounds per 66-symbol frame - within 1 %; 16 spills least)
+#ifdef LPHY_MAXABS_U
+    constexpr int U = LPHY_MAXABS_U;
+#else
+    constexpr int U = 16;
+#endif
+    // chirp index of sample 2 (b + 64 u + lane) for a round base b = 64 U r:
+    // the 128 U r term vanishes mod N
+    static_assert((128 * U) % N == 0, "chirp phase of the unrolled scan");
+    bool exact = (reinterpret_cast<uintptr_t>(fr) & 15) != 0;
+    if (!exact) {
+        const float4* f4 = reinterpret_cast<const float4*>(fr);
+        const unsigned n4 = count / 2;
+        float fm = 0.0f;
+        cf32 sum = czero();
+        auto round = [&](const float4 (&v)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                cf32 a = cf32{v[u].x, v[u].y}, b = cf32{v[u].z, v[u].w};
+                if constexpr (DECH) {
+                    const unsigned ci = (2u * (unsigned)lane + 128u * (unsigned)u) & (N - 1);
+                    a = cmul(a, down[ci]);
+                    b = cmul(b, down[(ci + 1) & (N - 1)]);
+                }
+                fm = max3_abs(fm, a.x, a.y);
+                fm = max3_abs(fm, b.x, b.y);
+                sum = sum + a;
+                sum = sum + b;
+            }
+        };
+        unsigned base = 0;
+        for (; base + U * 64 <= n4; base += U * 64) {
+            float4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = f4[base + u * 64 + lane];
+            round(v);
+        }
+        if (base < n4) {  // last partial round, zero-filled (zeros never raise the max)
+            float4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const unsigned j = base + u * 64 + lane;
+                v[u] = j < n4 ? f4[j] : float4{0.0f, 0.0f, 0.0f, 0.0f};
+            }
+            round(v);
+        }
+        // a NaN or inf sample (or an inf - inf) ends in the sum as NaN, or
+        // in the maximum as inf: the frame goes to the exact re-run
+        bad = !(sum.x == sum.x && sum.y == sum.y) || !(fm <= 3.40282347e38f);
+        mx = fm;
+        if ((count & 1) && lane == 0) acc(fr[count - 1], count - 1);
+    } else {
+        for (unsigned i = lane; i < count; i += 64) acc(fr[i], i);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float o = __shfl_xor(mx, off, 64);
+        mx = o > mx ? o : mx;
+    }
+    // NaN: the caller's norm_meta_hot routes the frame to k_post
+    return __ballot(bad) ? __builtin_nanf("") : mx;
+}
+
+enum : int { kUnitDead = 0, kUnitEst = 1, kUnitSym = 2 };
+
+// ---------------------------------------------------------------------------
+// Certified fast rotation (k_frames symbol units).
+//
+// The reference rotates sample i of symbol s by the glibc sincosf of
+// ph_i = fl(start_s + fl(rate * i)), start_s = rate * (s*N + t_off)
+// (LoRaDemod.cpp:152-158, phy.cpp:217-222): one double-precision sincos per
+// sample, half of the path's arithmetic.  A symbol's output is only the
+// argmax of |FFT|^2, and |FFT(y * e^{j start})| = |FFT(y)|: the common phase
+// start_s drops out of every magnitude.  So symbols are transformed as
+//     q_i = x_i * t_i,   t_i = [down] * e^{j rate i} * [scale] * [win]
+// with t a per-FRAME table (N entries, built once per frame from exact
+// sincos of fl(rate*i)), i.e. one complex multiply per sample instead of a
+// dechirp, a rescale, a sincos and a rotation.
+//
+// Exactness is certified per symbol, not assumed.  With u = 2^-24, A an
+// upper bound of sum_i |y_i| (the symbol's L1 norm), P = |start| + |rate| N,
+// L the number of KISS stages, the reference's bins X and ours X' satisfy
+//   | |X_k| - |X'_k| | <= B = u A (24 + 12 L + 2 |rate| N + P) (1 + 1e-3):
+//   * rotation inputs: the reference's sample differs from the ideal
+//     y_i e^{j(start + rate i)} by <= u(10 + |rate| N + P)|y_i| (dechirp
+//     3u, rescale u, sincos sqrt(2)u, phase roundings u(|rate| i + |ph|),
+//     rotation 3u, window u); ours from e^{j start}-times-ideal by
+//     <= u(10 + |rate| N)|y_i|;
+//   * transform: each KISS stage adds <= 6u (sum of its butterfly's input
+//     magnitudes) to an output; an output depends on one value of every
+//     sub-transform of a level, whose inputs partition the symbol, so both
+//     FFTs are within 6 L u A of the exact map (same float twiddles), and
+//     the input difference passes with gain (1+u)^L.
+// The reference's winner is ours when |X'_best| - 2B > |X'_second| (plus
+// the 2u rounding of |X|^2 on both sides and of the check itself); any
+// symbol that fails it - ties, near-ties, NaN, overflow risk, frames whose
+// time shift is not applied to every symbol - is recomputed with the exact
+// per-sample path.  The check below uses 4B (a factor 2 of slack).
+// ---------------------------------------------------------------------------
+constexpr float kU = 5.9604645e-8f;  // 2^-24
+
+// Table of frame `rec` (rate, scale, t_off): t_i for i = lane, lane+64, ...
+template <int SF, int MODE>
+__device__ __forceinline__ void build_rtab(cf32* tab, float rate, float scale, int t_off,
+                                           const cf32* down, const float* win, int lane) {
+    constexpr int N = 1 << SF;
+    const unsigned t0 = (unsigned)t_off & (N - 1);
+    for (int i = lane; i < N; i += 64) {
+        float sn, cs;
+        lphy_libm::sincosf_exact(rate * (float)i, &sn, &cs);
+        cf32 t = cf32{cs, sn};
+        if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) t = cmul(down[i], t);
+        if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) t = cmul(down[(t0 + (unsigned)i) & (N - 1)], t);
+        if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) t = cscale(t, scale);
+        if constexpr ((MODE & kWinBit) != 0) t = cscale(t, win[i]);
+        tab[i] = t;
+    }
+}
+
+// Whether the fast path may take this symbol unit: the table's dechirp
+// offset (mode 2) must match the symbol's window start.
+template <int SF, int MODE>
+__device__ __forceinline__ bool fast_applies(const SymCtx& c, int t_off) {
+    constexpr int N = 1 << SF;
+    if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+        return (c.base & (N - 1)) == ((unsigned)t_off & (N - 1));
+    return true;
+}
+
+// The certificate of the header comment.  amax bounds max(|Re y|, |Im y|)
+// over the symbol's samples before rotation (modes 1/2: <= 1 after the
+// frame's normalisation; mode 0: measured).
+//
+// Range guards keep every rounding relative: amax >= 1e-20 (denormal
+// arithmetic stays negligible against B), b.v >= 1e-30 (a normal |X|^2), and
+// a runner-up below 1e-30 is taken as 1e-30.
+template <int SF>
+__device__ __forceinline__ bool fast_certified(const ArgMax2& b, const SymCtx& c, float amax) {
+    constexpr int N = 1 << SF, L = (SF + 1) / 2;
+    const float A = (float)N * 1.41421366f * amax * 1.0001f;
+    const float ar = fabsf(c.rate) * (float)N;
+    const float P = fabsf(c.start) + ar;
+    const float B = kU * A * ((24.0f + 12.0f * L) + 2.0f * ar + P) * 1.001f;
+    const float lhs = sqrtf(b.v) * (1.0f - 8.0f * kU) - 4.0f * B;
+    const float rhs = sqrtf(fmaxf(b.v2, 1e-30f)) * (1.0f + 8.0f * kU);
+    return lhs > rhs && A < 1e18f && amax >= 1e-20f && b.v >= 1e-30f;
+}
+
+// Fast staging of one tile: symbol units q_i = x_i * t_i from the frame's
+// rotation table (LDS ring for SF <= 8, the lane's registers above), estimate
+// units exactly as stage_mixed (no rotation).  Returns the lane's
+// max(|Re x|, |Im x|) over its symbol samples for mode 0's certificate.
+template <int SF, int MODE, bool MIXED>
+__device__ __forceinline__ float stage_fast(cf32* lds, const Stage<SF>& stg, const cf32 (&raw)[16],
+                                            const SymCtx& c, int lam, const cf32* down,
+                                            const float* win, const cf32* rt,
+                                            const cf32 (&rreg)[16], bool est) {
+    using G = Geo<SF>;
+    constexpr int N = G::N;
+    constexpr bool RLDS = SF <= 8;
+    float amax = 0.0f;
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) {
+        const int i = lam + e * G::LPS;
+        const cf32 x = raw[e];
+        cf32 y;
+        if (MIXED && est) {
+            cf32 p = x;
+            if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) {
+                if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+                    p = cmul(p, down[((unsigned)c.base + (unsigned)i) & (N - 1)]);
+                p = cscale(p, c.scale);
+            }
+            y = c.ok ? p : czero();
+            if constexpr ((MODE & kWinBit) != 0) y = cscale(y, win[i]);
+        } else {
+            y = cmul(x, RLDS ? rt[i] : rreg[e]);
+            if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE)
+                amax = fmaxf(amax, fmaxf(fabsf(x.x), fabsf(x.y)));
+        }
+        stg.put(lds, e, y);
+    }
+    return amax;
+}
+
+template <int SF, int MODE, int OCC>
+__global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
+    using G = Geo<SF>;
+    static_assert(G::LPS <= 64, "fused path needs a symbol inside one wavefront");
+    constexpr int N = G::N;
+    constexpr bool TAB = N <= 1024;
+    constexpr int WT = 64 / G::LPS;               // units per tile
+    constexpr unsigned U = 2;                      // estimate units per frame
+    // prefix tiles: E of the first frame, then one tile that keeps its
+    // symbols two tiles behind it like every later frame's
+    constexpr unsigned PT = (U + WT - 1) / WT + 1;
+    constexpr int WPB = kTile / 64;
+    // rotation tables: per-wave LDS ring of two frames up to SF 8, per-lane
+    // registers (built when a team reaches a new frame) for SF 9-10
+    constexpr bool RLDS = SF <= 8;
+    const DemodArgs& A = P.A;
+    __shared__ cf32 lds[G::T * G::SSTRIDE];
+    __shared__ cf32 twl[N];
+    __shared__ cf32 dnl[TAB ? N : 1];
+    __shared__ float wnl[TAB ? N : 1];
+    __shared__ UnitResult ures[WPB][U];
+    __shared__ float4 ring[WPB][3];  // frame records: rate, scale, t_off, flags
+    __shared__ cf32 rtab[RLDS ? WPB : 1][2][RLDS ? N : 1];
+
+    const int tid = threadIdx.x;
+    for (int i = tid; i < N; i += kTile) {
+        twl[i] = A.tw[i];
+        if constexpr (TAB) {
+            if ((MODE & 3) != LPHY_MODE_LORA_DEMODULATE) dnl[i] = A.down[i];
+            if (A.win) wnl[i] = A.win[i];
+        }
+    }
+    __syncthreads();  // the last workgroup barrier: waves are independent below
+    const cf32* down = TAB ? dnl : A.down;
+    const float* win = A.win ? (TAB ? wnl : A.win) : nullptr;
+
+    const int lane = tid & 63, wv = tid >> 6;
+    const int slot = tid / G::LPS, lam = tid % G::LPS;
+    const unsigned wslot = (unsigned)(slot % WT);
+    const Stage<SF> stg(slot, lam);
+    const unsigned nframes = (unsigned)A.frames;
+    const unsigned S = (unsigned)A.total_syms, SL = U + S;
+    // offset of E(k+1) inside slice k: as late as the two-tile lead over
+    // D(k+1) allows (frames_fit guarantees S + 1 >= 2 WT)
+    const unsigned PE = S + 1 - 2 * WT;
+    const unsigned W = P.waves;
+    const unsigned w = blockIdx.x * WPB + wv;
+    if (w >= nframes) return;
+    const unsigned nk = (nframes - 1 - w) / W + 1;  // frames of this wave
+    const unsigned long long L = (unsigned long long)PT * WT + (unsigned long long)nk * SL;
+    const unsigned ntiles = (unsigned)((L + WT - 1) / WT);
+    const bool exact_only = A.exact_rotation != 0;
+
+    // unit of this team in tile t; (k, o) = slice and offset for t >= PT
+    auto unit_of = [&](unsigned t, unsigned k, unsigned o, unsigned& kind, unsigned& fk,
+                       unsigned& s) {
+        if (t < PT) {
+            const unsigned q = t * WT + wslot;
+            kind = q < U ? kUnitEst : kUnitDead;
+            fk = 0;
+            s = q;
+        } else if (o >= PE && o < PE + U) {
+            kind = k + 1 < nk ? kUnitEst : kUnitDead;
+            fk = k + 1;
+            s = o - PE;
+        } else {
+            kind = k < nk ? kUnitSym : kUnitDead;
+            fk = k;
+            s = o < PE ? o : o - U;
+        }
+    };
+    // context of a unit; symbol units read their frame record from the ring
+    auto ctx_of = [&](unsigned kind, unsigned fk, unsigned s) -> SymCtx {
+        const unsigned f = w + fk * W;
+        if (kind == kUnitSym) {
+            const float4 r = ring[wv][fk % 3];
+            lphy_frame_meta m{};
+            m.rate = r.x;
+            m.scale = r.y;
+            m.t_off = __float_as_int(r.z);
+            const unsigned fl = __float_as_uint(r.w);
+            m.status = (fl & 1u) ? 0 : -1;
+            m.have_sync = (fl & 2u) ? 1 : 0;
+            return sym_ctx(A, f, s, true, N, m);
+        }
+        SymCtx c{};
+        c.f = kind == kUnitEst ? f : w;
+        c.s = s;
+        c.base = kind == kUnitEst ? s * N : 0;
+        c.scale = 1.0f;
+        c.live = kind == kUnitEst;
+        return c;
+    };
+
+    unsigned k = 0, o = wslot;  // position of tile t (t >= PT)
+    unsigned kind, fk, su;
+    unit_of(0, k, o, kind, fk, su);
+    SymCtx c = ctx_of(kind, fk, su);
+    // M (modes 1/2): the max-abs scan of a frame runs in the tile before the
+    // one holding its first estimate unit, between that tile's staging and
+    // its IQ prefetch, when no tile data is held in registers; tile 0 holds
+    // E(0), scanned here.  (Measured alternative, 1.4x slower at SF7: the
+    // scan streamed one chunk per tile through a per-wave LDS buffer by
+    // LDS-DMA, issued after staging and folded a tile later - never behind
+    // the estimates, yet the chunk traffic and its folds cost more than the
+    // blocking scan's exposed latency.)
+    unsigned m_seq = 0xffffffffu;  // frame whose max-abs `mx` holds
+    float mx = 0.0f;
+    float mxe = 0.0f;              // max-abs of the frame estimated in this tile
+    auto scan_ahead = [&](unsigned nkind_, unsigned nfk_) {
+        if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) {
+            const unsigned long long nem = __ballot(nkind_ == kUnitEst);
+            if (nem) {
+                const unsigned nke = (unsigned)__shfl((int)nfk_, __ffsll((long long)nem) - 1, 64);
+                if (nke != m_seq) {
+#ifdef LPHY_ABLATE_FRAME_SCAN  // timing experiments only
+                    mx = 1.0f;
+#else
+                    mx = wave_maxabs<SF, MODE>(A, w + nke * W, down);
+#endif
+                    m_seq = nke;
+                }
+            }
+        }
+    };
+    scan_ahead(kind, fk);
+    cf32 raw[16];
+    {
+        const cf32* src = A.iq + (unsigned long long)c.f * A.frame_samples + c.base;
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) raw[e] = src[lam + e * G::LPS];
+    }
+    cf32 rreg[16];                 // SF 9-10: the team's table ...
+    unsigned rreg_fk = 0xffffffffu;  // ... of this frame
+    unsigned long long rechecks = 0;
+
+    for (unsigned t = 0; t < ntiles; ++t) {
+        // SF 9-10: a team entering a new frame builds its table entries
+        if constexpr (!RLDS) {
+            if (kind == kUnitSym && fk != rreg_fk) {
+                const unsigned t0 = (unsigned)c.toff & (N - 1);
+#pragma unroll
+                for (int e = 0; e < G::E; ++e) {
+                    const int i = lam + e * G::LPS;
+                    float sn, cs;
+                    lphy_libm::sincosf_exact(c.rate * (float)i, &sn, &cs);
+                    cf32 tv = cf32{cs, sn};
+                    if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) tv = cmul(down[i], tv);
+                    if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+                        tv = cmul(down[(t0 + (unsigned)i) & (N - 1)], tv);
+                    if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) tv = cscale(tv, c.scale);
+                    if constexpr ((MODE & kWinBit) != 0) tv = cscale(tv, win[i]);
+                    rreg[e] = tv;
+                }
+                rreg_fk = fk;
+            }
+        }
+        const cf32* rt = rtab[RLDS ? wv : 0][RLDS ? (fk & 1) : 0];
+        // estimate units in this tile (all of one frame): its max-abs first
+        const unsigned long long emask = __ballot(kind == kUnitEst);
+        unsigned ke = 0;
+        float amax;
+        if (emask) {
+            ke = (unsigned)__shfl((int)fk, __ffsll((long long)emask) - 1, 64);
+            mxe = mx;  // scanned ahead (frame ke == m_seq)
+            if (kind == kUnitEst) {
+                if ((MODE & 3) != LPHY_MODE_DEMODULATE) {
+                    const lphy_frame_meta nm = norm_meta_hot(mxe, true, A.no_scratch);
+                    c.scale = nm.scale;
+                    c.live = nm.status == 0;
+                }
+                c.ok = c.live;  // estimate this unit (else stage zeros)
+            }
+            amax = stage_fast<SF, MODE, true>(lds, stg, raw, c, lam, down, win, rt, rreg, kind != kUnitSym);
+        } else {
+            amax = stage_fast<SF, MODE, false>(lds, stg, raw, c, lam, down, win, rt, rreg, false);
+        }
+        if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) {
+#pragma unroll
+            for (int off = G::LPS / 2; off >= 1; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
+        } else {
+            amax = 1.0f;  // normalised frame: max(|I|,|Q|) <= 1 (see fast_certified)
+        }
+        team_sync<SF>();
+
+        // next tile's unit, context and IQ (in flight during the FFT)
+        unsigned nkk = k, no = o;
+        if (t + 1 == PT) {
+            nkk = 0;
+            no = wslot;
+        } else if (t + 1 > PT) {
+            no += WT;
+            if (no >= SL) { no -= SL; ++nkk; }
+        }
+        unsigned nkind, nfk, nsu;
+        unit_of(t + 1, nkk, no, nkind, nfk, nsu);
+        if (t + 1 < ntiles) scan_ahead(nkind, nfk);
+        const SymCtx nc = ctx_of(nkind, nfk, nsu);
+        if (t + 1 < ntiles) {
+            const cf32* nsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base;
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) raw[e] = nsrc[lam + e * G::LPS];
+        }
+
+        cf32 v[16];
+        // tiles of symbol units only: magnitude-only transform (fft_tile TRIV)
+        // (measured alternative: a packed-key max/min tournament for the top
+        // two, 3 % slower than this ordered scan)
+        if (emask) fft_tile<SF>(v, lds, slot, lam, twl);
+        else fft_tile<SF, true>(v, lds, slot, lam, twl);
+        const ArgMax2 b2 = symbol_argmax2<SF>(local_argmax2<SF>(v, lam));
+        ArgMax best{b2.v, b2.i};
+        if (emask) {
+            // detector outputs of the estimate units (LoRaDetector.hpp:60-71)
+            if (kind == kUnitEst) {
+#pragma unroll
+                for (int e = 0; e < G::E; ++e) lds[G::addr(slot, bin_of<SF>(e, lam))] = v[e];
+            }
+            team_sync<SF>();
+            // a NaN bin may hide an Annex G product: exact re-run (k_post)
+            const unsigned long long nanm = __ballot(kind == kUnitEst && c.ok && fft_has_nan<SF>(v));
+            if (kind == kUnitEst && lam == 0) {
+                ures[wv][su] = c.ok ? unit_result<SF>(lds, slot, best) : UnitResult{0, 0, 0.0f, 0.0f};
+                ures[wv][su].nan = ((nanm >> (slot * G::LPS)) & ((G::LPS == 64) ? ~0ull : ((1ull << G::LPS) - 1))) != 0;
+            }
+            team_sync<SF>();  // slot reads done before a re-check restages
+        }
+        // symbols the certificate does not cover: exact per-sample rotation
+        const bool redo = kind == kUnitSym && c.ok &&
+                          (exact_only || !fast_applies<SF, MODE>(c, c.toff) ||
+                           !fast_certified<SF>(b2, c, amax));
+        const unsigned long long rmask = __ballot(redo);
+        if (rmask) {
+            // one sample at a time: the re-check is rare, and a serial loop
+            // keeps its sincos temporaries out of the main path's registers
+            restage_symbol<SF, MODE, false>(lds, stg, A.iq + (unsigned long long)c.f * A.frame_samples + c.base,
+                                            c, lam, down, win);
+            team_sync<SF>();
+            cf32 vx[16];
+            fft_tile<SF>(vx, lds, slot, lam, twl);
+            // NaN bins: possibly an Annex G product, exact re-run of the frame
+            if (redo && fft_has_nan<SF>(vx) && lam == 0) A.meta[c.f].status = kStatusFixup;
+            const ArgMax ex = symbol_argmax<SF>(local_argmax<SF>(vx, lam), nullptr);
+            if (redo) best = ex;
+            rechecks += (unsigned long long)__popcll(rmask) / G::LPS;
+            team_sync<SF>();
+        }
+        if (kind == kUnitSym && lam == 0) {
+            // sw0 / sw1 also for frames that are not demodulated (0, as the
+            // separate-launch path leaves them)
+            if (c.have_sync && c.s < 2) store_symbol(A, c, c.ok ? (uint16_t)best.i : (uint16_t)0);
+            else if (c.ok) store_symbol(A, c, (uint16_t)best.i);
+        }
+        team_sync<SF>();  // slot reads (and ures) done
+        // the frame whose last estimate unit was in this tile: fold
+        const bool folding = __ballot(kind == kUnitEst && su == U - 1) != 0;
+        if (folding && lane == 0) {
+            lphy_frame_meta m{};
+            m.scale = 1.0f;
+            m.have_sync = 1;
+            if ((MODE & 3) != LPHY_MODE_DEMODULATE) m = norm_meta_hot(mxe, true, A.no_scratch);
+            if (m.status == 0) {
+                EstFold fold;
+                bool nan = false;
+#pragma unroll
+                for (unsigned u = 0; u < U; ++u) {
+                    const UnitResult r = ures[wv][u];
+                    nan |= r.nan != 0;
+                    if (r.valid) fold.add(r.idx, r.findex, 0, r.phase);
+                    else fold.add(0, 0.0f, 0, 0.0f);
+                }
+                fold.finish(m, (int)U, N, 1);
+                if (nan) m.status = kStatusFixup;
+            }
+            ring[wv][ke % 3] = float4{m.rate, m.scale, __int_as_float(m.t_off),
+                                      __uint_as_float((m.status == 0 ? 1u : 0u) | 2u)};
+            meta_put_est(&A.meta[w + ke * W], m);
+        }
+        team_sync<SF>();
+        if constexpr (RLDS) {
+            // the folded frame's rotation table, first read two tiles later
+            // (its slot's previous frame, ke - 2, has no units left)
+            if (folding) {
+                const float4 r = ring[wv][ke % 3];
+                if (__float_as_uint(r.w) & 1u)
+                    build_rtab<SF, MODE>(rtab[wv][ke & 1], r.x, r.y, __float_as_int(r.z), down, win, lane);
+            }
+        }
+        k = nkk;
+        o = no;
+        kind = nkind;
+        fk = nfk;
+        su = nsu;
+        c = nc;
+    }
+    if (lane == 0 && rechecks) atomicAdd(&A.counters[0], rechecks);
+}
+
+// ---------------------------------------------------------------------------
+// Per-frame finalisation: sync word, decode, CRC
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint8_t hamming84_decode(uint8_t b) {
+    // LoRaCodes.hpp:250-281 (decodeHamming84sx)
+    const unsigned b0 = b & 1, b1 = (b >> 1) & 1, b2 = (b >> 2) & 1, b3 = (b >> 3) & 1;
+    const unsigned b4 = (b >> 4) & 1, b5 = (b >> 5) & 1, b6 = (b >> 6) & 1, b7 = (b >> 7) & 1;
+    const unsigned syn = (b0 ^ b1 ^ b2 ^ b4) | ((b1 ^ b2 ^ b3 ^ b5) << 1) |
+                         ((b0 ^ b1 ^ b3 ^ b6) << 2) | ((b0 ^ b2 ^ b3 ^ b7) << 3);
+    switch (syn) {
+        case 0xD: return (b ^ 1) & 0xf;
+        case 0x7: return (b ^ 2) & 0xf;
+        case 0xB: return (b ^ 4) & 0xf;
+        case 0xE: return (b ^ 8) & 0xf;
+        default: return b & 0xf;
+    }
+}
+
+__device__ __forceinline__ uint16_t sx1272_checksum(const uint8_t* data, int len) {
+    // LoRaCodes.hpp:69-105
+    uint16_t res = 0;
+    uint8_t v = 0xff;
+    for (int i = 0; i < len; ++i) {
+        uint16_t crc = res;
+        for (int b = 0; b < 8; ++b) crc = (crc & 0x8000) ? (uint16_t)((crc << 1) ^ 0x1021) : (uint16_t)(crc << 1);
+        uint8_t t = v & 0xB8;
+        t ^= t >> 4; t ^= t >> 2; t ^= t >> 1;
+        v = (uint8_t)((t & 1) | (v << 1));
+        res = crc ^ data[i];
+    }
+    res ^= v;
+    uint8_t t = v & 0xB8;
+    t ^= t >> 4; t ^= t >> 2; t ^= t >> 1;
+    v = (uint8_t)((t & 1) | (v << 1));
+    res ^= (uint16_t)(v << 8);
+    return res;
+}
+
+
+
+__device__ __forceinline__ void finalize_frame(const FinalArgs& A, unsigned long long f) {
+    lphy_frame_meta m = A.meta[f];
+    if (m.status != 0) return;
+    if (A.set_sync && m.have_sync)
+        m.sync_word = (uint8_t)((((m.sw0 >> A.shift) & 0x0f) << 4) | ((m.sw1 >> A.shift) & 0x0f));
+    if (A.decode) {
+        if (A.nsyms & 1) {
+            m.status = -EINVAL;  // LoRaDecoder.cpp:10
+        } else {
+            const unsigned long long nb = A.nsyms / 2;
+            const uint16_t* s = A.syms + f * A.sym_stride;
+            uint8_t* out = A.bytes + f * nb;
+            for (unsigned long long k = 0; k < nb; ++k) {
+                const uint8_t hi = hamming84_decode((uint8_t)s[2 * k]) & 0x0f;
+                const uint8_t lo = hamming84_decode((uint8_t)s[2 * k + 1]) & 0x0f;
+                out[k] = (uint8_t)((hi << 4) | lo);
+            }
+            if (nb >= 4) {  // phy.cpp:252-259
+                const uint16_t provided = (uint16_t)(out[nb - 2] | (out[nb - 1] << 8));
+                m.crc_ok = provided == sx1272_checksum(out + 2, (int)(nb - 4));
+            } else {
+                m.crc_ok = 0;
+            }
+        }
+    }
+    A.meta[f] = m;
+}
+
+__global__ void k_finalize(FinalArgs A) {
+    const unsigned long long f = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < A.frames) finalize_frame(A, f);
+}
+
+// ---------------------------------------------------------------------------
+// Exact re-run of one frame by a whole 256-thread workgroup (k_post): the
+// reference's arithmetic with its Annex G complex products (cmul_x)
+// everywhere - max-abs (LoRaDemod.cpp:60-78), estimate (LoRaDemod.cpp:80-140
+// / phy.cpp:81-148), every symbol (LoRaDemod.cpp:142-176 / phy.cpp:204-238).
+// Frames get here only when a hot kernel met a non-finite value (status
+// kStatusFixup), so this path favours plainness over speed.
+// ---------------------------------------------------------------------------
+template <int SF>
+struct PostShared {
+    cf32 lds[Geo<SF>::T * Geo<SF>::SSTRIDE];
+    ArgMax red[kTile / 64];
+    UnitResult units[Geo<SF>::T];
+    float upow[Geo<SF>::T];
+    float wmax[kTile / 64];
+    lphy_frame_meta m;
+    uint16_t sw[2];
+    unsigned list[kTile];
+    unsigned count;
+};
+
+template <int SF, int MODE>
+__device__ void exact_frame(const DemodArgs& A, unsigned f, PostShared<SF>& sh) {
+    using G = Geo<SF>;
+    constexpr int N = G::N, T = G::T;
+    const int tid = threadIdx.x;
+    const int slot = tid / G::LPS, lam = tid % G::LPS;
+    const cf32* fr = A.iq + (unsigned long long)f * A.frame_samples;
+    const unsigned long long step = (unsigned long long)N * A.osr;
+    const bool have_sync = A.total_syms >= 2;
+    // (1) normalisation (modes 1, 2)
+    if (MODE != LPHY_MODE_DEMODULATE) {
+        const unsigned long long count = MODE == LPHY_MODE_DECHIRP_LORA_DEMODULATE
+                                             ? A.total_syms * N : A.frame_samples;
+        float mx = 0.0f;
+        for (unsigned long long i = tid; i < count; i += kTile) {
+            cf32 x = fr[i];
+            if (MODE == LPHY_MODE_DECHIRP_LORA_DEMODULATE) x = cmul_x(x, A.down[i & (N - 1)]);
+            maxabs_acc(mx, x);
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const float o = __shfl_xor(mx, off, 64);
+            mx = o > mx ? o : mx;
+        }
+        if ((tid & 63) == 0) sh.wmax[tid >> 6] = mx;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        lphy_frame_meta m{};
+        m.scale = 1.0f;
+        m.have_sync = have_sync;
+        if (MODE != LPHY_MODE_DEMODULATE) {
+            float mx = sh.wmax[0];
+            for (int w = 1; w < kTile / 64; ++w) mx = sh.wmax[w] > mx ? sh.wmax[w] : mx;
+            m = norm_meta(mx, have_sync, A.no_scratch);
+        }
+        sh.m = m;
+        sh.sw[0] = sh.sw[1] = 0;
+    }
+    __syncthreads();
+    // (2) estimate: units (symbol, osr phase) in chunks of T, folded in
+    // order by thread 0 (the separate k_estimate's unpacked path)
+    EstFold fold;
+    const int U = A.est_units;
+    const bool tie_low = MODE != LPHY_MODE_DEMODULATE;
+    for (int c0 = 0; c0 < U && sh.m.status == 0; c0 += T) {
+        const lphy_frame_meta m = sh.m;
+        const int u = c0 + slot;
+        const bool live = u < U;
+        const int s = live ? u / A.osr : 0, t = live ? u % A.osr : 0;
+        const Stage<SF> st(slot, lam);
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) {
+            const int i = lam + e * G::LPS;
+            cf32 x = czero();
+            if (live) x = est_sample(A, fr, (unsigned long long)s * step + t + (unsigned long long)i * A.osr, i, N, m);
+            st.put(sh.lds, e, x);
+        }
+        __syncthreads();
+        cf32 v[16];
+        fft_tile<SF, false, true>(v, sh.lds, slot, lam, A.tw);
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) sh.lds[G::addr(slot, bin_of<SF>(e, lam))] = v[e];
+        const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), sh.red);
+        __syncthreads();
+        if (lam == 0) {
+            sh.units[slot] = live ? unit_result<SF>(sh.lds, slot, best) : UnitResult{0, 0, 0.0f, 0.0f, 0};
+            sh.upow[slot] = live && A.osr > 1 ? detector_power(best.v > 0.0f ? best.v : 0.0f, A.power_scale) : 0.0f;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const int nu = U - c0 < T ? U - c0 : T;
+            for (int k = 0; k < nu; ++k) fold.unit(sh.units[k], A.osr > 1 ? sh.upow[k] : 0.0f, A.osr, tie_low);
+        }
+        __syncthreads();
+    }
+    if (tid == 0 && sh.m.status == 0) fold.finish(sh.m, U / A.osr, N, A.osr);
+    __syncthreads();
+    // (3) symbols, T per tile, exact per-sample rotation
+    const lphy_frame_meta m = sh.m;
+    const unsigned S = (unsigned)A.total_syms;
+    for (unsigned s0 = 0; s0 < S; s0 += T) {
+        const unsigned s = s0 + slot;
+        const bool live = s < S;
+        const SymCtx c = sym_ctx<true>(A, f, live ? s : 0, live, N, m);
+        if (A.win)
+            restage_symbol<SF, MODE | kWinBit, true>(sh.lds, Stage<SF>(slot, lam), fr + c.base, c, lam,
+                                                     A.down, A.win, (unsigned)A.osr);
+        else
+            restage_symbol<SF, MODE, true>(sh.lds, Stage<SF>(slot, lam), fr + c.base, c, lam,
+                                           A.down, nullptr, (unsigned)A.osr);
+        __syncthreads();
+        cf32 v[16];
+        fft_tile<SF, false, true>(v, sh.lds, slot, lam, A.tw);
+        const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), sh.red);
+        if (lam == 0 && live) {
+            if (c.have_sync && s < 2) sh.sw[s] = c.ok ? (uint16_t)best.i : (uint16_t)0;
+            else if (c.ok) A.syms[(unsigned long long)f * A.out_per_frame + (c.have_sync ? s - 2 : s)] = (uint16_t)best.i;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        lphy_frame_meta r = sh.m;
+        r.sw0 = sh.sw[0];
+        r.sw1 = sh.sw[1];
+        A.meta[f] = r;
+    }
+    __syncthreads();
+}
+
+// After the symbol kernels: the exact re-run of the frames they flagged,
+// then (fin) the per-frame finalisation, one thread per frame.
+template <int SF, int MODE>
+__global__ __launch_bounds__(kTile) void k_post(DemodArgs A, FinalArgs F, int fix, int fin) {
+    __shared__ PostShared<SF> sh;
+    const unsigned long long f = (unsigned long long)blockIdx.x * kTile + threadIdx.x;
+    if (fix) {
+        const bool flagged = f < A.frames && A.meta[f].status == kStatusFixup;
+        if (__syncthreads_or(flagged)) {
+            if (threadIdx.x == 0) sh.count = 0;
+            __syncthreads();
+            if (flagged) sh.list[atomicAdd(&sh.count, 1u)] = (unsigned)f;
+            __syncthreads();
+            const unsigned n = sh.count;
+            for (unsigned k = 0; k < n; ++k) exact_frame<SF, MODE>(A, sh.list[k], sh);
+        }
+    }
+    if (fin && f < A.frames) finalize_frame(F, f);
+}
+
+// ---------------------------------------------------------------------------
+// lora_modulate (LoRaMod.cpp:8-43 + ChirpGenerator.hpp:24-51), bit-exact.
+// Pass 1: one thread per frame walks the phase accumulator through every
+// symbol (no sincos) and records the phase at each symbol start.  Pass 2: one
+// thread per symbol regenerates its samples from that phase.
+// ---------------------------------------------------------------------------
+struct ModArgs {
+    const uint16_t* syms;
+    cf32* iq;
+    float* phase0;           // frames * (nsyms + 2) phase at symbol start
+    unsigned long long frames, nsyms;
+    int N, osr;
+    float bws, ampl;
+    uint8_t sync;
+};
+
+__device__ __forceinline__ float mod_f0(const ModArgs& A, unsigned long long f, unsigned long long s) {
+    const int shift = 0;
+    (void)shift;
+    uint16_t v;
+    if (s < 2) {
+        int sf = 0;
+        while ((1 << sf) < A.N) ++sf;
+        const unsigned sh = sf > 4 ? sf - 4 : 0;
+        v = s == 0 ? (uint16_t)((A.sync >> 4) << sh) : (uint16_t)((A.sync & 0x0f) << sh);
+    } else {
+        v = A.syms[f * A.nsyms + (s - 2)];
+    }
+    return (2.0f * kPi * (float)v * A.bws) / ((float)A.N * (float)A.osr);
+}
+
+__global__ void k_mod_phase(ModArgs A) {
+    const unsigned long long f = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= A.frames) return;
+    const float fmin = -kPi * A.bws / (float)A.osr;
+    const float fmax = kPi * A.bws / (float)A.osr;
+    const float fstep = (2.0f * kPi * A.bws) / (float)(A.N * A.osr * A.osr);
+    const int step = A.N * A.osr;
+    float phase = 0.0f;
+    const unsigned long long ns = A.nsyms + 2;
+    for (unsigned long long s = 0; s < ns; ++s) {
+        A.phase0[f * ns + s] = phase;
+        float fr = fmin + mod_f0(A, f, s);
+        for (int i = 0; i < step; ++i) {
+            fr += fstep;
+            if (fr > fmax) fr -= (fmax - fmin);
+            phase += fr;
+        }
+        const double w = floor((double)(phase / (2.0f * kPi))) * 2 * (double)kPi;
+        phase = (float)((double)phase - w);
+    }
+}
+
+__global__ void k_mod_samples(ModArgs A) {
+    const unsigned long long g = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long ns = A.nsyms + 2;
+    if (g >= A.frames * ns) return;
+    const unsigned long long f = g / ns, s = g % ns;
+    const float fmin = -kPi * A.bws / (float)A.osr;
+    const float fmax = kPi * A.bws / (float)A.osr;
+    const float fstep = (2.0f * kPi * A.bws) / (float)(A.N * A.osr * A.osr);
+    const int step = A.N * A.osr;
+    float phase = A.phase0[g];
+    float fr = fmin + mod_f0(A, f, s);
+    cf32* out = A.iq + (f * ns + s) * (unsigned long long)step;
+    for (int i = 0; i < step; ++i) {
+        fr += fstep;
+        if (fr > fmax) fr -= (fmax - fmin);
+        phase += fr;
+        float sn, cs;
+        lphy_libm::sincosf_exact(phase, &sn, &cs);
+        out[i] = cf32{A.ampl * cs, A.ampl * sn};
+    }
+}
+
+// compensate_offsets (phy.cpp:150-180): rotation then integer time shift.
+__global__ void k_comp_rotate(cf32* out, const cf32* in, unsigned long long count,
+                              float rate) {
+    const unsigned long long n = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= count) return;
+    const float ph = rate * (float)n;
+    float sn, cs;
+    lphy_libm::sincosf_exact(ph, &sn, &cs);
+    out[n] = cmul_x(in[n], cf32{cs, sn});  // samples[n] *= complex (phy.cpp:163)
+}
+
+__global__ void k_comp_shift(cf32* out, const cf32* in, unsigned long long count,
+                             long long offset) {
+    const unsigned long long n = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= count) return;
+    const long long src = (long long)n - offset;
+    out[n] = (src >= 0 && src < (long long)count) ? in[src] : czero();
+}
+
+}  // namespace
+
+#ifdef LPHY_SF  // per-SF translation unit: launch templates
+namespace {
+#define HIP_OK(x)                                                         \
+    do {                                                                  \
+        hipError_t e_ = (x);                                              \
+        if (e_ != hipSuccess) {                                           \
+            fprintf(stderr, "lphy_hip: %s failed: %s (%s:%d)\n", #x,      \
+                    hipGetErrorString(e_), __FILE__, __LINE__);           \
+            return -EIO;                                                  \
+        }                                                                 \
+    } while (0)
+
+// Waves per SIMD the demod kernel is register-budgeted for (launch bound):
+// 3 (<= 168 VGPRs) or 2 (<= 256).  LPHY_DEMOD_OCC overrides for experiments.
+constexpr int demod_occ(int sf) { return sf <= 8 ? 3 : 2; }
+
+template <int SF, int MODE, int OCC>
+int demod_grid() {
+    static int grid = 0;
+    if (grid == 0) {
+        int dev = 0, cus = 0, per = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_demod<SF, MODE, OCC>, kTile, 0);
+        grid = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
+    }
+    return grid;
+}
+
+inline int cu_count() {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (cus <= 0) cus = 256;
+    }
+    return cus;
+}
+
+// per_cu > 0 caps the persistent grid at per_cu workgroups per CU (room
+// for a concurrent kernel on another stream)
+template <int SF, int MODE, int OCC>
+void launch_symbols_occ(const DemodArgs& A0, unsigned long long tiles, hipStream_t st, int per_cu) {
+    using G = Geo<SF>;
+    constexpr bool WAVE = G::LPS <= 64;
+    constexpr int WT = WAVE ? 64 / G::LPS : G::T;      // symbols per worker tile
+    constexpr int WPB = WAVE ? kTile / 64 : 1;         // workers per workgroup
+    unsigned long long g = (unsigned long long)demod_grid<SF, MODE, OCC>();
+    if (per_cu > 0 && g > (unsigned long long)per_cu * cu_count()) g = (unsigned long long)per_cu * cu_count();
+    const unsigned long long wtiles = (A0.frames * A0.total_syms + WT - 1) / WT;
+    unsigned long long grid = (wtiles + WPB - 1) / WPB;
+    if (grid > g) grid = g;
+    DemodArgs A = A0;
+    const unsigned long long stride = grid * WPB * WT;  // symbols per worker step
+    A.stride_f = (unsigned)(stride / A0.total_syms);
+    A.stride_s = (unsigned)(stride % A0.total_syms);
+    (void)tiles;
+    hipLaunchKernelGGL((k_demod<SF, MODE, OCC>), dim3((unsigned)grid), dim3(kTile), 0, st, A);
+}
+
+template <int SF, int MODE>
+void launch_symbols(const DemodArgs& A, unsigned long long tiles, hipStream_t st, int per_cu) {
+    launch_symbols_occ<SF, MODE, demod_occ(SF)>(A, tiles, st, per_cu);
+}
+
+// Fused path (k_frames).
+template <int SF, int MODE, int OCC>
+int frames_grid() {
+    static int grid = 0;
+    if (grid == 0) {
+        int dev = 0, cus = 0, per = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_frames<SF, MODE, OCC>, kTile, 0);
+        grid = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
+    }
+    return grid;
+}
+
+template <int SF, int MODE, int OCC>
+int launch_frames_occ(const DemodArgs& A, hipStream_t st) {
+    FrameArgs P{};
+    P.A = A;
+    constexpr unsigned WPB = kTile / 64;
+    unsigned long long blocks = (unsigned long long)frames_grid<SF, MODE, OCC>();
+    const unsigned long long need = (A.frames + WPB - 1) / WPB;
+    if (blocks > need) blocks = need;
+    P.waves = (unsigned)(blocks * WPB);
+    hipLaunchKernelGGL((k_frames<SF, MODE, OCC>), dim3((unsigned)blocks), dim3(kTile), 0, st, P);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+// Waves per SIMD of k_frames: 2 (<= 256 VGPRs; its loop carries more state
+// than k_demod's and spills at 3).
+template <int SF, int MODE>
+int launch_frames_mode(const DemodArgs& A, hipStream_t st) {
+    return launch_frames_occ<SF, MODE, 2>(A, st);
+}
+
+
+
+template <int SF, int MODE>
+void launch_symbols_w(const DemodArgs& A, unsigned long long tiles, hipStream_t st, int per_cu) {
+    if (A.osr > 1) {
+        // oversampled input: strided symbol loads (no dechirp mode here)
+        if constexpr ((MODE & 3) != LPHY_MODE_DECHIRP_LORA_DEMODULATE) {
+            if (A.win) launch_symbols_occ<SF, MODE | kWinBit | kOsrBit, 2>(A, tiles, st, per_cu);
+            else launch_symbols_occ<SF, MODE | kOsrBit, 2>(A, tiles, st, per_cu);
+        }
+        return;
+    }
+    if (A.win) launch_symbols<SF, MODE | kWinBit>(A, tiles, st, per_cu);
+    else launch_symbols<SF, MODE>(A, tiles, st, per_cu);
+}
+
+template <int SF>
+int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symbols, int per_cu) {
+    using G = Geo<SF>;
+    if (prologue) {
+        if (A.mode != LPHY_MODE_DEMODULATE)
+            hipLaunchKernelGGL(k_maxabs<SF>, dim3((unsigned)A.frames), dim3(kTile), 0, st, A);
+        const int fpt = A.est_units <= G::T ? G::T / A.est_units : 1;
+        const unsigned long long blocks = (A.frames + fpt - 1) / fpt;
+        hipLaunchKernelGGL(k_estimate<SF>, dim3((unsigned)blocks), dim3(kTile), 0, st, A);
+    }
+    if (symbols) {
+        const unsigned long long nsym = A.frames * A.total_syms;
+        const unsigned long long tiles = (nsym + G::T - 1) / G::T;
+        if (tiles) {
+            switch (A.mode) {
+                case LPHY_MODE_DEMODULATE: launch_symbols_w<SF, LPHY_MODE_DEMODULATE>(A, tiles, st, per_cu); break;
+                case LPHY_MODE_LORA_DEMODULATE: launch_symbols_w<SF, LPHY_MODE_LORA_DEMODULATE>(A, tiles, st, per_cu); break;
+                default: launch_symbols_w<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>(A, tiles, st, per_cu); break;
+            }
+        }
+    }
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+template <int SF>
+int launch_frames_sf(const DemodArgs& A, hipStream_t st) {
+    if constexpr (Geo<SF>::LPS > 64) {
+        (void)A; (void)st;
+        return -ENOTSUP;
+    } else {
+        switch (A.mode) {
+            case LPHY_MODE_DEMODULATE:
+                return A.win ? launch_frames_mode<SF, LPHY_MODE_DEMODULATE | kWinBit>(A, st)
+                             : launch_frames_mode<SF, LPHY_MODE_DEMODULATE>(A, st);
+            case LPHY_MODE_LORA_DEMODULATE:
+                return A.win ? launch_frames_mode<SF, LPHY_MODE_LORA_DEMODULATE | kWinBit>(A, st)
+                             : launch_frames_mode<SF, LPHY_MODE_LORA_DEMODULATE>(A, st);
+            default:
+                return A.win ? launch_frames_mode<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE | kWinBit>(A, st)
+                             : launch_frames_mode<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>(A, st);
+        }
+    }
+}
+
+template <int SF>
+int launch_post_sf(int mode, const DemodArgs& A, const FinalArgs& F, bool fix, bool fin, hipStream_t st) {
+    const dim3 grid((unsigned)((A.frames + kTile - 1) / kTile));
+    switch (mode) {
+        case LPHY_MODE_DEMODULATE:
+            hipLaunchKernelGGL((k_post<SF, LPHY_MODE_DEMODULATE>), grid, dim3(kTile), 0, st, A, F, (int)fix, (int)fin);
+            break;
+        case LPHY_MODE_LORA_DEMODULATE:
+            hipLaunchKernelGGL((k_post<SF, LPHY_MODE_LORA_DEMODULATE>), grid, dim3(kTile), 0, st, A, F, (int)fix, (int)fin);
+            break;
+        default:
+            hipLaunchKernelGGL((k_post<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>), grid, dim3(kTile), 0, st, A, F, (int)fix,
+                               (int)fin);
+            break;
+    }
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+template <int SF>
+int launch_estimate_sf(const DemodArgs& A, hipStream_t st) {
+    const int fpt = A.est_units <= Geo<SF>::T ? Geo<SF>::T / A.est_units : 1;
+    hipLaunchKernelGGL(k_estimate<SF>, dim3((unsigned)((A.frames + fpt - 1) / fpt)), dim3(kTile), 0, st, A);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+}  // namespace
+#endif
