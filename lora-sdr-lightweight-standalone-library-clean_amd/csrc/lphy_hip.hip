@@ -30,9 +30,24 @@
 // ===========================================================================
 // Host side
 // ===========================================================================
-// ===========================================================================
-// Host side
-// ===========================================================================
+#ifndef __HIP_DEVICE_COMPILE__
+// Empty launch tables, overridden by every lphy_sf.hip object linked in
+// (experiment builds may link only the SF they time: tools/ubench/variants.py)
+namespace lphy {
+__attribute__((weak)) extern const SfOps sf_ops_1 = {};
+__attribute__((weak)) extern const SfOps sf_ops_2 = {};
+__attribute__((weak)) extern const SfOps sf_ops_3 = {};
+__attribute__((weak)) extern const SfOps sf_ops_4 = {};
+__attribute__((weak)) extern const SfOps sf_ops_5 = {};
+__attribute__((weak)) extern const SfOps sf_ops_6 = {};
+__attribute__((weak)) extern const SfOps sf_ops_7 = {};
+__attribute__((weak)) extern const SfOps sf_ops_8 = {};
+__attribute__((weak)) extern const SfOps sf_ops_9 = {};
+__attribute__((weak)) extern const SfOps sf_ops_10 = {};
+__attribute__((weak)) extern const SfOps sf_ops_11 = {};
+__attribute__((weak)) extern const SfOps sf_ops_12 = {};
+}  // namespace lphy
+#endif
 struct lphy_hip_ctx {
     int device = 0;
     unsigned sf = 0, N = 0, bw_hz = 0, osr = 1;
@@ -112,7 +127,7 @@ const SfOps* sf_ops(unsigned sf) {
     static const SfOps* const t[13] = {nullptr,    &sf_ops_1, &sf_ops_2, &sf_ops_3,  &sf_ops_4,
                                        &sf_ops_5,  &sf_ops_6, &sf_ops_7, &sf_ops_8,  &sf_ops_9,
                                        &sf_ops_10, &sf_ops_11, &sf_ops_12};
-    return sf >= 1 && sf <= 12 ? t[sf] : nullptr;
+    return sf >= 1 && sf <= 12 && t[sf]->demod ? t[sf] : nullptr;
 }
 
 int launch_demod(unsigned sf, const DemodArgs& A, hipStream_t st, bool pro, bool sym, int per_cu = 0) {

@@ -156,6 +156,10 @@ __device__ __forceinline__ void maxabs_acc(float& mx, cf32 x) {
 // product (cmul_x) could differ from the hot kernels' plain one, and is
 // re-run exactly by k_post.  Never left in a record after the call.
 constexpr int kStatusFixup = 0x7f5a0001;
+// ... and: some symbols were left uncertified by the fused kernel's fast
+// rotation (value kSymRecheck in the output; k_post recomputes exactly those)
+constexpr int kStatusRecheck = 0x7f5a0002;
+constexpr uint16_t kSymRecheck = 0xffff;  // never a bin index (N <= 4096)
 
 // Normalisation decision of LoRaDemod.cpp:60-78 from the frame's max-abs.
 __device__ __forceinline__ lphy_frame_meta norm_meta(float mx, bool have_sync, int no_scratch) {
@@ -1092,7 +1096,6 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     }
     cf32 rreg[16];                 // SF 9-10: the team's table ...
     unsigned rreg_fk = 0xffffffffu;  // ... of this frame
-    unsigned long long rechecks = 0;
 
     for (unsigned t = 0; t < ntiles; ++t) {
         // SF 9-10: a team entering a new frame builds its table entries
@@ -1189,27 +1192,16 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         const bool redo = kind == kUnitSym && c.ok &&
                           (exact_only || !fast_applies<SF, MODE>(c, c.toff) ||
                            !fast_certified<SF>(b2, c, amax));
-        const unsigned long long rmask = __ballot(redo);
-        if (rmask) {
-            // one sample at a time: the re-check is rare, and a serial loop
-            // keeps its sincos temporaries out of the main path's registers
-            restage_symbol<SF, MODE, false>(lds, stg, A.iq + (unsigned long long)c.f * A.frame_samples + c.base,
-                                            c, lam, down, win);
-            team_sync<SF>();
-            cf32 vx[16];
-            fft_tile<SF>(vx, lds, slot, lam, twl);
-            // NaN bins: possibly an Annex G product, exact re-run of the frame
-            if (redo && fft_has_nan<SF>(vx) && lam == 0) A.meta[c.f].status = kStatusFixup;
-            const ArgMax ex = symbol_argmax<SF>(local_argmax<SF>(vx, lam), nullptr);
-            if (redo) best = ex;
-            rechecks += (unsigned long long)__popcll(rmask) / G::LPS;
-            team_sync<SF>();
-        }
+        // (no exact re-run here: it would keep a second transform's state
+        // live beside the prefetch.  The symbol is left as kSymRecheck and
+        // its frame as kStatusRecheck; k_post recomputes it exactly.)
         if (kind == kUnitSym && lam == 0) {
             // sw0 / sw1 also for frames that are not demodulated (0, as the
             // separate-launch path leaves them)
-            if (c.have_sync && c.s < 2) store_symbol(A, c, c.ok ? (uint16_t)best.i : (uint16_t)0);
-            else if (c.ok) store_symbol(A, c, (uint16_t)best.i);
+            const uint16_t out = redo ? kSymRecheck : (uint16_t)best.i;
+            if (c.have_sync && c.s < 2) store_symbol(A, c, c.ok ? out : (uint16_t)0);
+            else if (c.ok) store_symbol(A, c, out);
+            if (redo) A.meta[c.f].status = kStatusRecheck;
         }
         team_sync<SF>();  // slot reads (and ures) done
         // the frame whose last estimate unit was in this tile: fold
@@ -1253,7 +1245,6 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         su = nsu;
         c = nc;
     }
-    if (lane == 0 && rechecks) atomicAdd(&A.counters[0], rechecks);
 }
 
 // ---------------------------------------------------------------------------
@@ -1347,6 +1338,7 @@ struct PostShared {
     lphy_frame_meta m;
     uint16_t sw[2];
     unsigned list[kTile];
+    unsigned listf[kTile];
     unsigned count;
 };
 
@@ -1460,21 +1452,95 @@ __device__ void exact_frame(const DemodArgs& A, unsigned f, PostShared<SF>& sh) 
     __syncthreads();
 }
 
-// After the symbol kernels: the exact re-run of the frames they flagged,
-// then (fin) the per-frame finalisation, one thread per frame.
+// Symbols the fused kernel's certificate left open (kSymRecheck in the
+// output, frame status kStatusRecheck) among the workgroup's frames fb ..
+// fb + kTile - 1: the reference's per-sample rotation with its Annex G
+// products, T (frame, symbol) pairs per tile; the frames' offsets from the
+// hot kernel stand (only symbol units were uncertified).  Thread t scans
+// frame fb + t when `mine` (its status is kStatusRecheck).
+template <int SF, int MODE>
+__device__ void recheck_frames(const DemodArgs& A, unsigned long long fb, bool mine, PostShared<SF>& sh) {
+    using G = Geo<SF>;
+    constexpr int N = G::N, T = G::T;
+    const int tid = threadIdx.x;
+    const int slot = tid / G::LPS, lam = tid % G::LPS;
+    const unsigned S = (unsigned)A.total_syms;
+    unsigned cur = mine ? 0u : S;  // this thread's scan position in its frame
+    unsigned long long done = 0;
+    lphy_frame_meta mm{};
+    if (mine) mm = A.meta[fb + tid];
+    for (;;) {
+        __syncthreads();
+        if (tid == 0) sh.count = 0;
+        __syncthreads();
+        // collect up to kTile open symbols
+        if (cur < S) {
+            const unsigned long long f = fb + tid;
+            const bool hs = mm.have_sync != 0;
+            const uint16_t* out = A.syms + f * A.out_per_frame;
+            for (; cur < S; ++cur) {
+                const uint16_t v = (hs && cur < 2) ? (cur == 0 ? mm.sw0 : mm.sw1) : out[hs ? cur - 2 : cur];
+                if (v != kSymRecheck) continue;
+                const unsigned k = atomicAdd(&sh.count, 1u);
+                if (k >= kTile) break;  // full: this symbol goes in the next round
+                sh.list[k] = cur;
+                sh.listf[k] = (unsigned)tid;
+            }
+        }
+        __syncthreads();
+        const unsigned n = sh.count < kTile ? sh.count : kTile;
+        if (n == 0) break;
+        done += n;
+        for (unsigned k0 = 0; k0 < n; k0 += T) {
+            const unsigned k = k0 + (unsigned)slot;
+            const bool live = k < n;
+            const unsigned sy = live ? sh.list[k] : 0;
+            const unsigned long long f = fb + (live ? sh.listf[k] : 0);
+            lphy_frame_meta m = A.meta[f];
+            m.status = 0;
+            const SymCtx c = sym_ctx<true>(A, (unsigned)f, sy, live, N, m);
+            const cf32* fr = A.iq + f * A.frame_samples;
+            if (A.win)
+                restage_symbol<SF, MODE | kWinBit, true>(sh.lds, Stage<SF>(slot, lam), fr + c.base, c, lam,
+                                                         A.down, A.win, (unsigned)A.osr);
+            else
+                restage_symbol<SF, MODE, true>(sh.lds, Stage<SF>(slot, lam), fr + c.base, c, lam,
+                                               A.down, nullptr, (unsigned)A.osr);
+            __syncthreads();
+            cf32 v[16];
+            fft_tile<SF, false, true>(v, sh.lds, slot, lam, A.tw);
+            const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), sh.red);
+            if (lam == 0 && live) store_symbol(A, c, (uint16_t)best.i);
+            __syncthreads();
+        }
+    }
+    if (tid == 0 && done) atomicAdd(&A.counters[0], done);
+}
+
+// After the symbol kernels: the exact re-run of the frames they flagged
+// (kStatusFixup: whole frame; kStatusRecheck: the open symbols), then (fin)
+// the per-frame finalisation, one thread per frame.
 template <int SF, int MODE>
 __global__ __launch_bounds__(kTile) void k_post(DemodArgs A, FinalArgs F, int fix, int fin) {
     __shared__ PostShared<SF> sh;
+    __shared__ unsigned flist[kTile];
+    __shared__ unsigned fcount;
     const unsigned long long f = (unsigned long long)blockIdx.x * kTile + threadIdx.x;
     if (fix) {
-        const bool flagged = f < A.frames && A.meta[f].status == kStatusFixup;
-        if (__syncthreads_or(flagged)) {
-            if (threadIdx.x == 0) sh.count = 0;
+        const int st = f < A.frames ? A.meta[f].status : 0;
+        const bool fixup = st == kStatusFixup, recheck = st == kStatusRecheck;
+        if (__syncthreads_or(fixup)) {
+            if (threadIdx.x == 0) fcount = 0;
             __syncthreads();
-            if (flagged) sh.list[atomicAdd(&sh.count, 1u)] = (unsigned)f;
+            if (fixup) flist[atomicAdd(&fcount, 1u)] = (unsigned)f;
             __syncthreads();
-            const unsigned n = sh.count;
-            for (unsigned k = 0; k < n; ++k) exact_frame<SF, MODE>(A, sh.list[k], sh);
+            const unsigned n = fcount;
+            for (unsigned k = 0; k < n; ++k) exact_frame<SF, MODE>(A, flist[k], sh);
+        }
+        if (__syncthreads_or(recheck)) {
+            recheck_frames<SF, MODE>(A, (unsigned long long)blockIdx.x * kTile, recheck, sh);
+            __syncthreads();
+            if (recheck) A.meta[f].status = 0;
         }
     }
     if (fin && f < A.frames) finalize_frame(F, f);
@@ -1672,9 +1738,12 @@ int launch_frames_occ(const DemodArgs& A, hipStream_t st) {
 
 // Waves per SIMD of k_frames: 2 (<= 256 VGPRs; its loop carries more state
 // than k_demod's and spills at 3).
+#ifndef LPHY_FRAMES_OCC  // experiments: -DLPHY_FRAMES_OCC=3
+#define LPHY_FRAMES_OCC 2
+#endif
 template <int SF, int MODE>
 int launch_frames_mode(const DemodArgs& A, hipStream_t st) {
-    return launch_frames_occ<SF, MODE, 2>(A, st);
+    return launch_frames_occ<SF, MODE, LPHY_FRAMES_OCC>(A, st);
 }
 
 

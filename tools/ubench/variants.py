@@ -1,5 +1,5 @@
-"""Build-flag / source variants of liblphy_hip.so restricted to one SF
-(-DLPHY_ONLY_SF) and time their kernels on the bench workload.
+"""Build-flag / source variants of liblphy_hip.so restricted to one SF (the
+host TU plus that SF's kernel TU) and time their kernels on the bench workload.
   python tools/ubench/variants.py build <sf> name:"flags" ...   (dev container)
   python tools/ubench/variants.py run <sf> name ...             (GPU box)
 Timing aid only."""
@@ -19,8 +19,9 @@ def build(sf, specs):
         name, _, flags = spec.partition(":")
         so = HERE / f"var_{name}.so"
         cmd = (f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off "
-               f"-fno-slp-vectorize -fPIC -shared -DLPHY_ONLY_SF={sf} {flags} -I{ROOT}/include "
-               f"-I{PKG}/csrc -o {so} {PKG}/csrc/lphy_hip.hip")
+               f"-fno-slp-vectorize -fPIC -shared -DLPHY_SF={sf} {flags} -I{ROOT}/include "
+               f"-I{PKG}/csrc -o {so} {PKG}/csrc/lphy_hip.hip {PKG}/csrc/lphy_sf.hip "
+               f"{PKG}/csrc/lphy_stream.hip")
         procs.append((name, subprocess.Popen(cmd, shell=True)))
     for name, p in procs:
         assert p.wait() == 0, name
