@@ -86,10 +86,14 @@ enum lphy_flags {
     LPHY_F_UNFUSED = 32u,        /* separate prologue / symbol launches
                                     instead of the fused single launch
                                     (same results; for comparison)       */
-    LPHY_F_EXACT_ROTATION = 64u  /* fused launch: rotate every symbol with
+    LPHY_F_EXACT_ROTATION = 64u, /* fused launch: rotate every symbol with
                                     the per-sample sincos of the reference
                                     instead of the certified per-frame
                                     table (same results; for comparison) */
+    LPHY_F_RESIDENT = 128u       /* fused launch: where it applies (SF 7,
+                                    56..70 whole symbols per frame), the
+                                    single-read kernel that keeps each frame
+                                    on the CU (same results; experimental) */
 };
 
 enum lphy_window { LPHY_WINDOW_NONE = 0, LPHY_WINDOW_HANN = 1 };

@@ -310,6 +310,7 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     A.no_scratch = (flags & LPHY_F_NO_SCRATCH) ? 1 : 0;
     A.exact_rotation = (flags & LPHY_F_EXACT_ROTATION) ? 1 : 0;
     A.counters = c->d_counters;
+    A.resident = (flags & LPHY_F_RESIDENT) ? 1 : 0;
     const size_t est_syms = mode == LPHY_MODE_DEMODULATE ? 2 : (total < 2 ? total : 2);
     A.est_units = (int)(est_syms * c->osr);
     // 32-bit symbol / sample bookkeeping in the kernels
@@ -326,6 +327,7 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     // c: the co-running kernels slowed each other ~2x, 1.1x slower overall.)
     const bool fused = (all || (stages & both) == both) && !(flags & LPHY_F_UNFUSED) &&
                        fused_enabled() && frames_fit(c->sf, c->osr, A.est_units, total);
+    A.sentinels = fused ? 1 : 0;  // k_cuframe marks open symbols in the output only
     int rc = fused ? launch_frames(c->sf, A, st)
                    : launch_demod(c->sf, A, st, all || (stages & LPHY_F_STAGE_PROLOGUE),
                                   all || (stages & LPHY_F_STAGE_SYMBOLS));

@@ -67,6 +67,8 @@ struct DemodArgs {
     int exact_rotation;      // LPHY_F_EXACT_ROTATION: no certified fast path
     float power_scale;       // LoRaDetector.hpp:29, (float)(20*log10((double)N))
     unsigned long long* counters;  // ctx counters: [0] rechecks, [1..4] phase clocks
+    int sentinels;           // k_post: look for kSymRecheck in frames with status 0 (k_cuframe)
+    int resident;            // LPHY_F_RESIDENT: k_cuframe where it applies
     // persistent demod workers: symbol stride per step split into whole
     // frames + symbols (host-computed, so the kernel never divides)
     unsigned stride_f, stride_s;
@@ -1517,6 +1519,16 @@ __device__ void recheck_frames(const DemodArgs& A, unsigned long long fb, bool m
     if (tid == 0 && done) atomicAdd(&A.counters[0], done);
 }
 
+// Whether frame f holds a symbol left open by k_cuframe, which marks them in
+// the output only (kSymRecheck): its symbols and the sync symbols' record.
+__device__ __forceinline__ bool has_sentinel(const DemodArgs& A, unsigned long long f) {
+    const lphy_frame_meta m = A.meta[f];
+    bool any = m.have_sync && (m.sw0 == kSymRecheck || m.sw1 == kSymRecheck);
+    const uint16_t* o = A.syms + f * A.out_per_frame;
+    for (unsigned long long i = 0; i < A.out_per_frame; ++i) any |= o[i] == kSymRecheck;
+    return any;
+}
+
 // After the symbol kernels: the exact re-run of the frames they flagged
 // (kStatusFixup: whole frame; kStatusRecheck: the open symbols), then (fin)
 // the per-frame finalisation, one thread per frame.
@@ -1528,7 +1540,8 @@ __global__ __launch_bounds__(kTile) void k_post(DemodArgs A, FinalArgs F, int fi
     const unsigned long long f = (unsigned long long)blockIdx.x * kTile + threadIdx.x;
     if (fix) {
         const int st = f < A.frames ? A.meta[f].status : 0;
-        const bool fixup = st == kStatusFixup, recheck = st == kStatusRecheck;
+        const bool fixup = st == kStatusFixup;
+        const bool recheck = st == kStatusRecheck || (A.sentinels && f < A.frames && st == 0 && has_sentinel(A, f));
         if (__syncthreads_or(fixup)) {
             if (threadIdx.x == 0) fcount = 0;
             __syncthreads();
@@ -1545,6 +1558,8 @@ __global__ __launch_bounds__(kTile) void k_post(DemodArgs A, FinalArgs F, int fi
     }
     if (fin && f < A.frames) finalize_frame(F, f);
 }
+
+#include "lphy_cuframe.h"
 
 // ---------------------------------------------------------------------------
 // lora_modulate (LoRaMod.cpp:8-43 + ChirpGenerator.hpp:24-51), bit-exact.
@@ -1741,8 +1756,41 @@ int launch_frames_occ(const DemodArgs& A, hipStream_t st) {
 #ifndef LPHY_FRAMES_OCC  // experiments: -DLPHY_FRAMES_OCC=3
 #define LPHY_FRAMES_OCC 2
 #endif
+// Single-read CU-resident kernel (lphy_cuframe.h) for the frames it takes:
+// SF 7, whole symbols only, 56..70 symbols, 16-byte aligned IQ.  Opt-in
+// (LPHY_F_RESIDENT, or LPHY_CUFRAME=1 for experiments): it is bit-exact
+// (tests/test_gpu_cuframe.py) but its barrier-locked rounds leave the waves
+// waiting, so it is slower than k_frames today.
+inline bool cuframe_enabled(const DemodArgs& A) {
+    static int env = -1;
+    if (env < 0) {
+        const char* e = getenv("LPHY_CUFRAME");
+        env = (e && e[0] == '1') ? 1 : 0;
+    }
+    return A.resident || env == 1;
+}
+template <int SF>
+bool cuframe_fit(const DemodArgs& A) {
+    using C = CuCfg<SF>;
+    const unsigned long long S = A.total_syms;
+    return cuframe_enabled(A) && S >= (unsigned long long)C::SMIN && S <= (unsigned long long)C::SMAX &&
+           A.frame_samples == S * (unsigned long long)C::N && A.est_units == 2 &&
+           (reinterpret_cast<uintptr_t>(A.iq) & 15) == 0;
+}
+template <int SF, int MODE>
+int launch_cuframe(const DemodArgs& A, hipStream_t st) {
+    unsigned long long blocks = (unsigned long long)cu_count();
+    if (blocks > A.frames) blocks = A.frames;
+    hipLaunchKernelGGL((k_cuframe<SF, MODE>), dim3((unsigned)blocks), dim3(CuCfg<SF>::THREADS), 0, st, A);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
 template <int SF, int MODE>
 int launch_frames_mode(const DemodArgs& A, hipStream_t st) {
+    if constexpr (SF == 7) {
+        if (cuframe_fit<SF>(A)) return launch_cuframe<SF, MODE>(A, st);
+    }
     return launch_frames_occ<SF, MODE, LPHY_FRAMES_OCC>(A, st);
 }
 

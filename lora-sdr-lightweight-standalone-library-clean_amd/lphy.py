@@ -30,6 +30,7 @@ F_STAGE_SYMBOLS = 8
 F_STAGE_FINAL = 16
 F_UNFUSED = 32  # separate prologue / symbol launches (lphy_hip.h)
 F_EXACT_ROTATION = 64  # fused launch without the certified per-frame rotation table
+F_RESIDENT = 128  # fused launch: single-read CU-resident kernel where it applies (SF 7)
 WINDOW_NONE = 0
 WINDOW_HANN = 1
 
