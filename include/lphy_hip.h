@@ -200,6 +200,65 @@ const char* lphy_hip_version(void);
  * synchronises the device.  Returns 0 or -EIO. */
 int lphy_hip_recheck_count(lphy_hip_ctx* ctx, unsigned long long* out, int reset);
 
+/* ------------------------------------------------------------------------
+ * Batch forms of the codec helpers of the reference's LoRaCodes.hpp (SURVEY
+ * §8f rank 3) on device buffers; `stream` is a hipStream_t (NULL = default).
+ * Rows are `frames` records `stride` elements apart.  Results equal the
+ * reference helper applied to each row (tests/test_gpu_codes.py).
+ * --------------------------------------------------------------------- */
+enum lphy_whiten_kind {
+    LPHY_WHITEN_SX1232 = 0,      /* SX1232RadioComputeWhitening (LoRaCodes.hpp:111-137) */
+    LPHY_WHITEN_SX1272 = 1,      /* Sx1272ComputeWhitening (LoRaCodes.hpp:147-167)      */
+    LPHY_WHITEN_SX1272_LFSR = 2  /* Sx1272ComputeWhiteningLfsr (LoRaCodes.hpp:176-189)  */
+};
+enum lphy_code_op {
+    LPHY_CODE_ENC84 = 0,   /* encodeHamming84sx (LoRaCodes.hpp:229-242)             */
+    LPHY_CODE_DEC84 = 1,   /* decodeHamming84sx (:250-281); flags bit0 error, bit1 bad */
+    LPHY_CODE_ENC74 = 2,   /* encodeHamming74sx (:287-297)                          */
+    LPHY_CODE_DEC74 = 3,   /* decodeHamming74sx (:306-334); flags bit0 error         */
+    LPHY_CODE_ENCP54 = 4,  /* encodeParity54 (:347-350)                             */
+    LPHY_CODE_CHKP54 = 5,  /* checkParity54 (:340-345); flags bit0 error             */
+    LPHY_CODE_ENCP64 = 6,  /* encodeParity64 (:367-371)                             */
+    LPHY_CODE_CHKP64 = 7   /* checkParity64 (:357-365); flags bit0 error             */
+};
+enum lphy_sum_kind {
+    LPHY_SUM_SX1272_CRC = 0, /* sx1272DataChecksum over `len` bytes (LoRaCodes.hpp:92-105) */
+    LPHY_SUM_HEADER = 1,     /* headerChecksum of the row's first 2 bytes (:43-67)        */
+    LPHY_SUM_CHECKSUM8 = 2   /* checksum8 over `len` bytes (:32-41)                       */
+};
+
+/* binaryToGray16 (to_binary = 0) / grayToBinary16 (1), in place
+ * (LoRaCodes.hpp:201-222). */
+int lphy_hip_gray_batch(uint16_t* d_syms, size_t count, int to_binary, void* stream);
+
+/* diagonalInterleaveSx (LoRaCodes.hpp:376-393) per row: cw_per_frame / ppm
+ * blocks of ppm codewords -> (4 + rdd) symbols each.  -ERANGE when a row's
+ * symbols exceed sym_stride.  1 <= ppm <= 16, rdd <= 4. */
+int lphy_hip_interleave_batch(const uint8_t* d_cw, size_t frames, size_t cw_stride, size_t cw_per_frame,
+                              uint16_t* d_syms, size_t sym_stride, unsigned ppm, unsigned rdd,
+                              void* stream);
+
+/* diagonalDeterleaveSx (LoRaCodes.hpp:396-412) per row: syms_per_frame /
+ * (4 + rdd) blocks -> ppm codewords each, written as the reference leaves a
+ * zero-initialised codeword buffer. */
+int lphy_hip_deinterleave_batch(const uint16_t* d_syms, size_t frames, size_t sym_stride,
+                                size_t syms_per_frame, uint8_t* d_cw, size_t cw_stride, unsigned ppm,
+                                unsigned rdd, void* stream);
+
+/* Whitening / de-whitening of the first `len` bytes of every row in place
+ * (the generators are involutions).  bit_ofs and rdd as the reference's
+ * bitOfs / RDD (ignored by LPHY_WHITEN_SX1232). */
+int lphy_hip_whiten_batch(uint8_t* d_bytes, size_t frames, size_t stride, size_t len, int kind,
+                          int bit_ofs, unsigned rdd, void* stream);
+
+/* Hamming / parity code `op` on `count` bytes in place; the decoders' error
+ * flags go to d_flags[i] when it is not NULL. */
+int lphy_hip_hamming_batch(uint8_t* d_bytes, size_t count, int op, uint8_t* d_flags, void* stream);
+
+/* Checksum `kind` of every row -> d_out[frame] (uint16). */
+int lphy_hip_checksum_batch(const uint8_t* d_bytes, size_t frames, size_t stride, size_t len, int kind,
+                            uint16_t* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

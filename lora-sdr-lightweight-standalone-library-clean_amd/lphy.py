@@ -62,7 +62,14 @@ EXPORTS = (
     "lphy_hip_compensate", "lphy_hip_modulate_batch", "lphy_hip_demod_host",
     "lphy_hip_decode_host", "lphy_hip_estimate_host", "lphy_hip_compensate_host",
     "lphy_hip_modulate_host", "lphy_hip_demod_stream", "lphy_hip_sync", "lphy_hip_version",
+    "lphy_hip_gray_batch", "lphy_hip_interleave_batch", "lphy_hip_deinterleave_batch",
+    "lphy_hip_whiten_batch", "lphy_hip_hamming_batch", "lphy_hip_checksum_batch",
 )
+
+WHITEN_SX1232, WHITEN_SX1272, WHITEN_SX1272_LFSR = 0, 1, 2
+CODE_ENC84, CODE_DEC84, CODE_ENC74, CODE_DEC74 = 0, 1, 2, 3
+CODE_ENCP54, CODE_CHKP54, CODE_ENCP64, CODE_CHKP64 = 4, 5, 6, 7
+SUM_SX1272_CRC, SUM_HEADER, SUM_CHECKSUM8 = 0, 1, 2
 
 _LIB = None
 
@@ -111,6 +118,12 @@ def load(path: Path = HIP_SO) -> C.CDLL:
     L.lphy_hip_sync.argtypes = [_vp]
     L.lphy_hip_recheck_count.argtypes = [_vp, C.POINTER(C.c_ulonglong), C.c_int]
     L.lphy_hip_version.restype = C.c_char_p
+    L.lphy_hip_gray_batch.argtypes = [_vp, _sz, C.c_int, _vp]
+    L.lphy_hip_interleave_batch.argtypes = [_vp, _sz, _sz, _sz, _vp, _sz, C.c_uint, C.c_uint, _vp]
+    L.lphy_hip_deinterleave_batch.argtypes = [_vp, _sz, _sz, _sz, _vp, _sz, C.c_uint, C.c_uint, _vp]
+    L.lphy_hip_whiten_batch.argtypes = [_vp, _sz, _sz, _sz, C.c_int, C.c_int, C.c_uint, _vp]
+    L.lphy_hip_hamming_batch.argtypes = [_vp, _sz, C.c_int, _vp, _vp]
+    L.lphy_hip_checksum_batch.argtypes = [_vp, _sz, _sz, _sz, C.c_int, _vp, _vp]
     _LIB = L
     return L
 
@@ -302,3 +315,43 @@ def encode_payloads(payloads: np.ndarray) -> np.ndarray:
     out[..., 0::2] = t[p >> 4]
     out[..., 1::2] = t[p & 0x0F]
     return out
+
+
+# --- LoRaCodes.hpp batch kernels (device tensors) -------
+def _dptr(t, name, nbytes, itemsize):
+    return _dev_buf(t, name, t.device.index or 0, nbytes, itemsize)
+
+
+def gray_batch(syms, to_binary: bool, stream=None):
+    """binaryToGray16 / grayToBinary16 in place on a uint16 (int16) tensor."""
+    n = syms.numel()
+    _chk(load().lphy_hip_gray_batch(_dptr(syms, "syms", n * 2, 2), n, int(to_binary), stream),
+         "lphy_hip_gray_batch")
+
+
+def interleave_batch(cw, frames, cw_stride, cw_per_frame, syms, sym_stride, ppm, rdd, stream=None):
+    _chk(load().lphy_hip_interleave_batch(_dptr(cw, "cw", frames * cw_stride, 1), frames, cw_stride,
+                                          cw_per_frame, _dptr(syms, "syms", frames * sym_stride * 2, 2),
+                                          sym_stride, ppm, rdd, stream), "lphy_hip_interleave_batch")
+
+
+def deinterleave_batch(syms, frames, sym_stride, syms_per_frame, cw, cw_stride, ppm, rdd, stream=None):
+    _chk(load().lphy_hip_deinterleave_batch(_dptr(syms, "syms", frames * sym_stride * 2, 2), frames,
+                                            sym_stride, syms_per_frame, _dptr(cw, "cw", frames * cw_stride, 1),
+                                            cw_stride, ppm, rdd, stream), "lphy_hip_deinterleave_batch")
+
+
+def whiten_batch(buf, frames, stride, length, kind, bit_ofs=0, rdd=4, stream=None):
+    _chk(load().lphy_hip_whiten_batch(_dptr(buf, "buf", frames * stride, 1), frames, stride, length, kind,
+                                      bit_ofs, rdd, stream), "lphy_hip_whiten_batch")
+
+
+def hamming_batch(buf, op, flags=None, stream=None):
+    n = buf.numel()
+    pf = _dptr(flags, "flags", n, 1) if flags is not None else None
+    _chk(load().lphy_hip_hamming_batch(_dptr(buf, "buf", n, 1), n, op, pf, stream), "lphy_hip_hamming_batch")
+
+
+def checksum_batch(buf, frames, stride, length, kind, out, stream=None):
+    _chk(load().lphy_hip_checksum_batch(_dptr(buf, "buf", frames * stride, 1), frames, stride, length, kind,
+                                        _dptr(out, "out", frames * 2, 2), stream), "lphy_hip_checksum_batch")

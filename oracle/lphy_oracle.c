@@ -611,6 +611,141 @@ ssize_t orc_demodulate(unsigned sf, unsigned bw_hz, unsigned osr, int hann,
 }
 
 /* ---------------------------------------------------------------------- */
+/* LoRaCodes.hpp codec helpers                          */
+/* ---------------------------------------------------------------------- */
+static unsigned orc_par(unsigned v) {
+    unsigned p = 0;
+    while (v) { p ^= v & 1u; v >>= 1; }
+    return p;
+}
+
+uint16_t orc_gray(uint16_t v, int to_binary) {
+    /* LoRaCodes.hpp:201-207 num ^ (num >> 1); :212-222 prefix XOR by 8,4,2,1 */
+    unsigned x = v;
+    if (!to_binary) return (uint16_t)(x ^ (x >> 1));
+    x ^= x >> 8; x ^= x >> 4; x ^= x >> 2; x ^= x >> 1;
+    return (uint16_t)x;
+}
+
+void orc_interleave(const uint8_t* cw, size_t ncw, uint16_t* syms, size_t ppm, size_t rdd) {
+    /* LoRaCodes.hpp:376-393 */
+    for (size_t blk = 0; blk < ncw / ppm; ++blk)
+        for (size_t bit = 0; bit < 4 + rdd; ++bit) {
+            unsigned s = 0;
+            for (size_t c = 0; c < ppm; ++c)
+                s |= (unsigned)((cw[blk * ppm + (c + bit) % ppm] >> bit) & 1u) << c;
+            syms[blk * (4 + rdd) + bit] = (uint16_t)s;
+        }
+}
+
+void orc_deinterleave(const uint16_t* syms, size_t nsyms, uint8_t* cw, size_t ppm, size_t rdd) {
+    /* LoRaCodes.hpp:396-412 (ORs into cw, zeroed by the caller) */
+    for (size_t blk = 0; blk < nsyms / (4 + rdd); ++blk)
+        for (size_t bit = 0; bit < 4 + rdd; ++bit) {
+            unsigned s = syms[blk * (4 + rdd) + bit];
+            for (size_t c = 0; c < ppm; ++c, s >>= 1)
+                cw[blk * ppm + (c + bit) % ppm] |= (uint8_t)((s & 1u) << bit);
+        }
+}
+
+static uint64_t orc_lfsr64(uint64_t r) {
+    return (r >> 8) | (((r >> 32) ^ (r >> 24) ^ (r >> 16) ^ r) << 56); /* poly 0x1D */
+}
+
+void orc_whiten(uint8_t* buf, size_t len, int kind, int bit_ofs, unsigned rdd) {
+    if (kind == 0) { /* SX1232RadioComputeWhitening, LoRaCodes.hpp:111-137 */
+        unsigned msb = 0x01, lsb = 0xFF;
+        for (size_t j = 0; j < len; ++j) {
+            buf[j] ^= (uint8_t)lsb;
+            for (int i = 0; i < 8; ++i) {
+                unsigned prev = msb;
+                msb = (lsb & 1u) ^ ((lsb >> 5) & 1u);
+                lsb = ((lsb >> 1) & 0xFFu) | ((prev << 7) & 0x80u);
+            }
+        }
+    } else if (kind == 1) { /* Sx1272ComputeWhitening, :147-167 */
+        static const int ofs0[8] = {6, 4, 2, 0, -112, -114, -302, -34};
+        static const int ofs1[5] = {6, 4, 2, 0, -360};
+        static const uint64_t seq[8] = {
+            0x0102291EA751AAFFull, 0xD24B050A8D643A17ull, 0x5B279B671120B8F4ull, 0x032B37B9F6FB55A2ull,
+            0x994E0F87E95E2D16ull, 0x7CBCFC7631984C26ull, 0x281C8E4F0DAEF7F9ull, 0x1741886EB7733B15ull};
+        const int* ofs = rdd == 1 ? ofs1 : ofs0;
+        for (size_t j = 0; j < len; ++j) {
+            uint8_t x = 0;
+            for (unsigned i = 0; i < 4 + rdd; ++i) {
+                int t = (ofs[i] + (int)j + bit_ofs + 510) % 510;
+                if (seq[t >> 6] & ((uint64_t)1 << (t & 0x3F))) x |= (uint8_t)(1u << i);
+            }
+            buf[j] ^= x;
+        }
+    } else { /* Sx1272ComputeWhiteningLfsr, :176-189 */
+        const uint64_t s1[2] = {0x6572D100E85C2EFFull, 0xE85C2EFFFFFFFFFFull};
+        const uint64_t s2[2] = {0x05121100F8ECFEEFull, 0xF8ECFEEFEFEFEFEFull};
+        const uint8_t m = (uint8_t)(0xffu >> (4 - rdd));
+        uint64_t r[2] = {rdd == 1 ? s2[0] : s1[0], rdd == 1 ? s2[1] : s1[1]};
+        int i;
+        for (i = 0; i < bit_ofs; ++i) r[i & 1] = orc_lfsr64(r[i & 1]);
+        for (size_t j = 0; j < len; ++j, ++i) {
+            buf[j] ^= (uint8_t)(r[i & 1] & m);
+            r[i & 1] = orc_lfsr64(r[i & 1]);
+        }
+    }
+}
+
+uint8_t orc_hamming(uint8_t b, int op, uint8_t* flags) {
+    /* LoRaCodes.hpp:229-371 */
+    unsigned x = b, fl = 0, out;
+    switch (op) {
+        case 0: return orc_encode_hamming84(b);
+        case 1: {
+            unsigned syn = orc_par(x & 0x17) | (orc_par(x & 0x2E) << 1) | (orc_par(x & 0x4B) << 2) |
+                           (orc_par(x & 0x8D) << 3);
+            unsigned flip = 0;
+            if (syn) fl |= 1;
+            if (syn == 0xD) flip = 1;
+            else if (syn == 0x7) flip = 2;
+            else if (syn == 0xB) flip = 4;
+            else if (syn == 0xE) flip = 8;
+            else if (syn != 0 && syn != 1 && syn != 2 && syn != 4 && syn != 8) fl |= 2;
+            out = (x ^ flip) & 0xF;
+            break;
+        }
+        case 2: out = (x & 0xF) | (orc_par(x & 0x7) << 4) | (orc_par(x & 0xE) << 5) | (orc_par(x & 0xB) << 6); break;
+        case 3: {
+            unsigned syn = orc_par(x & 0x17) | (orc_par(x & 0x2E) << 1) | (orc_par(x & 0x4B) << 2);
+            unsigned flip = syn == 0x5 ? 1 : syn == 0x7 ? 2 : syn == 0x3 ? 4 : syn == 0x6 ? 8 : 0;
+            if (syn) fl |= 1;
+            out = (x ^ flip) & 0xF;
+            break;
+        }
+        case 4: out = (x & 0xF) | (orc_par(x & 0xF) << 4); break;
+        case 5: if (orc_par(x & 0x1F)) fl |= 1; out = x & 0xF; break;
+        case 6: out = (orc_par(x & 0x7) << 4) | (orc_par(x & 0xE) << 5) | (x & 0xF); break;
+        default: if (orc_par(x & 0x17) | orc_par(x & 0x2E)) fl |= 1; out = x & 0xF; break;
+    }
+    if (flags) *flags = (uint8_t)fl;
+    return (uint8_t)out;
+}
+
+uint16_t orc_checksum(const uint8_t* buf, size_t len, int kind) {
+    if (kind == 0) return orc_sx1272_checksum(buf, (int)len); /* :92-105 */
+    if (kind == 1) {                                         /* :43-67 */
+        const unsigned a0 = (buf[0] >> 4) & 1, a1 = (buf[0] >> 5) & 1, a2 = (buf[0] >> 6) & 1, a3 = (buf[0] >> 7) & 1;
+        const unsigned b0 = buf[0] & 1, b1 = (buf[0] >> 1) & 1, b2 = (buf[0] >> 2) & 1, b3 = (buf[0] >> 3) & 1;
+        const unsigned c0 = buf[1] & 1, c1 = (buf[1] >> 1) & 1, c2 = (buf[1] >> 2) & 1, c3 = (buf[1] >> 3) & 1;
+        return (uint16_t)(((a0 ^ a1 ^ a2 ^ a3) << 4) | ((a3 ^ b1 ^ b2 ^ b3 ^ c0) << 3) |
+                          ((a2 ^ b0 ^ b3 ^ c1 ^ c3) << 2) | ((a1 ^ b0 ^ b2 ^ c0 ^ c1 ^ c2) << 1) |
+                          (a0 ^ b1 ^ c0 ^ c1 ^ c2 ^ c3));
+    }
+    uint8_t acc = 0; /* checksum8, :32-41 */
+    for (size_t i = 0; i < len; ++i) {
+        acc = (uint8_t)((acc >> 1) + ((acc & 1u) << 7));
+        acc = (uint8_t)(acc + buf[i]);
+    }
+    return acc;
+}
+
+/* ---------------------------------------------------------------------- */
 /* phy.cpp:150-180: rotate by e^{j rate n}, then shift by round(time_offset) */
 /* ---------------------------------------------------------------------- */
 void orc_compensate_offsets(unsigned sf, unsigned osr, float cfo,

@@ -78,6 +78,18 @@ void orc_compensate_offsets(unsigned sf, unsigned osr, float cfo,
 ssize_t orc_decode(const uint16_t* syms, size_t n, uint8_t* out, size_t cap,
                    uint8_t* crc_out);
 
+/* LoRaCodes.hpp helpers, restated for the GPU batch
+ * kernels' parity tests.  kind / op numbering as include/lphy_hip.h. */
+uint16_t orc_gray(uint16_t v, int to_binary);                         /* :201-222 */
+void orc_interleave(const uint8_t* cw, size_t ncw, uint16_t* syms,
+                    size_t ppm, size_t rdd);                          /* :376-393 */
+void orc_deinterleave(const uint16_t* syms, size_t nsyms, uint8_t* cw,
+                      size_t ppm, size_t rdd);                        /* :396-412 */
+void orc_whiten(uint8_t* buf, size_t len, int kind, int bit_ofs,
+                unsigned rdd);                                        /* :111-189 */
+uint8_t orc_hamming(uint8_t x, int op, uint8_t* flags);               /* :229-371 */
+uint16_t orc_checksum(const uint8_t* buf, size_t len, int kind);      /* :32-105  */
+
 /* Multi-threaded timing harness for bench.py's cpu_baseline ("port" kind):
  * mode 1 = dechirp + lora_demodulate + lora_decode per frame,
  * mode 0 = demodulate + decode.  Returns wall seconds. */

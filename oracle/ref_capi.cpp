@@ -110,6 +110,41 @@ uint8_t ref_decode_hamming84(uint8_t b) {
     return decodeHamming84sx(b, e, bad);
 }
 
+// LoRaCodes.hpp helpers, forwarded one to one.
+uint16_t ref_gray(uint16_t v, int to_binary) { return to_binary ? grayToBinary16(v) : binaryToGray16(v); }
+void ref_interleave(const uint8_t* cw, size_t ncw, uint16_t* syms, size_t ppm, size_t rdd) {
+    diagonalInterleaveSx(cw, ncw, syms, ppm, rdd);
+}
+void ref_deinterleave(const uint16_t* syms, size_t nsyms, uint8_t* cw, size_t ppm, size_t rdd) {
+    diagonalDeterleaveSx(syms, nsyms, cw, ppm, rdd);
+}
+void ref_whiten(uint8_t* buf, size_t len, int kind, int bit_ofs, unsigned rdd) {
+    if (kind == 0) SX1232RadioComputeWhitening(buf, (uint16_t)len);
+    else if (kind == 1) Sx1272ComputeWhitening(buf, (uint16_t)len, bit_ofs, (int)rdd);
+    else Sx1272ComputeWhiteningLfsr(buf, (uint16_t)len, bit_ofs, rdd);
+}
+uint8_t ref_hamming(uint8_t x, int op, uint8_t* flags) {
+    bool e = false, b = false;
+    uint8_t out;
+    switch (op) {
+        case 0: out = encodeHamming84sx(x); break;
+        case 1: out = decodeHamming84sx(x, e, b); break;
+        case 2: out = encodeHamming74sx(x); break;
+        case 3: out = decodeHamming74sx(x, e); break;
+        case 4: out = encodeParity54(x); break;
+        case 5: out = checkParity54(x, e); break;
+        case 6: out = encodeParity64(x); break;
+        default: out = checkParity64(x, e); break;
+    }
+    if (flags) *flags = (uint8_t)((e ? 1 : 0) | (b ? 2 : 0));
+    return out;
+}
+uint16_t ref_checksum(const uint8_t* buf, size_t len, int kind) {
+    if (kind == 0) return sx1272DataChecksum(buf, (int)len);
+    if (kind == 1) return headerChecksum(buf);
+    return checksum8(buf, len);
+}
+
 // LoRaDemod.cpp:11-197 (init + demodulate + free).  metrics_out gets
 // {cfo, time_offset} as stored in ws->metrics.
 ssize_t ref_lora_demodulate(unsigned sf, int window, const float* samples,

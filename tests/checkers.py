@@ -44,6 +44,8 @@ def build_oracle() -> None:
 
 
 class Oracle:
+    _p = "orc_"
+
     def __init__(self, path: Path = ORACLE_SO):
         if not path.exists():
             build_oracle()
@@ -79,9 +81,49 @@ class Oracle:
         L.orc_decode.restype = C.c_ssize_t
         L.orc_compensate_offsets.argtypes = [C.c_uint, C.c_uint, C.c_float, C.c_float,
                                              _f32p, C.c_size_t]
+        L.orc_gray.argtypes = [C.c_uint16, C.c_int]
+        L.orc_gray.restype = C.c_uint16
+        L.orc_interleave.argtypes = [_u8p, C.c_size_t, _u16p, C.c_size_t, C.c_size_t]
+        L.orc_deinterleave.argtypes = [_u16p, C.c_size_t, _u8p, C.c_size_t, C.c_size_t]
+        L.orc_whiten.argtypes = [_u8p, C.c_size_t, C.c_int, C.c_int, C.c_uint]
+        L.orc_hamming.argtypes = [C.c_uint8, C.c_int, _u8p]
+        L.orc_hamming.restype = C.c_uint8
+        L.orc_checksum.argtypes = [_u8p, C.c_size_t, C.c_int]
+        L.orc_checksum.restype = C.c_uint16
         L.orc_bench.argtypes = [C.c_int, C.c_uint, C.c_uint, _f32p, C.c_size_t,
                                 C.c_size_t, _u8p, C.c_int]
         L.orc_bench.restype = C.c_double
+
+
+    # --- LoRaCodes.hpp helpers -------------------------
+    def gray(self, v, to_binary):
+        return getattr(self.lib, self._p + "gray")(int(v), int(to_binary))
+
+    def interleave(self, cw, ppm, rdd):
+        cw = np.ascontiguousarray(cw, np.uint8)
+        out = np.zeros(max((len(cw) // ppm) * (4 + rdd), 1), np.uint16)
+        getattr(self.lib, self._p + "interleave")(_p(cw, _u8p), len(cw), _p(out, _u16p), ppm, rdd)
+        return out[: (len(cw) // ppm) * (4 + rdd)]
+
+    def deinterleave(self, syms, ppm, rdd):
+        syms = np.ascontiguousarray(syms, np.uint16)
+        out = np.zeros(max((len(syms) // (4 + rdd)) * ppm, 1), np.uint8)
+        getattr(self.lib, self._p + "deinterleave")(_p(syms, _u16p), len(syms), _p(out, _u8p), ppm, rdd)
+        return out[: (len(syms) // (4 + rdd)) * ppm]
+
+    def whiten(self, buf, kind, bit_ofs=0, rdd=4):
+        b = np.array(buf, np.uint8, copy=True)
+        getattr(self.lib, self._p + "whiten")(_p(b, _u8p), len(b), kind, bit_ofs, rdd)
+        return b
+
+    def hamming(self, x, op):
+        fl = np.zeros(1, np.uint8)
+        out = getattr(self.lib, self._p + "hamming")(int(x), op, _p(fl, _u8p))
+        return int(out), int(fl[0])
+
+    def checksum(self, buf, kind):
+        b = np.ascontiguousarray(np.frombuffer(bytes(buf), np.uint8)) if not isinstance(buf, np.ndarray) else np.ascontiguousarray(buf, np.uint8)
+        return getattr(self.lib, self._p + "checksum")(_p(b, _u8p), len(b), kind)
 
     # --- producers -----------------------------------------------------
     def genchirp(self, N, osr, NN, f0, down, ampl, phase, bw_scale):
@@ -172,7 +214,7 @@ class Oracle:
         r = self.lib.orc_lora_decode(_p(syms, _u16p), len(syms), _p(out, _u8p))
         return r, out[: max(r, 0)]
 
-    def checksum(self, data):
+    def sx_checksum(self, data):
         d = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8))
         return self.lib.orc_sx1272_checksum(_p(d, _u8p), len(d))
 
@@ -187,6 +229,7 @@ class Oracle:
 
 class Reference:
     """The reference library (oracle/_ref), when it has been built."""
+    _p = "ref_"
 
     def __init__(self, path: Path = REF_SO):
         if not path.exists():
@@ -224,10 +267,50 @@ class Reference:
         L.ref_decode.restype = C.c_ssize_t
         L.ref_compensate_offsets.argtypes = [C.c_uint, C.c_uint, C.c_float, C.c_float,
                                              _f32p, C.c_size_t]
+        L.ref_gray.argtypes = [C.c_uint16, C.c_int]
+        L.ref_gray.restype = C.c_uint16
+        L.ref_interleave.argtypes = [_u8p, C.c_size_t, _u16p, C.c_size_t, C.c_size_t]
+        L.ref_deinterleave.argtypes = [_u16p, C.c_size_t, _u8p, C.c_size_t, C.c_size_t]
+        L.ref_whiten.argtypes = [_u8p, C.c_size_t, C.c_int, C.c_int, C.c_uint]
+        L.ref_hamming.argtypes = [C.c_uint8, C.c_int, _u8p]
+        L.ref_hamming.restype = C.c_uint8
+        L.ref_checksum.argtypes = [_u8p, C.c_size_t, C.c_int]
+        L.ref_checksum.restype = C.c_uint16
         for n in ("ref_bench_modeA", "ref_bench_modeB"):
             getattr(L, n).argtypes = [C.c_uint, C.c_uint, _f32p, C.c_size_t,
                                       C.c_size_t, _u8p, C.c_int]
             getattr(L, n).restype = C.c_double
+
+
+    # --- LoRaCodes.hpp helpers -------------------------
+    def gray(self, v, to_binary):
+        return getattr(self.lib, self._p + "gray")(int(v), int(to_binary))
+
+    def interleave(self, cw, ppm, rdd):
+        cw = np.ascontiguousarray(cw, np.uint8)
+        out = np.zeros(max((len(cw) // ppm) * (4 + rdd), 1), np.uint16)
+        getattr(self.lib, self._p + "interleave")(_p(cw, _u8p), len(cw), _p(out, _u16p), ppm, rdd)
+        return out[: (len(cw) // ppm) * (4 + rdd)]
+
+    def deinterleave(self, syms, ppm, rdd):
+        syms = np.ascontiguousarray(syms, np.uint16)
+        out = np.zeros(max((len(syms) // (4 + rdd)) * ppm, 1), np.uint8)
+        getattr(self.lib, self._p + "deinterleave")(_p(syms, _u16p), len(syms), _p(out, _u8p), ppm, rdd)
+        return out[: (len(syms) // (4 + rdd)) * ppm]
+
+    def whiten(self, buf, kind, bit_ofs=0, rdd=4):
+        b = np.array(buf, np.uint8, copy=True)
+        getattr(self.lib, self._p + "whiten")(_p(b, _u8p), len(b), kind, bit_ofs, rdd)
+        return b
+
+    def hamming(self, x, op):
+        fl = np.zeros(1, np.uint8)
+        out = getattr(self.lib, self._p + "hamming")(int(x), op, _p(fl, _u8p))
+        return int(out), int(fl[0])
+
+    def checksum(self, buf, kind):
+        b = np.ascontiguousarray(np.frombuffer(bytes(buf), np.uint8)) if not isinstance(buf, np.ndarray) else np.ascontiguousarray(buf, np.uint8)
+        return getattr(self.lib, self._p + "checksum")(_p(b, _u8p), len(b), kind)
 
     def fft(self, x):
         x = _cf(np.asarray(x, np.complex64))

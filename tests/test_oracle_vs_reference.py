@@ -244,3 +244,42 @@ def test_compensate_offsets_bit_exact(oracle, reference, sf, osr, cfo, toff):
     x[3] = complex(np.inf, 0.5)  # Annex G product inside the rotation
     _nan_bits_equal(oracle.compensate_offsets(x, sf, cfo, toff, osr).view(np.float32),
                     reference.compensate_offsets(x, sf, cfo, toff, osr).view(np.float32))
+
+
+# ---- LoRaCodes.hpp helpers: oracle vs the reference header
+def test_codes_gray_and_hamming_exhaustive(oracle, reference):
+    for v in range(0, 65536, 7):
+        for tb in (0, 1):
+            assert oracle.gray(v, tb) == reference.gray(v, tb)
+    for x in range(256):
+        for op in range(8):
+            assert oracle.hamming(x, op) == reference.hamming(x, op), (x, op)
+
+
+@pytest.mark.parametrize("ppm,rdd", [(p, r) for p in (5, 7, 8, 10, 12) for r in (0, 1, 2, 4)])
+def test_codes_interleaver(oracle, reference, ppm, rdd):
+    rng = np.random.default_rng(ppm * 10 + rdd)
+    cw = rng.integers(0, 1 << (4 + rdd), 3 * ppm + 2, dtype=np.uint8)
+    a, b = oracle.interleave(cw, ppm, rdd), reference.interleave(cw, ppm, rdd)
+    np.testing.assert_array_equal(a, b)
+    syms = rng.integers(0, 1 << ppm, 3 * (4 + rdd) + 1, dtype=np.uint16)
+    np.testing.assert_array_equal(oracle.deinterleave(syms, ppm, rdd), reference.deinterleave(syms, ppm, rdd))
+    # round trip of whole blocks
+    np.testing.assert_array_equal(oracle.deinterleave(a, ppm, rdd), cw[: len(a) // (4 + rdd) * ppm])
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_codes_whitening_and_checksums(oracle, reference, kind):
+    rng = np.random.default_rng(40 + kind)
+    for rdd in (0, 1, 2, 3, 4):
+        for bit_ofs in (0, 1, 7, 100):
+            buf = rng.integers(0, 256, 255, dtype=np.uint8)
+            np.testing.assert_array_equal(oracle.whiten(buf, kind, bit_ofs, rdd),
+                                          reference.whiten(buf, kind, bit_ofs, rdd))
+    for n in (0, 1, 2, 5, 64, 255):
+        buf = rng.integers(0, 256, max(n, 2), dtype=np.uint8)[: max(n, 2)]
+        assert oracle.checksum(buf[:n] if kind != 1 else buf, kind) == \
+            reference.checksum(buf[:n] if kind != 1 else buf, kind)
+    # whitening_test.cpp:30-31 known answer
+    w = oracle.whiten(np.frombuffer(bytes.fromhex("DEADBEEF700D"), np.uint8), 2, 0, 4)
+    assert w.tobytes() == bytes.fromhex("215290102CF2")
