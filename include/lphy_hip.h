@@ -259,6 +259,69 @@ int lphy_hip_hamming_batch(uint8_t* d_bytes, size_t count, int op, uint8_t* d_fl
 int lphy_hip_checksum_batch(const uint8_t* d_bytes, size_t frames, size_t stride, size_t len, int kind,
                             uint16_t* d_out, void* stream);
 
+/* lora_encode (LoRaEncoder.cpp:6-18) per row: byte j of the first `len`
+ * bytes -> symbols 2j, 2j+1 (encodeHamming84sx of the high, low nibble),
+ * the symbols modulate_batch takes.  -ERANGE when 2*len > sym_stride. */
+int lphy_hip_lora_encode_batch(const uint8_t* d_bytes, size_t frames, size_t stride, size_t len,
+                               uint16_t* d_syms, size_t sym_stride, void* stream);
+
+/* ------------------------------------------------------------------------
+ * LoRaWAN MAC helpers batched: lorawan::compute_mic
+ * (lorawan.cpp:35-98, AES-128 CMAC over B0 || data) and parse_frame's
+ * checks (lorawan.cpp:150-176) on the decoded bytes of many frames at once.
+ * Keys are 16-byte records in device memory (d_keys, 4-byte aligned).
+ * --------------------------------------------------------------------- */
+typedef struct lphy_lorawan_desc { /* one MIC job */
+    uint64_t offset;   /* byte offset of the frame's MHDR..FRMPayload in d_bytes */
+    uint32_t len;      /* bytes the MIC covers (compute_mic's len)            */
+    uint32_t devaddr;
+    uint32_t fcnt;     /* 32-bit frame counter as compute_mic takes it        */
+    uint32_t key;      /* index into d_keys                                   */
+    uint32_t uplink;   /* nonzero: uplink (B0 byte 5 = 0)                     */
+    uint32_t reserved;
+} lphy_lorawan_desc;
+
+typedef struct lphy_lorawan_frame { /* parse_frame's outcome for one row */
+    int32_t  status;          /* parse_frame's return: FRMPayload length, or
+                                 -EINVAL (MIC mismatch) / -ERANGE (short frame,
+                                 FOpts past the MIC); -ENOKEY: key index
+                                 >= nkeys (not a reference outcome)          */
+    uint32_t devaddr;
+    uint32_t mic;             /* MIC the frame carries (last 4 bytes)         */
+    uint32_t calc_mic;        /* MIC computed over the rest                   */
+    uint32_t payload_offset;  /* FRMPayload's offset in the row (status >= 0) */
+    uint32_t payload_len;
+    uint16_t fcnt;
+    uint8_t  mhdr;            /* MType = mhdr >> 5, Major = mhdr & 3          */
+    uint8_t  fctrl;           /* FOpts (at offset 8) length = fctrl & 0x0F    */
+    uint8_t  fopts_len;
+    uint8_t  reserved[3];
+} lphy_lorawan_frame;         /* 32 bytes; all-zero but status when len < 12 */
+
+#define LPHY_LW_APPEND 1u  /* mic_batch: also store the 4 MIC bytes (little
+                              endian) right after each frame's data, as
+                              build_frame does (lorawan.cpp:131-134) */
+
+/* compute_mic for every descriptor -> d_mic[i] (NULL allowed with
+ * LPHY_LW_APPEND).  d_bytes is written only with LPHY_LW_APPEND.  A
+ * descriptor naming a key >= nkeys gets MIC 0 and nothing appended. */
+int lphy_hip_lorawan_mic_batch(uint8_t* d_bytes, const lphy_lorawan_desc* d_desc, size_t frames,
+                               const uint8_t* d_keys, size_t nkeys, uint32_t* d_mic, unsigned flags,
+                               void* stream);
+
+/* parse_frame's checks on `frames` rows of decoded bytes `stride` apart
+ * (e.g. demod_batch's d_bytes): row i holds d_lens[i] bytes (d_lens NULL:
+ * `len` each) and uses key d_key_index[i] (NULL: key 0).  Results in
+ * d_out[i].  Lengths up to 65535 bytes. */
+int lphy_hip_lorawan_parse_batch(const uint8_t* d_bytes, size_t frames, size_t stride,
+                                 const uint32_t* d_lens, size_t len, const uint8_t* d_keys, size_t nkeys,
+                                 const uint32_t* d_key_index, lphy_lorawan_frame* d_out, void* stream);
+
+/* One compute_mic through the batch kernel, host buffers (device `device`);
+ * serialised process-wide.  Returns 0, -EINVAL, -ENODEV or -EIO. */
+int lphy_hip_lorawan_mic_host(int device, const uint8_t key[16], int uplink, uint32_t devaddr, uint32_t fcnt,
+                              const uint8_t* data, size_t len, uint32_t* mic);
+
 #ifdef __cplusplus
 }
 #endif

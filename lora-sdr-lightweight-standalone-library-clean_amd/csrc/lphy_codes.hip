@@ -258,9 +258,39 @@ __global__ void k_checksum(const uint8_t* b, unsigned long long stride, unsigned
     out[f] = (uint16_t)r;
 }
 
+// lora_encode (LoRaEncoder.cpp:6-18): one thread per byte, two Hamming(8,4)
+// codewords out, high nibble first.
+__device__ __forceinline__ unsigned enc84(unsigned x) {
+    return (x & 0xF) | (par(x & 0x7) << 4) | (par(x & 0xE) << 5) | (par(x & 0xB) << 6) | (par(x & 0xD) << 7);
+}
+
+__global__ void k_lora_encode(const uint8_t* b, unsigned long long stride, unsigned long long frames, unsigned len,
+                              uint16_t* sy, unsigned long long sy_stride) {
+    const unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= frames * len) return;
+    const unsigned long long f = t / len;
+    const unsigned j = (unsigned)(t - f * len);
+    const unsigned x = b[f * stride + j];
+    uint16_t* o = sy + f * sy_stride + 2ull * j;
+    o[0] = (uint16_t)enc84(x >> 4);
+    o[1] = (uint16_t)enc84(x & 0xF);
+}
+
 }  // namespace
 
 extern "C" {
+
+int lphy_hip_lora_encode_batch(const uint8_t* d_bytes, size_t frames, size_t stride, size_t len,
+                               uint16_t* d_syms, size_t sym_stride, void* stream) {
+    if (len > stride || len > 0x7fffffff || (frames && len && (!d_bytes || !d_syms))) return -EINVAL;
+    if (2 * len > sym_stride) return -ERANGE;
+    if (!frames || !len) return 0;
+    hipLaunchKernelGGL(k_lora_encode, dim3(blocks_for(frames * len)), dim3(kThreads), 0, (hipStream_t)stream,
+                       d_bytes, (unsigned long long)stride, (unsigned long long)frames, (unsigned)len, d_syms,
+                       (unsigned long long)sym_stride);
+    CODES_OK(hipGetLastError());
+    return 0;
+}
 
 int lphy_hip_gray_batch(uint16_t* d_syms, size_t count, int to_binary, void* stream) {
     if (!d_syms && count) return -EINVAL;

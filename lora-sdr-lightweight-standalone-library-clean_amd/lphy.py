@@ -64,6 +64,8 @@ EXPORTS = (
     "lphy_hip_modulate_host", "lphy_hip_demod_stream", "lphy_hip_sync", "lphy_hip_version",
     "lphy_hip_gray_batch", "lphy_hip_interleave_batch", "lphy_hip_deinterleave_batch",
     "lphy_hip_whiten_batch", "lphy_hip_hamming_batch", "lphy_hip_checksum_batch",
+    "lphy_hip_lora_encode_batch", "lphy_hip_lorawan_mic_batch", "lphy_hip_lorawan_parse_batch",
+    "lphy_hip_lorawan_mic_host",
 )
 
 WHITEN_SX1232, WHITEN_SX1272, WHITEN_SX1272_LFSR = 0, 1, 2
@@ -124,6 +126,11 @@ def load(path: Path = HIP_SO) -> C.CDLL:
     L.lphy_hip_whiten_batch.argtypes = [_vp, _sz, _sz, _sz, C.c_int, C.c_int, C.c_uint, _vp]
     L.lphy_hip_hamming_batch.argtypes = [_vp, _sz, C.c_int, _vp, _vp]
     L.lphy_hip_checksum_batch.argtypes = [_vp, _sz, _sz, _sz, C.c_int, _vp, _vp]
+    L.lphy_hip_lora_encode_batch.argtypes = [_vp, _sz, _sz, _sz, _vp, _sz, _vp]
+    L.lphy_hip_lorawan_mic_batch.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp, C.c_uint, _vp]
+    L.lphy_hip_lorawan_parse_batch.argtypes = [_vp, _sz, _sz, _vp, _sz, _vp, _sz, _vp, _vp, _vp]
+    L.lphy_hip_lorawan_mic_host.argtypes = [C.c_int, _vp, C.c_int, C.c_uint32, C.c_uint32, _vp, _sz,
+                                            C.POINTER(C.c_uint32)]
     _LIB = L
     return L
 
@@ -318,7 +325,7 @@ def encode_payloads(payloads: np.ndarray) -> np.ndarray:
 
 
 # --- LoRaCodes.hpp batch kernels (device tensors) -------
-def _dptr(t, name, nbytes, itemsize):
+def _dptr(t, name, nbytes, itemsize=None):
     return _dev_buf(t, name, t.device.index or 0, nbytes, itemsize)
 
 
@@ -355,3 +362,55 @@ def hamming_batch(buf, op, flags=None, stream=None):
 def checksum_batch(buf, frames, stride, length, kind, out, stream=None):
     _chk(load().lphy_hip_checksum_batch(_dptr(buf, "buf", frames * stride, 1), frames, stride, length, kind,
                                         _dptr(out, "out", frames * 2, 2), stream), "lphy_hip_checksum_batch")
+
+
+def lora_encode_batch(data, frames, stride, length, syms, sym_stride, stream=None):
+    """lora_encode (LoRaEncoder.cpp:6-18) per row on device tensors."""
+    _chk(load().lphy_hip_lora_encode_batch(_dptr(data, "data", frames * stride, 1), frames, stride, length,
+                                           _dptr(syms, "syms", frames * sym_stride * 2, 2), sym_stride, stream),
+         "lphy_hip_lora_encode_batch")
+
+
+# --- LoRaWAN (lorawan.cpp; SURVEY 8f rank 4) ----------------------------
+LW_APPEND = 1
+# lphy_lorawan_desc / lphy_lorawan_frame (include/lphy_hip.h) as numpy dtypes
+LORAWAN_DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("devaddr", "<u4"), ("fcnt", "<u4"),
+                               ("key", "<u4"), ("uplink", "<u4"), ("reserved", "<u4")])
+LORAWAN_FRAME_DTYPE = np.dtype([("status", "<i4"), ("devaddr", "<u4"), ("mic", "<u4"), ("calc_mic", "<u4"),
+                                ("payload_offset", "<u4"), ("payload_len", "<u4"), ("fcnt", "<u2"),
+                                ("mhdr", "u1"), ("fctrl", "u1"), ("fopts_len", "u1"), ("reserved", "u1", 3)])
+
+
+def lorawan_mic_batch(data, desc, keys, mic=None, flags=0, stream=None):
+    """compute_mic for every descriptor row.  data: uint8 device tensor;
+    desc: device tensor holding len(desc) LORAWAN_DESC_DTYPE records (bytes);
+    keys: uint8 device tensor of 16-byte keys; mic: int32 device tensor."""
+    frames = desc.numel() * desc.element_size() // 32
+    nkeys = keys.numel() // 16
+    pm = _dptr(mic, "mic", frames * 4, 4) if mic is not None else None
+    _chk(load().lphy_hip_lorawan_mic_batch(_dptr(data, "data", 1, 1), _dptr(desc, "desc", frames * 32), frames,
+                                           _dptr(keys, "keys", nkeys * 16, 1), nkeys, pm, flags, stream),
+         "lphy_hip_lorawan_mic_batch")
+
+
+def lorawan_parse_batch(data, frames, stride, length, keys, out, lens=None, key_index=None, stream=None):
+    """parse_frame's checks on `frames` rows of decoded bytes; out: device
+    tensor of frames * 32 bytes (view it as LORAWAN_FRAME_DTYPE on the host)."""
+    nkeys = keys.numel() // 16
+    pl = _dptr(lens, "lens", frames * 4, 4) if lens is not None else None
+    pk = _dptr(key_index, "key_index", frames * 4, 4) if key_index is not None else None
+    _chk(load().lphy_hip_lorawan_parse_batch(_dptr(data, "data", (frames - 1) * stride + 1 if frames else 0, 1),
+                                             frames, stride, pl, length, _dptr(keys, "keys", nkeys * 16, 1),
+                                             nkeys, pk, _dptr(out, "out", frames * 32), stream),
+         "lphy_hip_lorawan_parse_batch")
+
+
+def lorawan_mic(key, uplink, devaddr, fcnt, data, device=0):
+    """One compute_mic on the GPU from host bytes."""
+    k = np.frombuffer(bytes(key), np.uint8)
+    d = np.frombuffer(bytes(data) + b"\0", np.uint8)
+    out = C.c_uint32()
+    _chk(load().lphy_hip_lorawan_mic_host(device, k.ctypes.data, int(uplink), devaddr & 0xFFFFFFFF,
+                                          fcnt & 0xFFFFFFFF, d.ctypes.data, len(data), C.byref(out)),
+         "lphy_hip_lorawan_mic_host")
+    return out.value

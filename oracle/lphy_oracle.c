@@ -781,6 +781,147 @@ typedef struct {
     uint8_t* bytes;
 } orc_job;
 
+/* ------------------------------------------------------------------ LoRaWAN
+ *  lorawan.cpp:35-177 and the AES-128 it calls
+ * (src/lorawan/aes.c, tiny-AES-c, AES128 + ECB).  The cipher is restated from
+ * FIPS-197 itself, byte by byte, with the S-box derived from the field
+ * inverse and the affine map rather than tabulated; it is pinned against the
+ * reference build (ref_aes128 / ref_lorawan_mic), FIPS-197 appendix C.1 and
+ * the MIC known answer lorawan_mic_test.cpp:10-11. */
+static uint8_t gf_mul(uint8_t a, uint8_t b) {
+    uint8_t r = 0;
+    while (b) {
+        if (b & 1) r ^= a;
+        a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1B : 0));
+        b >>= 1;
+    }
+    return r;
+}
+
+static uint8_t aes_sbox(uint8_t x) {
+    uint8_t inv = 1, p = x;  /* x^254 = x^-1 (0 -> 0) */
+    for (int e = 254; e; e >>= 1) {
+        if (e & 1) inv = gf_mul(inv, p);
+        p = gf_mul(p, p);
+    }
+    if (!x) inv = 0;
+    uint8_t y = 0x63;
+    for (int k = 0; k < 5; ++k) y ^= (uint8_t)((inv << k) | (inv >> ((8 - k) & 7)));
+    return y;
+}
+
+void orc_aes128(const uint8_t key[16], uint8_t blk[16]) {
+    uint8_t S[256], w[176];
+    for (int i = 0; i < 256; ++i) S[i] = aes_sbox((uint8_t)i);
+    memcpy(w, key, 16);
+    uint8_t rc = 1;
+    for (int i = 16; i < 176; i += 4) {
+        uint8_t t0 = w[i - 4], t1 = w[i - 3], t2 = w[i - 2], t3 = w[i - 1];
+        if (i % 16 == 0) {  /* SubWord(RotWord) ^ Rcon */
+            const uint8_t u = t0;
+            t0 = (uint8_t)(S[t1] ^ rc);
+            t1 = S[t2];
+            t2 = S[t3];
+            t3 = S[u];
+            rc = gf_mul(rc, 2);
+        }
+        w[i] = w[i - 16] ^ t0;
+        w[i + 1] = w[i - 15] ^ t1;
+        w[i + 2] = w[i - 14] ^ t2;
+        w[i + 3] = w[i - 13] ^ t3;
+    }
+    uint8_t st[16], t[16];
+    for (int i = 0; i < 16; ++i) st[i] = blk[i] ^ w[i];
+    for (int r = 1; r <= 10; ++r) {
+        /* SubBytes + ShiftRows: byte (row, col) <- (row, col + row) */
+        for (int c = 0; c < 4; ++c)
+            for (int row = 0; row < 4; ++row) t[4 * c + row] = S[st[4 * ((c + row) & 3) + row]];
+        if (r < 10) {
+            for (int c = 0; c < 4; ++c) {
+                const uint8_t* a = t + 4 * c;
+                const uint8_t m0 = gf_mul(a[0], 2) ^ gf_mul(a[1], 3) ^ a[2] ^ a[3];
+                const uint8_t m1 = a[0] ^ gf_mul(a[1], 2) ^ gf_mul(a[2], 3) ^ a[3];
+                const uint8_t m2 = a[0] ^ a[1] ^ gf_mul(a[2], 2) ^ gf_mul(a[3], 3);
+                const uint8_t m3 = gf_mul(a[0], 3) ^ a[1] ^ a[2] ^ gf_mul(a[3], 2);
+                st[4 * c] = m0, st[4 * c + 1] = m1, st[4 * c + 2] = m2, st[4 * c + 3] = m3;
+            }
+        } else {
+            memcpy(st, t, 16);
+        }
+        for (int i = 0; i < 16; ++i) st[i] ^= w[16 * r + i];
+    }
+    memcpy(blk, st, 16);
+}
+
+/* CMAC subkey doubling: the 16 bytes as one big-endian number, << 1, with
+ * the 0x87 reduction (lorawan.cpp:15-31). */
+static void cmac_double(const uint8_t* in, uint8_t* out) {
+    const int msb = in[0] >> 7;
+    for (int i = 0; i < 16; ++i) out[i] = (uint8_t)((in[i] << 1) | (i < 15 ? in[i + 1] >> 7 : 0));
+    if (msb) out[15] ^= 0x87;
+}
+
+/* lorawan.cpp:35-98: AES-CMAC over B0 || data, the first 4 bytes of the tag
+ * little-endian. */
+uint32_t orc_lorawan_mic(const uint8_t key[16], int uplink, uint32_t devaddr,
+                         uint32_t fcnt, const uint8_t* data, size_t len) {
+    uint8_t L[16] = {0}, K1[16], K2[16];
+    orc_aes128(key, L);
+    cmac_double(L, K1);
+    cmac_double(K1, K2);
+    uint8_t b0[16] = {0x49, 0, 0, 0, 0, (uint8_t)(uplink ? 0 : 1),
+                      (uint8_t)devaddr, (uint8_t)(devaddr >> 8), (uint8_t)(devaddr >> 16),
+                      (uint8_t)(devaddr >> 24), (uint8_t)fcnt, (uint8_t)(fcnt >> 8),
+                      (uint8_t)(fcnt >> 16), (uint8_t)(fcnt >> 24), (uint8_t)(len >> 8),
+                      (uint8_t)len};
+    const size_t total = len + 16, nblk = (total + 15) / 16;
+    uint8_t X[16] = {0};
+    for (size_t b = 0; b < nblk; ++b) {
+        uint8_t m[16] = {0};
+        size_t have = 0;
+        for (size_t j = 0; j < 16 && 16 * b + j < total; ++j, ++have) {
+            const size_t pos = 16 * b + j;
+            m[j] = pos < 16 ? b0[pos] : data[pos - 16];
+        }
+        if (b + 1 == nblk) {
+            const uint8_t* K = have == 16 ? K1 : K2;
+            if (have < 16) m[have] = 0x80;
+            for (int j = 0; j < 16; ++j) m[j] ^= K[j];
+        }
+        for (int j = 0; j < 16; ++j) X[j] ^= m[j];
+        orc_aes128(key, X);
+    }
+    return (uint32_t)X[0] | (uint32_t)X[1] << 8 | (uint32_t)X[2] << 16 | (uint32_t)X[3] << 24;
+}
+
+/* lorawan.cpp:150-176 on the decoded bytes (the `produced` bytes of
+ * lora_phy::decode).  rec = {status, devaddr, mic, calc_mic, payload_offset,
+ * payload_len, fcnt, mhdr, fctrl, fopts_len}; status as parse_frame returns
+ * it (FRMPayload length, -EINVAL on a MIC mismatch, -ERANGE). */
+void orc_lorawan_parse(const uint8_t key[16], const uint8_t* b, size_t len, int64_t* rec) {
+    memset(rec, 0, 10 * sizeof(int64_t));
+    if (len < 12) {
+        rec[0] = -ERANGE;
+        return;
+    }
+    const uint32_t devaddr = b[1] | b[2] << 8 | b[3] << 16 | (uint32_t)b[4] << 24;
+    const uint32_t fcnt = b[6] | b[7] << 8;
+    const uint32_t mic = b[len - 4] | b[len - 3] << 8 | b[len - 2] << 16 | (uint32_t)b[len - 1] << 24;
+    const uint32_t calc = orc_lorawan_mic(key, ((b[0] >> 5) & 1) == 0, devaddr, fcnt, b, len - 4);
+    const size_t fol = b[5] & 0x0F;
+    rec[1] = devaddr, rec[2] = mic, rec[3] = calc, rec[6] = fcnt, rec[7] = b[0], rec[8] = b[5];
+    rec[9] = (int64_t)fol;
+    if (mic != calc) {
+        rec[0] = -EINVAL;
+    } else if (8 + fol > len - 4) {
+        rec[0] = -ERANGE;
+    } else {
+        rec[4] = (int64_t)(8 + fol);
+        rec[5] = (int64_t)(len - 4 - 8 - fol);
+        rec[0] = rec[5];
+    }
+}
+
 static void* orc_worker(void* arg) {
     orc_job* j = (orc_job*)arg;
     const size_t N = (size_t)1 << j->sf, nsym = j->fs / N;

@@ -90,6 +90,15 @@ void orc_whiten(uint8_t* buf, size_t len, int kind, int bit_ofs,
 uint8_t orc_hamming(uint8_t x, int op, uint8_t* flags);               /* :229-371 */
 uint16_t orc_checksum(const uint8_t* buf, size_t len, int kind);      /* :32-105  */
 
+/* LoRaWAN: FIPS-197 AES-128 encryption of one block in
+ * place; compute_mic (lorawan.cpp:35-98); parse_frame's checks on decoded
+ * bytes (lorawan.cpp:150-176), rec[10] as documented in lphy_oracle.c. */
+void orc_aes128(const uint8_t key[16], uint8_t blk[16]);
+uint32_t orc_lorawan_mic(const uint8_t key[16], int uplink, uint32_t devaddr,
+                         uint32_t fcnt, const uint8_t* data, size_t len);
+void orc_lorawan_parse(const uint8_t key[16], const uint8_t* bytes, size_t len,
+                       int64_t* rec);
+
 /* Multi-threaded timing harness for bench.py's cpu_baseline ("port" kind):
  * mode 1 = dechirp + lora_demodulate + lora_decode per frame,
  * mode 0 = demodulate + decode.  Returns wall seconds. */

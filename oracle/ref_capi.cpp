@@ -11,6 +11,10 @@
 #include <lora_phy/phy.hpp>
 #include <lora_phy/ChirpGenerator.hpp>
 #include <lora_phy/LoRaCodes.hpp>
+#include <lorawan/lorawan.hpp>
+extern "C" {
+#include <lorawan/aes.h>
+}
 
 #include <chrono>
 #include <complex>
@@ -322,6 +326,62 @@ double ref_bench_modeA(unsigned sf, unsigned bw_hz, const float* iq,
     for (auto& t : th) t.join();
     auto t1 = std::chrono::steady_clock::now();
     return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// ---- LoRaWAN (lorawan.cpp + tiny-AES aes.c), SURVEY §8f rank 4
+void ref_aes128(const uint8_t key[16], uint8_t blk[16]) {
+    AES_ctx ctx;
+    AES_init_ctx(&ctx, key);
+    AES_ECB_encrypt(&ctx, blk);
+}
+
+uint32_t ref_lorawan_mic(const uint8_t key[16], int uplink, uint32_t devaddr, uint32_t fcnt,
+                         const uint8_t* data, size_t len) {
+    return lorawan::compute_mic(key, uplink != 0, devaddr, fcnt, data, len);
+}
+
+// build_frame: hdr = {mtype, major, devaddr, fctrl, fcnt}; returns its value,
+// symbols in `syms` (capacity cap), tmp bytes in `tmp` (capacity tmp_cap).
+long ref_lorawan_build(const uint8_t key[16], const uint32_t* hdr, const uint8_t* fopts, size_t nfopts,
+                       const uint8_t* payload, size_t npay, uint16_t* syms, size_t cap, uint8_t* tmp,
+                       size_t tmp_cap) {
+    lora_workspace ws{};
+    lorawan::Frame f;
+    f.mhdr.mtype = static_cast<lorawan::MType>(hdr[0]);
+    f.mhdr.major = static_cast<uint8_t>(hdr[1]);
+    f.fhdr.devaddr = hdr[2];
+    f.fhdr.fctrl = static_cast<uint8_t>(hdr[3]);
+    f.fhdr.fcnt = static_cast<uint16_t>(hdr[4]);
+    f.fhdr.fopts.assign(fopts, fopts + nfopts);
+    f.payload.assign(payload, payload + npay);
+    return lorawan::build_frame(&ws, key, f, syms, cap, tmp, tmp_cap);
+}
+
+// parse_frame: out = {mtype, major, devaddr, fctrl, fcnt, nfopts, npay} of the
+// Frame after the call (pre-set to all-ones markers), fopts / payload bytes
+// copied to the given buffers (capacity 256 / 65536).  `tmp` must hold
+// symbol_count / 2 bytes whatever tmp_cap says (the reference decodes before
+// checking the capacity).
+long ref_lorawan_parse(const uint8_t key[16], const uint16_t* syms, size_t n, uint8_t* tmp, size_t tmp_cap,
+                       uint32_t* out, uint8_t* fopts, uint8_t* payload) {
+    lora_workspace ws{};
+    lorawan::Frame f;
+    f.mhdr.mtype = static_cast<lorawan::MType>(7);
+    f.mhdr.major = 3;
+    f.fhdr.devaddr = 0xFFFFFFFFu;
+    f.fhdr.fctrl = 0xFF;
+    f.fhdr.fcnt = 0xFFFF;
+    long r = lorawan::parse_frame(&ws, key, syms, n, f, tmp, tmp_cap);
+    out[0] = static_cast<uint32_t>(f.mhdr.mtype);
+    out[1] = f.mhdr.major;
+    out[2] = f.fhdr.devaddr;
+    out[3] = f.fhdr.fctrl;
+    out[4] = f.fhdr.fcnt;
+    out[5] = static_cast<uint32_t>(f.fhdr.fopts.size());
+    out[6] = static_cast<uint32_t>(f.payload.size());
+    std::memcpy(fopts, f.fhdr.fopts.data(), f.fhdr.fopts.size());
+    std::memcpy(payload, f.payload.data(), f.payload.size());
+    return r;
 }
 
 }  // extern "C"

@@ -43,7 +43,34 @@ def build_oracle() -> None:
     subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "oracle"], check=True)
 
 
-class Oracle:
+def _u8(x) -> np.ndarray:
+    """bytes / list / array -> a fresh contiguous uint8 array."""
+    if isinstance(x, (bytes, bytearray)):
+        return np.frombuffer(bytes(x), np.uint8).copy()
+    return np.array(x, np.uint8, copy=True)
+
+
+class _LoRaWANMixin:
+    """compute_mic / AES-128 (lorawan.cpp:35-98, aes.c) on either library."""
+
+    def _lw_types(self, L, pre):
+        getattr(L, pre + "aes128").argtypes = [_u8p, _u8p]
+        getattr(L, pre + "lorawan_mic").argtypes = [_u8p, C.c_int, C.c_uint32, C.c_uint32, _u8p, C.c_size_t]
+        getattr(L, pre + "lorawan_mic").restype = C.c_uint32
+
+    def aes128(self, key, block):
+        k, b = _u8(key), _u8(block)
+        getattr(self.lib, self._p + "aes128")(_p(k, _u8p), _p(b, _u8p))
+        return b
+
+    def lorawan_mic(self, key, uplink, devaddr, fcnt, data):
+        k = _u8(key)
+        d = np.frombuffer(bytes(data) + b"\0", np.uint8)
+        return int(getattr(self.lib, self._p + "lorawan_mic")(_p(k, _u8p), int(uplink), devaddr & 0xFFFFFFFF,
+                                                               fcnt & 0xFFFFFFFF, _p(d, _u8p), len(data)))
+
+
+class Oracle(_LoRaWANMixin):
     _p = "orc_"
 
     def __init__(self, path: Path = ORACLE_SO):
@@ -93,6 +120,8 @@ class Oracle:
         L.orc_bench.argtypes = [C.c_int, C.c_uint, C.c_uint, _f32p, C.c_size_t,
                                 C.c_size_t, _u8p, C.c_int]
         L.orc_bench.restype = C.c_double
+        self._lw_types(L, "orc_")
+        L.orc_lorawan_parse.argtypes = [_u8p, _u8p, C.c_size_t, C.POINTER(C.c_int64)]
 
 
     # --- LoRaCodes.hpp helpers -------------------------
@@ -124,6 +153,16 @@ class Oracle:
     def checksum(self, buf, kind):
         b = np.ascontiguousarray(np.frombuffer(bytes(buf), np.uint8)) if not isinstance(buf, np.ndarray) else np.ascontiguousarray(buf, np.uint8)
         return getattr(self.lib, self._p + "checksum")(_p(b, _u8p), len(b), kind)
+
+    def lorawan_parse(self, key, data):
+        """parse_frame's checks on decoded bytes -> dict (lphy_oracle.c)."""
+        k = _u8(key)
+        d = np.frombuffer(bytes(data) + b"\0", np.uint8)
+        rec = np.zeros(10, np.int64)
+        self.lib.orc_lorawan_parse(_p(k, _u8p), _p(d, _u8p), len(data), rec.ctypes.data_as(C.POINTER(C.c_int64)))
+        names = ("status", "devaddr", "mic", "calc_mic", "payload_offset", "payload_len", "fcnt", "mhdr",
+                 "fctrl", "fopts_len")
+        return {n: int(v) for n, v in zip(names, rec)}
 
     # --- producers -----------------------------------------------------
     def genchirp(self, N, osr, NN, f0, down, ampl, phase, bw_scale):
@@ -227,7 +266,7 @@ class Oracle:
         return t, out
 
 
-class Reference:
+class Reference(_LoRaWANMixin):
     """The reference library (oracle/_ref), when it has been built."""
     _p = "ref_"
 
@@ -276,6 +315,13 @@ class Reference:
         L.ref_hamming.restype = C.c_uint8
         L.ref_checksum.argtypes = [_u8p, C.c_size_t, C.c_int]
         L.ref_checksum.restype = C.c_uint16
+        self._lw_types(L, "ref_")
+        _u32p = C.POINTER(C.c_uint32)
+        L.ref_lorawan_build.argtypes = [_u8p, _u32p, _u8p, C.c_size_t, _u8p, C.c_size_t, _u16p,
+                                        C.c_size_t, _u8p, C.c_size_t]
+        L.ref_lorawan_build.restype = C.c_long
+        L.ref_lorawan_parse.argtypes = [_u8p, _u16p, C.c_size_t, _u8p, C.c_size_t, _u32p, _u8p, _u8p]
+        L.ref_lorawan_parse.restype = C.c_long
         for n in ("ref_bench_modeA", "ref_bench_modeB"):
             getattr(L, n).argtypes = [C.c_uint, C.c_uint, _f32p, C.c_size_t,
                                       C.c_size_t, _u8p, C.c_int]
@@ -311,6 +357,36 @@ class Reference:
     def checksum(self, buf, kind):
         b = np.ascontiguousarray(np.frombuffer(bytes(buf), np.uint8)) if not isinstance(buf, np.ndarray) else np.ascontiguousarray(buf, np.uint8)
         return getattr(self.lib, self._p + "checksum")(_p(b, _u8p), len(b), kind)
+
+    def lorawan_build(self, key, mtype, major, devaddr, fctrl, fcnt, fopts, payload, cap=None, tmp_cap=None):
+        """lorawan::build_frame -> (return value, symbols, tmp bytes)."""
+        k = _u8(key)
+        hdr = np.array([mtype, major, devaddr & 0xFFFFFFFF, fctrl, fcnt & 0xFFFF], np.uint32)
+        fo = np.frombuffer(bytes(fopts) + b"\0", np.uint8)
+        pl = np.frombuffer(bytes(payload) + b"\0", np.uint8)
+        need = 12 + len(fopts) + len(payload)
+        cap = 2 * need if cap is None else cap
+        tmp_cap = need if tmp_cap is None else tmp_cap
+        syms = np.zeros(max(cap, 1), np.uint16)
+        tmp = np.zeros(max(tmp_cap, need, 1), np.uint8)
+        r = self.lib.ref_lorawan_build(_p(k, _u8p), hdr.ctypes.data_as(C.POINTER(C.c_uint32)), _p(fo, _u8p),
+                                       len(fopts), _p(pl, _u8p), len(payload), _p(syms, _u16p), cap,
+                                       _p(tmp, _u8p), tmp_cap)
+        return int(r), syms[: max(int(r), 0)], tmp
+
+    def lorawan_parse(self, key, syms, tmp_cap=None):
+        """lorawan::parse_frame -> (return value, Frame fields dict)."""
+        k = _u8(key)
+        sy = np.ascontiguousarray(syms, np.uint16)
+        tmp_cap = len(sy) // 2 if tmp_cap is None else tmp_cap
+        tmp = np.zeros(max(len(sy) // 2, tmp_cap, 1), np.uint8)
+        out = np.zeros(7, np.uint32)
+        fo, pl = np.zeros(256, np.uint8), np.zeros(65536, np.uint8)
+        r = self.lib.ref_lorawan_parse(_p(k, _u8p), _p(sy, _u16p), len(sy), _p(tmp, _u8p), tmp_cap,
+                                       out.ctypes.data_as(C.POINTER(C.c_uint32)), _p(fo, _u8p), _p(pl, _u8p))
+        f = dict(zip(("mtype", "major", "devaddr", "fctrl", "fcnt"), (int(v) for v in out[:5])))
+        f["fopts"], f["payload"] = fo[: out[5]].tobytes(), pl[: out[6]].tobytes()
+        return int(r), f
 
     def fft(self, x):
         x = _cf(np.asarray(x, np.complex64))

@@ -53,7 +53,7 @@ def crc_payload(rng, n: int, oracle) -> str:
     """n-byte payload whose last two bytes are the sx1272 checksum of
     payload[2:n-2], so lora_phy::decode reports crc_ok (phy.cpp:252-259)."""
     body = bytearray(rng.integers(0, 256, n - 2, dtype=np.uint8).tobytes())
-    c = oracle.checksum(bytes(body[2:]))
+    c = oracle.sx_checksum(bytes(body[2:]))
     return (bytes(body) + bytes([c & 0xFF, c >> 8])).hex()
 
 
