@@ -33,3 +33,27 @@ def test_cxx_api_transcript_matches_reference(tmp_path):
     assert len(a) == len(b) and len(b) >= 25
     bad = [(x, y) for x, y in zip(a, b) if x != y]
     assert not bad, "\n".join(f"ours: {x[:300]}\nref:  {y[:300]}" for x, y in bad[:5])
+
+
+LW_REF_PROBE = ROOT / "oracle" / "_ref" / "lorawan_api_probe_ref"
+
+
+def test_lorawan_api_transcript_matches_reference(tmp_path):
+    """lorawan:: drop-in (include/lorawan/lorawan.hpp, GPU MIC + decode)
+    against the reference's lorawan.cpp + tiny-AES: the same probe
+    (tests/cpp/lorawan_api_probe.cpp) built against both."""
+    if not LW_REF_PROBE.exists():
+        pytest.skip("reference lorawan probe not built (oracle/Makefile lwprobe)")
+    exe = tmp_path / "lwprobe_amd"
+    subprocess.run(["g++", "-O2", "-std=gnu++17", f"-I{ROOT / 'include'}", "-o", str(exe),
+                    str(ROOT / "tests" / "cpp" / "lorawan_api_probe.cpp"), f"-L{PKG / 'lib'}", "-llora_phy_amd",
+                    f"-Wl,-rpath,{PKG / 'lib'}"], check=True)
+    ours = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert ours.returncode == 0, ours.stderr
+    ref = subprocess.run([str(LW_REF_PROBE)], capture_output=True, text=True, timeout=300)
+    assert ref.returncode == 0, ref.stderr
+    a, b = ours.stdout.splitlines(), ref.stdout.splitlines()
+    assert len(a) == len(b) and len(b) >= 400
+    assert b[0] == "mic kat 82b5c3d6"
+    bad = [(x, y) for x, y in zip(a, b) if x != y]
+    assert not bad, "\n".join(f"ours: {x[:300]}\nref:  {y[:300]}" for x, y in bad[:5])
