@@ -90,10 +90,15 @@ enum lphy_flags {
                                     the per-sample sincos of the reference
                                     instead of the certified per-frame
                                     table (same results; for comparison) */
-    LPHY_F_RESIDENT = 128u       /* fused launch: where it applies (SF 7,
+    LPHY_F_RESIDENT = 128u,      /* fused launch: where it applies (SF 7,
                                     56..70 whole symbols per frame), the
                                     single-read kernel that keeps each frame
                                     on the CU (same results; experimental) */
+    LPHY_F_SCAN_FIRST = 256u     /* fused launch, modes 1/2: scan each whole
+                                    frame's max-abs before its estimate (a
+                                    second read of the frame) instead of the
+                                    speculative normalisation checked at the
+                                    frame's end (same results; comparison) */
 };
 
 enum lphy_window { LPHY_WINDOW_NONE = 0, LPHY_WINDOW_HANN = 1 };

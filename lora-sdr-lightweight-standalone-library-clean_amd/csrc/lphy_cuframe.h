@@ -418,9 +418,13 @@ __global__ __launch_bounds__(512, 1) void k_cuframe(DemodArgs A) {
             }
 #pragma unroll
             for (int e = 0; e < G::E; ++e) {
-                const cf32 x = v[e];
+                cf32 x = v[e];
                 if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE)
                     amax = fmaxf(amax, fmaxf(fabsf(x.x), fabsf(x.y)));
+                // mode 2: the exact dechirp at the sample's chirp index (the
+                // table holds the rotation and scale only, build_rtab)
+                if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+                    x = cmul(x, sh.dnl[(base + (unsigned)Gr0::inidx(e, lam)) & (N - 1)]);
                 v[e] = cmul(x, rt[Gr0::inidx(e, lam)]);
             }
 #ifndef LPHY_ABLATE_CU_DFFT  // timing experiments only

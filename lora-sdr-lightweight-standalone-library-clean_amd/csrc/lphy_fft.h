@@ -110,6 +110,18 @@ __device__ __forceinline__ cf32 csub_rot(cf32 a, cf32 b) {
     asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
+// Fused complex product for the certified fast path only (symbol units
+// whose result is the argmax of |X|^2, proven against the rounding bound of
+// fast_certified): (ax bx - ay by, ax by + ay bx) as one v_pk_mul_f32 and one
+// v_pk_fma_f32.  Each part rounds once after an exact product instead of
+// three times, so its error is within the plain product's bound.  Never used
+// where the reference's bits are reproduced.
+__device__ __forceinline__ cf32 cmul_fma(cf32 a, cf32 b) {
+    const cf32 t = a.yy * b.yx;  // (ay by, ay bx)
+    cf32 r;                      // (ax bx - t.x, ax by + t.y): the sign as a modifier
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_lo:[0,0,1]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+    return r;
+}
 __device__ __forceinline__ cf32 cadd(cf32 a, cf32 b) { return a + b; }
 __device__ __forceinline__ cf32 csub(cf32 a, cf32 b) { return a - b; }
 __device__ __forceinline__ cf32 cscale(cf32 a, float s) { return a * s; }
@@ -292,14 +304,19 @@ __device__ __forceinline__ void pass_butterflies(cf32 (&v)[16], int lam,
                 // twiddle index 0 for every lane: MH == 1 makes low == 0
                 const bool one = TRIV && P::MH == 1 && (a % w) == 0;
                 cf32* x = &v[s * P::GS];
+                // TRIV transforms only feed the certified |X|^2 argmax: fused products
+                auto mul = [&](cf32 u, cf32 t) __attribute__((always_inline)) {
+                    if constexpr (TRIV) return cmul_fma(u, t);
+                    else return cmul_t<AG>(u, t);
+                };
                 if (R == 2) {
-                    const cf32 t = one ? x[a + w] : cmul_t<AG>(x[a + w], tw[k * fs]);
+                    const cf32 t = one ? x[a + w] : mul(x[a + w], tw[k * fs]);
                     x[a + w] = csub(x[a], t);
                     x[a] = cadd(x[a], t);
                 } else {
-                    const cf32 s0 = one ? x[a + w] : cmul_t<AG>(x[a + w], tw[k * fs]);
-                    const cf32 s1 = one ? x[a + 2 * w] : cmul_t<AG>(x[a + 2 * w], tw[k * fs * 2]);
-                    const cf32 s2 = one ? x[a + 3 * w] : cmul_t<AG>(x[a + 3 * w], tw[k * fs * 3]);
+                    const cf32 s0 = one ? x[a + w] : mul(x[a + w], tw[k * fs]);
+                    const cf32 s1 = one ? x[a + 2 * w] : mul(x[a + 2 * w], tw[k * fs * 2]);
+                    const cf32 s2 = one ? x[a + 3 * w] : mul(x[a + 3 * w], tw[k * fs * 3]);
                     const cf32 s5 = csub(x[a], s1);
                     const cf32 a0 = cadd(x[a], s1);
                     const cf32 s3 = cadd(s0, s2);

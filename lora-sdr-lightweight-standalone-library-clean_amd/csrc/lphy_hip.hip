@@ -311,6 +311,7 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     A.exact_rotation = (flags & LPHY_F_EXACT_ROTATION) ? 1 : 0;
     A.counters = c->d_counters;
     A.resident = (flags & LPHY_F_RESIDENT) ? 1 : 0;
+    A.spec = (mode != LPHY_MODE_DEMODULATE && !A.no_scratch && !(flags & LPHY_F_SCAN_FIRST)) ? 1 : 0;
     const size_t est_syms = mode == LPHY_MODE_DEMODULATE ? 2 : (total < 2 ? total : 2);
     A.est_units = (int)(est_syms * c->osr);
     // 32-bit symbol / sample bookkeeping in the kernels

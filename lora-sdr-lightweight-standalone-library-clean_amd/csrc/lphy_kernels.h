@@ -69,6 +69,7 @@ struct DemodArgs {
     unsigned long long* counters;  // ctx counters: [0] rechecks, [1..4] phase clocks
     int sentinels;           // k_post: look for kSymRecheck in frames with status 0 (k_cuframe)
     int resident;            // LPHY_F_RESIDENT: k_cuframe where it applies
+    int spec;                // k_frames modes 1/2: speculative normalisation (no whole-frame pre-scan)
     // persistent demod workers: symbol stride per step split into whole
     // frames + symbols (host-computed, so the kernel never divides)
     unsigned stride_f, stride_s;
@@ -162,6 +163,14 @@ constexpr int kStatusFixup = 0x7f5a0001;
 // rotation (value kSymRecheck in the output; k_post recomputes exactly those)
 constexpr int kStatusRecheck = 0x7f5a0002;
 constexpr uint16_t kSymRecheck = 0xffff;  // never a bin index (N <= 4096)
+// ... and: k_frames demodulated the frame with the normalisation of its
+// first two symbols, but a later sample raised the frame's max-abs, so the
+// estimate must be redone with the exact scale and the symbols' certificates
+// re-checked against the exact rate (k_post settle_frames).  The record then
+// holds {cfo: the frame's max-abs, time_offset: the symbols' least
+// certificate ratio}; the second code also has symbols left open.
+constexpr int kStatusSettle = 0x7f5a0003;
+constexpr int kStatusSettleRecheck = 0x7f5a0004;
 
 // Normalisation decision of LoRaDemod.cpp:60-78 from the frame's max-abs.
 __device__ __forceinline__ lphy_frame_meta norm_meta(float mx, bool have_sync, int no_scratch) {
@@ -765,12 +774,14 @@ __device__ __forceinline__ float max3_abs(float m, float a, float b) {
 }
 
 template <int SF, int MODE>
-__device__ __forceinline__ float wave_maxabs(const DemodArgs& A, unsigned f, const cf32* down) {
+__device__ __forceinline__ float wave_maxabs(const DemodArgs& A, unsigned f, const cf32* down,
+                                             unsigned limit = 0) {
     constexpr int N = 1 << SF;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     const int lane = threadIdx.x & 63;
     const cf32* fr = A.iq + (unsigned long long)f * A.frame_samples;
-    const unsigned count = DECH ? (unsigned)A.total_syms * N : (unsigned)A.frame_samples;
+    // limit: the first `limit` samples only (speculative normalisation)
+    const unsigned count = limit ? limit : (DECH ? (unsigned)A.total_syms * N : (unsigned)A.frame_samples);
     float mx = 0.0f;
     bool bad = false;  // non-finite [dechirped] sample
     auto acc = [&](cf32 x, unsigned i) {
@@ -842,6 +853,53 @@ __device__ __forceinline__ float wave_maxabs(const DemodArgs& A, unsigned f, con
     return __ballot(bad) ? __builtin_nanf("") : mx;
 }
 
+// Max-abs of samples [lo, hi) of frame f by one wavefront, per-sample fold
+// with the reference's NaN rules; `bad` when one is non-finite.  Used for
+// the few samples no symbol window of a speculatively normalised frame
+// covers (a negative time shift's last samples, mode 1's partial symbol).
+template <int SF, int MODE>
+__device__ float wave_range_maxabs(const DemodArgs& A, unsigned f, unsigned lo, unsigned hi,
+                                   const cf32* down, bool& bad) {
+    constexpr int N = 1 << SF;
+    const int lane = threadIdx.x & 63;
+    const cf32* fr = A.iq + (unsigned long long)f * A.frame_samples;
+    float mx = 0.0f;
+    bool b = false;
+    for (unsigned i = lo + (unsigned)lane; i < hi; i += 64) {
+        cf32 x = fr[i];
+        if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) x = cmul(x, down[i & (N - 1)]);
+        b |= !(__builtin_isfinite(x.x) && __builtin_isfinite(x.y));
+        maxabs_acc(mx, x);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float o = __shfl_xor(mx, off, 64);
+        mx = o > mx ? o : mx;
+    }
+    bad = __ballot(b) != 0;
+    return mx;
+}
+
+// End of the samples the frame's symbol windows (shifted by t_off as
+// LoRaDemod.cpp:144-150 does) and its two estimate symbols cover together,
+// a contiguous run from sample 0; the frame's max-abs needs [end, count) too.
+__device__ __forceinline__ unsigned covered_end(unsigned S, unsigned N, unsigned count, int t) {
+    unsigned end = S * N;
+    if (t > 0) {
+        // windows s with s N + t + N <= count are shifted
+        if ((unsigned long long)t + N <= count) {
+            const unsigned long long smax = ((unsigned long long)count - (unsigned)t - N) / N;
+            const unsigned long long last = smax < S - 1 ? smax : S - 1;
+            const unsigned long long e = (last + 1) * N + (unsigned)t;
+            if (e > end) end = (unsigned)e;
+        }
+    } else if (t < 0) {
+        const unsigned long long off = (unsigned long long)(-(long long)t);
+        if (off <= (unsigned long long)(S - 1) * N) end = (unsigned)(S * N - off);
+    }
+    return end > 2 * N ? end : 2 * N;
+}
+
 enum : int { kUnitDead = 0, kUnitEst = 1, kUnitSym = 2 };
 
 // ---------------------------------------------------------------------------
@@ -885,26 +943,24 @@ template <int SF, int MODE>
 __device__ __forceinline__ void build_rtab(cf32* tab, float rate, float scale, int t_off,
                                            const cf32* down, const float* win, int lane) {
     constexpr int N = 1 << SF;
-    const unsigned t0 = (unsigned)t_off & (N - 1);
+    (void)t_off;
     for (int i = lane; i < N; i += 64) {
         float sn, cs;
         lphy_libm::sincosf_exact(rate * (float)i, &sn, &cs);
         cf32 t = cf32{cs, sn};
         if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) t = cmul(down[i], t);
-        if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) t = cmul(down[(t0 + (unsigned)i) & (N - 1)], t);
         if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) t = cscale(t, scale);
         if constexpr ((MODE & kWinBit) != 0) t = cscale(t, win[i]);
         tab[i] = t;
     }
 }
 
-// Whether the fast path may take this symbol unit: the table's dechirp
-// offset (mode 2) must match the symbol's window start.
+// Whether the fast path may take this symbol unit: every window (mode 2
+// dechirps each sample exactly at its own chirp index before the table).
 template <int SF, int MODE>
 __device__ __forceinline__ bool fast_applies(const SymCtx& c, int t_off) {
-    constexpr int N = 1 << SF;
-    if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
-        return (c.base & (N - 1)) == ((unsigned)t_off & (N - 1));
+    (void)c;
+    (void)t_off;
     return true;
 }
 
@@ -916,21 +972,32 @@ __device__ __forceinline__ bool fast_applies(const SymCtx& c, int t_off) {
 // arithmetic stays negligible against B), b.v >= 1e-30 (a normal |X|^2), and
 // a runner-up below 1e-30 is taken as 1e-30.
 template <int SF>
-__device__ __forceinline__ bool fast_certified(const ArgMax2& b, const SymCtx& c, float amax) {
+__device__ __forceinline__ float cert_bound(float rate, float start, float amax) {
     constexpr int N = 1 << SF, L = (SF + 1) / 2;
     const float A = (float)N * 1.41421366f * amax * 1.0001f;
-    const float ar = fabsf(c.rate) * (float)N;
-    const float P = fabsf(c.start) + ar;
-    const float B = kU * A * ((24.0f + 12.0f * L) + 2.0f * ar + P) * 1.001f;
-    const float lhs = sqrtf(b.v) * (1.0f - 8.0f * kU) - 4.0f * B;
-    const float rhs = sqrtf(fmaxf(b.v2, 1e-30f)) * (1.0f + 8.0f * kU);
-    return lhs > rhs && A < 1e18f && amax >= 1e-20f && b.v >= 1e-30f;
+    const float ar = fabsf(rate) * (float)N;
+    const float P = fabsf(start) + ar;
+    return kU * A * ((24.0f + 12.0f * L) + 2.0f * ar + P) * 1.001f;
+}
+// winner's lead over the runner-up, less the |X|^2 roundings
+__device__ __forceinline__ float cert_gap(const ArgMax2& b) {
+    return sqrtf(b.v) * (1.0f - 8.0f * kU) - sqrtf(fmaxf(b.v2, 1e-30f)) * (1.0f + 8.0f * kU);
+}
+template <int SF>
+__device__ __forceinline__ bool fast_certified(const ArgMax2& b, const SymCtx& c, float amax) {
+    constexpr int N = 1 << SF;
+    const float A = (float)N * 1.41421366f * amax * 1.0001f;
+    const float B = cert_bound<SF>(c.rate, c.start, amax);
+    return cert_gap(b) > 4.0f * B && A < 1e18f && amax >= 1e-20f && b.v >= 1e-30f;
 }
 
-// Fast staging of one tile: symbol units q_i = x_i * t_i from the frame's
-// rotation table (LDS ring for SF <= 8, the lane's registers above), estimate
-// units exactly as stage_mixed (no rotation).  Returns the lane's
-// max(|Re x|, |Im x|) over its symbol samples for mode 0's certificate.
+// Fast staging of one tile: symbol units q_i = y_i * t_i from the frame's
+// rotation table t (LDS ring for SF <= 8, the lane's registers above) with a
+// fused product, where y is the sample, or in mode 2 its exact dechirp at
+// its own chirp index (down: the doubled table); estimate units exactly as
+// stage_mixed (no rotation).  Returns the lane's max(|Re y|, |Im y|) over its
+// symbol samples: mode 0's certificate amplitude, and for modes 1/2 the
+// samples' share of the frame's max-abs (speculative normalisation).
 template <int SF, int MODE, bool MIXED>
 __device__ __forceinline__ float stage_fast(cf32* lds, const Stage<SF>& stg, const cf32 (&raw)[16],
                                             const SymCtx& c, int lam, const cf32* down,
@@ -940,6 +1007,7 @@ __device__ __forceinline__ float stage_fast(cf32* lds, const Stage<SF>& stg, con
     constexpr int N = G::N;
     constexpr bool RLDS = SF <= 8;
     float amax = 0.0f;
+    const cf32* dl = down + (c.base & (N - 1)) + lam;
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const int i = lam + e * G::LPS;
@@ -955,9 +1023,10 @@ __device__ __forceinline__ float stage_fast(cf32* lds, const Stage<SF>& stg, con
             y = c.ok ? p : czero();
             if constexpr ((MODE & kWinBit) != 0) y = cscale(y, win[i]);
         } else {
-            y = cmul(x, RLDS ? rt[i] : rreg[e]);
-            if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE)
-                amax = fmaxf(amax, fmaxf(fabsf(x.x), fabsf(x.y)));
+            cf32 p = x;
+            if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) p = cmul(x, dl[e * G::LPS]);
+            amax = max3_abs(amax, p.x, p.y);
+            y = cmul_fma(p, RLDS ? rt[i] : rreg[e]);
         }
         stg.put(lds, e, y);
     }
@@ -970,6 +1039,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     static_assert(G::LPS <= 64, "fused path needs a symbol inside one wavefront");
     constexpr int N = G::N;
     constexpr bool TAB = N <= 1024;
+    static_assert(TAB, "LDS tables (the doubled down-chirp) for every fused SF");
     constexpr int WT = 64 / G::LPS;               // units per tile
     constexpr unsigned U = 2;                      // estimate units per frame
     // prefix tiles: E of the first frame, then one tile that keeps its
@@ -982,17 +1052,20 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     const DemodArgs& A = P.A;
     __shared__ cf32 lds[G::T * G::SSTRIDE];
     __shared__ cf32 twl[N];
-    __shared__ cf32 dnl[TAB ? N : 1];
+    // down-chirp twice over (entry i = down[i mod N]): a symbol window's
+    // chirp indices t0 + i, i < N, need no wrap
+    __shared__ cf32 dnl[TAB ? 2 * N : 1];
     __shared__ float wnl[TAB ? N : 1];
     __shared__ UnitResult ures[WPB][U];
     __shared__ float4 ring[WPB][3];  // frame records: rate, scale, t_off, flags
+    __shared__ float ringmx[WPB][3];  // ... and the max-abs their normalisation used
     __shared__ cf32 rtab[RLDS ? WPB : 1][2][RLDS ? N : 1];
 
     const int tid = threadIdx.x;
     for (int i = tid; i < N; i += kTile) {
         twl[i] = A.tw[i];
         if constexpr (TAB) {
-            if ((MODE & 3) != LPHY_MODE_LORA_DEMODULATE) dnl[i] = A.down[i];
+            if ((MODE & 3) != LPHY_MODE_LORA_DEMODULATE) dnl[i] = dnl[i + N] = A.down[i];
             if (A.win) wnl[i] = A.win[i];
         }
     }
@@ -1016,6 +1089,18 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     const unsigned long long L = (unsigned long long)PT * WT + (unsigned long long)nk * SL;
     const unsigned ntiles = (unsigned)((L + WT - 1) / WT);
     const bool exact_only = A.exact_rotation != 0;
+    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    // Speculative normalisation (modes 1/2).  The reference scales the whole
+    // frame by 1 / max(|I|,|Q|) before it estimates (LoRaDemod.cpp:60-78), so
+    // the exact estimate needs every sample first: a blocking pre-scan that
+    // re-reads the frame.  Instead M scans only the two estimate symbols, the
+    // frame is estimated and demodulated with that normalisation, and each
+    // symbol unit folds its own samples' max-abs while they are in registers.
+    // When the symbol that ends the frame is done, the frame's true max-abs
+    // is known: the same normalisation means every output stands; otherwise
+    // the frame goes to k_post's settle_frames (exact estimate, certificates
+    // re-checked against the exact rate, else the whole-frame re-run).
+    const bool spec = (MODE & 3) != LPHY_MODE_DEMODULATE && A.spec != 0;
 
     // unit of this team in tile t; (k, o) = slice and offset for t >= PT
     auto unit_of = [&](unsigned t, unsigned k, unsigned o, unsigned& kind, unsigned& fk,
@@ -1082,7 +1167,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
 #ifdef LPHY_ABLATE_FRAME_SCAN  // timing experiments only
                     mx = 1.0f;
 #else
-                    mx = wave_maxabs<SF, MODE>(A, w + nke * W, down);
+                    mx = wave_maxabs<SF, MODE>(A, w + nke * W, down, spec ? 2u * N : 0u);
 #endif
                     m_seq = nke;
                 }
@@ -1098,12 +1183,17 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     }
     cf32 rreg[16];                 // SF 9-10: the team's table ...
     unsigned rreg_fk = 0xffffffffu;  // ... of this frame
+    // speculative normalisation: the lane's running state for the two frames
+    // whose symbols can be in flight (by parity of the frame): max-abs of the
+    // symbol samples, least certificate ratio, flags (1 NaN, 2 symbol open)
+    constexpr float kBig = 3.0e38f;
+    float sp_mx0 = 0.0f, sp_mx1 = 0.0f, sp_r0 = kBig, sp_r1 = kBig;
+    unsigned sp_fl0 = 0u, sp_fl1 = 0u;
 
     for (unsigned t = 0; t < ntiles; ++t) {
         // SF 9-10: a team entering a new frame builds its table entries
         if constexpr (!RLDS) {
             if (kind == kUnitSym && fk != rreg_fk) {
-                const unsigned t0 = (unsigned)c.toff & (N - 1);
 #pragma unroll
                 for (int e = 0; e < G::E; ++e) {
                     const int i = lam + e * G::LPS;
@@ -1111,8 +1201,6 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
                     lphy_libm::sincosf_exact(c.rate * (float)i, &sn, &cs);
                     cf32 tv = cf32{cs, sn};
                     if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) tv = cmul(down[i], tv);
-                    if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
-                        tv = cmul(down[(t0 + (unsigned)i) & (N - 1)], tv);
                     if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) tv = cscale(tv, c.scale);
                     if constexpr ((MODE & kWinBit) != 0) tv = cscale(tv, win[i]);
                     rreg[e] = tv;
@@ -1144,7 +1232,15 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
 #pragma unroll
             for (int off = G::LPS / 2; off >= 1; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
         } else {
-            amax = 1.0f;  // normalised frame: max(|I|,|Q|) <= 1 (see fast_certified)
+            // normalised frame: max(|I|,|Q|) <= 1 (see fast_certified); under
+            // speculation the frame end confirms it or settles the frame
+            if (spec) {
+                // the symbol's [dechirped] samples, as the pre-scan folds them
+                const float lm = kind == kUnitSym && c.ok ? amax : 0.0f;
+                if (fk & 1) sp_mx1 = fmaxf(sp_mx1, lm);
+                else sp_mx0 = fmaxf(sp_mx0, lm);
+            }
+            amax = 1.0f;
         }
         team_sync<SF>();
 
@@ -1197,6 +1293,23 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         // (no exact re-run here: it would keep a second transform's state
         // live beside the prefetch.  The symbol is left as kSymRecheck and
         // its frame as kStatusRecheck; k_post recomputes it exactly.)
+        if (spec && kind == kUnitSym && c.ok) {
+            // a NaN sample reaches every bin (fft_has_nan); the certificate's
+            // lead over its bound, for the frame end's rate check
+            const cf32 q = v[0] * v[0];
+            const float q2 = q.x + q.y;
+            unsigned fl = q2 == q2 ? 0u : 1u;
+            float r = kBig;
+            if (redo) fl |= 2u;
+            else r = cert_gap(b2) / cert_bound<SF>(c.rate, c.start, 1.0f);
+            if (fk & 1) {
+                sp_fl1 |= fl;
+                sp_r1 = fminf(sp_r1, r);
+            } else {
+                sp_fl0 |= fl;
+                sp_r0 = fminf(sp_r0, r);
+            }
+        }
         if (kind == kUnitSym && lam == 0) {
             // sw0 / sw1 also for frames that are not demodulated (0, as the
             // separate-launch path leaves them)
@@ -1228,6 +1341,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             }
             ring[wv][ke % 3] = float4{m.rate, m.scale, __int_as_float(m.t_off),
                                       __uint_as_float((m.status == 0 ? 1u : 0u) | 2u)};
+            ringmx[wv][ke % 3] = mxe;
             meta_put_est(&A.meta[w + ke * W], m);
         }
         team_sync<SF>();
@@ -1238,6 +1352,45 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
                 const float4 r = ring[wv][ke % 3];
                 if (__float_as_uint(r.w) & 1u)
                     build_rtab<SF, MODE>(rtab[wv][ke & 1], r.x, r.y, __float_as_int(r.z), down, win, lane);
+            }
+        }
+        // speculative normalisation: the tile holding a frame's last symbol
+        // unit closes the frame (its other symbols are in earlier tiles)
+        if (spec) {
+            const unsigned long long fe = __ballot(kind == kUnitSym && su == S - 1);
+            if (fe) {
+                const unsigned kf = (unsigned)__shfl((int)fk, __ffsll((long long)fe) - 1, 64);
+                const bool p1 = (kf & 1) != 0;
+                float m = p1 ? sp_mx1 : sp_mx0, r = p1 ? sp_r1 : sp_r0;
+                const unsigned fl = p1 ? sp_fl1 : sp_fl0;
+                if (p1) { sp_mx1 = 0.0f; sp_r1 = kBig; sp_fl1 = 0u; }
+                else { sp_mx0 = 0.0f; sp_r0 = kBig; sp_fl0 = 0u; }
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    m = fmaxf(m, __shfl_xor(m, off, 64));
+                    r = fminf(r, __shfl_xor(r, off, 64));
+                }
+                const bool nan = __ballot(fl & 1u) != 0, open = __ballot(fl & 2u) != 0;
+                const float4 rr = ring[wv][kf % 3];
+                if (__float_as_uint(rr.w) & 1u) {
+                    const unsigned f = w + kf * W;
+                    const unsigned cnt = DECH ? S * N : (unsigned)A.frame_samples;
+                    const unsigned end = covered_end(S, N, cnt, __float_as_int(rr.z));
+                    bool fbad = false;
+                    if (end < cnt) m = fmaxf(m, wave_range_maxabs<SF, MODE>(A, f, end, cnt, down, fbad));
+                    if (lane == 0) {
+                        const float mx01 = ringmx[wv][kf % 3];
+                        const float mt = fmaxf(m, mx01);
+                        const lphy_frame_meta mg = norm_meta(mx01, true, 0), me = norm_meta(mt, true, 0);
+                        if (nan || fbad || !(mt <= 3.40282347e38f)) {
+                            A.meta[f].status = kStatusFixup;
+                        } else if (me.scale != mg.scale || me.normalised != mg.normalised) {
+                            A.meta[f].cfo = mt;
+                            A.meta[f].time_offset = r;
+                            A.meta[f].status = open ? kStatusSettleRecheck : kStatusSettle;
+                        }
+                    }
+                }
             }
         }
         k = nkk;
@@ -1519,6 +1672,79 @@ __device__ void recheck_frames(const DemodArgs& A, unsigned long long fb, bool m
     if (tid == 0 && done) atomicAdd(&A.counters[0], done);
 }
 
+// Frames k_frames demodulated under a speculative normalisation that the
+// frame's later samples overturned (status kStatusSettle[Recheck]), among the
+// workgroup's frames fb .. fb + kTile - 1 (thread t: frame fb + t, `mine`).
+// Their two estimate symbols are transformed again, T/2 frames per tile, with
+// the exact normalisation (the reference's arithmetic, as exact_frame), and
+// folded into the exact offsets.  The symbols stand when the time shift is
+// unchanged and every certified symbol's lead still covers the larger sample
+// bound and the rate difference: a rate error d moves every bin by at most
+// |d| N sum|y_i| <= |d| N A (the phase error of sample i is |d| i), charged
+// twice on both sides of the comparison as fast_certified charges its B.
+// Otherwise the frame is re-run whole (kStatusFixup).
+template <int SF, int MODE>
+__device__ void settle_frames(const DemodArgs& A, unsigned long long fb, bool mine, PostShared<SF>& sh) {
+    using G = Geo<SF>;
+    constexpr int N = G::N, T = G::T, FPT = T / 2;
+    const int tid = threadIdx.x;
+    const int slot = tid / G::LPS, lam = tid % G::LPS;
+    if (tid == 0) sh.count = 0;
+    __syncthreads();
+    if (mine) sh.list[atomicAdd(&sh.count, 1u)] = (unsigned)tid;
+    __syncthreads();
+    const unsigned n = sh.count;
+    for (unsigned k0 = 0; k0 < n; k0 += FPT) {
+        const unsigned k = k0 + (unsigned)slot / 2, s = (unsigned)slot & 1u;
+        const bool live = k < n;
+        const unsigned long long f = fb + (live ? sh.list[k] : 0u);
+        const lphy_frame_meta m = norm_meta(A.meta[f].cfo, true, 0);  // cfo holds the max-abs
+        const cf32* fr = A.iq + f * A.frame_samples;
+        const Stage<SF> st(slot, lam);
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) {
+            const int i = lam + e * G::LPS;
+            st.put(sh.lds, e, live ? est_sample(A, fr, (unsigned long long)s * N + (unsigned)i, i, N, m) : czero());
+        }
+        __syncthreads();
+        cf32 v[16];
+        fft_tile<SF, false, true>(v, sh.lds, slot, lam, A.tw);
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) sh.lds[G::addr(slot, bin_of<SF>(e, lam))] = v[e];
+        const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), sh.red);
+        __syncthreads();
+        if (lam == 0) sh.units[slot] = live ? unit_result<SF>(sh.lds, slot, best) : UnitResult{0, 0, 0.0f, 0.0f, 0};
+        __syncthreads();
+        if (tid < FPT && k0 + (unsigned)tid < n) {
+            const unsigned long long g = fb + sh.list[k0 + tid];
+            const lphy_frame_meta sm = A.meta[g];
+            lphy_frame_meta e = norm_meta(sm.cfo, true, 0);
+            EstFold fold;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const UnitResult r = sh.units[2 * tid + u];
+                if (r.valid) fold.add(r.idx, r.findex, 0, r.phase);
+                else fold.add(0, 0.0f, 0, 0.0f);
+            }
+            fold.finish(e, 2, N, 1);
+            // amplitude bound of the speculatively scaled samples, and the
+            // smallest bound of any symbol (|start| grows with the symbol)
+            const float a = fmaxf(1.0f, sm.cfo * sm.scale) * 1.0001f;
+            const float b1 = cert_bound<SF>(sm.rate, sm.rate * (float)sm.t_off, 1.0f);
+            const float d = fabsf(e.rate - sm.rate) * (1.0f + 4.0f * kU);
+            const float A1 = (float)N * 1.41421366f * 1.0001f;
+            const bool ok = e.t_off == sm.t_off && sm.t_off >= -N && sm.t_off <= N &&
+                            sm.time_offset > 4.0f * a + 4.0f * d * (float)N * A1 * a / b1;
+            lphy_frame_meta r = e;
+            r.sw0 = sm.sw0;
+            r.sw1 = sm.sw1;
+            r.status = !ok ? kStatusFixup : (sm.status == kStatusSettleRecheck ? kStatusRecheck : 0);
+            A.meta[g] = r;
+        }
+        __syncthreads();
+    }
+}
+
 // Whether frame f holds a symbol left open by k_cuframe, which marks them in
 // the output only (kSymRecheck): its symbols and the sync symbols' record.
 __device__ __forceinline__ bool has_sentinel(const DemodArgs& A, unsigned long long f) {
@@ -1539,7 +1765,13 @@ __global__ __launch_bounds__(kTile) void k_post(DemodArgs A, FinalArgs F, int fi
     __shared__ unsigned fcount;
     const unsigned long long f = (unsigned long long)blockIdx.x * kTile + threadIdx.x;
     if (fix) {
-        const int st = f < A.frames ? A.meta[f].status : 0;
+        int st = f < A.frames ? A.meta[f].status : 0;
+        const bool settle = st == kStatusSettle || st == kStatusSettleRecheck;
+        if (__syncthreads_or(settle)) {
+            settle_frames<SF, MODE>(A, (unsigned long long)blockIdx.x * kTile, settle, sh);
+            __syncthreads();
+            if (f < A.frames) st = A.meta[f].status;
+        }
         const bool fixup = st == kStatusFixup;
         const bool recheck = st == kStatusRecheck || (A.sentinels && f < A.frames && st == 0 && has_sentinel(A, f));
         if (__syncthreads_or(fixup)) {

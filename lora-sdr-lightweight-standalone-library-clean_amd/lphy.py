@@ -31,6 +31,7 @@ F_STAGE_FINAL = 16
 F_UNFUSED = 32  # separate prologue / symbol launches (lphy_hip.h)
 F_EXACT_ROTATION = 64  # fused launch without the certified per-frame rotation table
 F_RESIDENT = 128  # fused launch: single-read CU-resident kernel where it applies (SF 7)
+F_SCAN_FIRST = 256  # fused launch, modes 1/2: whole-frame max-abs pre-scan (no speculation)
 WINDOW_NONE = 0
 WINDOW_HANN = 1
 

@@ -29,6 +29,7 @@ ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--so", default="")
 ap.add_argument("--unfused", action="store_true")
 ap.add_argument("--exact", action="store_true")
+ap.add_argument("--flags", type=int, default=0, help="extra LPHY_F_* bits (e.g. 256 = SCAN_FIRST)")
 ap.add_argument("--check", action="store_true", help="compare outputs across builds")
 ap.add_argument("--rounds", type=int, default=1, help="interleave the builds this many times")
 a = ap.parse_args()
@@ -46,6 +47,7 @@ if a.unfused:
     flags |= lphy.F_UNFUSED
 if a.exact:
     flags |= lphy.F_EXACT_ROTATION
+flags |= a.flags
 ref = {}
 dems = []
 for so in sos:

@@ -21,7 +21,7 @@ def build(sf, specs):
         cmd = (f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off "
                f"-fno-slp-vectorize -fPIC -shared -DLPHY_SF={sf} {flags} -I{ROOT}/include "
                f"-I{PKG}/csrc -o {so} {PKG}/csrc/lphy_hip.hip {PKG}/csrc/lphy_sf.hip "
-               f"{PKG}/csrc/lphy_stream.hip")
+               f"{PKG}/csrc/lphy_stream.hip {PKG}/csrc/lphy_codes.hip {PKG}/csrc/lphy_lorawan.hip")
         procs.append((name, subprocess.Popen(cmd, shell=True)))
     for name, p in procs:
         assert p.wait() == 0, name
