@@ -218,7 +218,8 @@ def measured_traffic(kernel: str, frames: int):
         except ValueError:
             continue
         k = d.get("kernels", {}).get(kernel)
-        if k and d.get("frames") == frames:
+        # the bench's mode (2) only; summaries without the HBM passes skipped
+        if k and "hbm_bytes_per_launch" in k and d.get("frames") == frames and d.get("mode", 2) == 2:
             best = {"bytes": k["hbm_bytes_per_launch"], "source": f"{f.name}"}
     return best
 

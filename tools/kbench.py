@@ -29,6 +29,7 @@ ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--so", default="")
 ap.add_argument("--unfused", action="store_true")
 ap.add_argument("--exact", action="store_true")
+ap.add_argument("--burst", action="store_true", help="time the reps back-to-back (one event pair)")
 ap.add_argument("--flags", type=int, default=0, help="extra LPHY_F_* bits (e.g. 256 = SCAN_FIRST)")
 ap.add_argument("--check", action="store_true", help="compare outputs across builds")
 ap.add_argument("--rounds", type=int, default=1, help="interleave the builds this many times")
@@ -69,7 +70,16 @@ for r in range(a.rounds):
             torch.cuda.synchronize()
             d.recheck_count(reset=True)
             ts = []
-            for _ in range(a.reps):
+            if a.burst:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.reps):
+                    d.demod_batch(iq, a.frames, fs, out, meta, mode, flags, payload=pl, stream=st)
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1) / a.reps)
+            for _ in range(0 if a.burst else a.reps):
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record()

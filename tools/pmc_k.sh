@@ -14,5 +14,6 @@ run_pass() {
 }
 run_pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES && \
 run_pass wait SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES GRBM_GUI_ACTIVE && \
-run_pass fetch FETCH_SIZE
+run_pass fetch FETCH_SIZE && \
+run_pass write WRITE_SIZE
 echo "pmc rc=$?"

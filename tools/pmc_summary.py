@@ -2,7 +2,8 @@
 per kernel, HBM bytes per launch = FETCH_SIZE x 2 (gfx950 reports half of a
 wide streaming read, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, both in KiB
 in rocprofv3's output; plus the SQ counters when those passes ran.
-Usage: python tools/pmc_summary.py <pmc dir> <tag> <frames> <sf>"""
+Usage: python tools/pmc_summary.py <pmc dir> <tag> <frames> <sf> [dest dir] [mode]
+(mode: the lphy mode the passes ran, default 2 = the bench's)"""
 import csv
 import json
 import re
@@ -30,7 +31,8 @@ def load(d: Path):
 def main():
     d, tag, frames, sf = Path(sys.argv[1]), sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
     acc, n = load(d)
-    out = {"tag": tag, "frames": frames, "sf": sf, "source": str(d), "kernels": {}}
+    mode = int(sys.argv[6]) if len(sys.argv) > 6 else 2
+    out = {"tag": tag, "frames": frames, "sf": sf, "mode": mode, "source": str(d), "kernels": {}}
     for k, c in acc.items():
         if not k.startswith("k_"):
             continue
