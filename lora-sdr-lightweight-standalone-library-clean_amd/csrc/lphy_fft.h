@@ -342,14 +342,16 @@ __device__ __forceinline__ void lds_st(cf32* lds, int byte_off, cf32 v) {
     *reinterpret_cast<cf32*>(reinterpret_cast<char*>(lds) + byte_off) = v;
 }
 
-template <int SF, int PI, bool LAST, bool TRIV, bool AG>
+template <int SF, int PI, bool LAST, bool TRIV, bool AG, bool REG0 = false>
 __device__ __forceinline__ void run_pass(cf32 (&v)[16], cf32* lds, int slot, int lam,
                                          const cf32* __restrict__ tw) {
     using G = Geo<SF>;
     constexpr Passes<SF> PS{};
     constexpr int HI = PS.hi[PI], LO = PS.lo[PI];
     using Gr = Group<SF, HI, LO>;
-    if (PI == 0) {
+    if (PI == 0 && REG0) {
+        // inputs already in registers, in first-pass order (first_pass_index)
+    } else if (PI == 0) {
         const int lb8 = G::lbase(slot, Gr::inidx(0, lam)) << 3;
 #pragma unroll
         for (int e = 0; e < G::E; ++e) v[e] = lds_ld(lds, G::at8(lb8, G::cpart(Gr::inidx(e, 0)) << 3));
@@ -368,13 +370,13 @@ __device__ __forceinline__ void run_pass(cf32 (&v)[16], cf32* lds, int slot, int
     }
 }
 
-template <int SF, int PI, bool TRIV, bool AG>
+template <int SF, int PI, bool TRIV, bool AG, bool REG0 = false>
 __device__ __forceinline__ void run_passes(cf32 (&v)[16], cf32* lds, int slot, int lam,
                                            const cf32* __restrict__ tw) {
     constexpr Passes<SF> PS{};
     if constexpr (PI < PS.n) {
-        run_pass<SF, PI, PI == PS.n - 1, TRIV, AG>(v, lds, slot, lam, tw);
-        run_passes<SF, PI + 1, TRIV, AG>(v, lds, slot, lam, tw);
+        run_pass<SF, PI, PI == PS.n - 1, TRIV, AG, REG0>(v, lds, slot, lam, tw);
+        run_passes<SF, PI + 1, TRIV, AG, false>(v, lds, slot, lam, tw);
     }
 }
 
@@ -383,10 +385,21 @@ __device__ __forceinline__ void run_passes(cf32 (&v)[16], cf32* lds, int slot, i
 // thread of the tile (contains barriers).
 // TRIV: see pass_butterflies (magnitude-only consumers).
 // AG: every product with the reference's Annex G recovery (cmul_x).
-template <int SF, bool TRIV = false, bool AG = false>
+// REG0: v already holds the symbol's samples in first-pass order (element e
+// = sample first_pass_index<SF>(e, lam)), so the transform starts without the
+// natural-order LDS staging round trip.
+template <int SF, bool TRIV = false, bool AG = false, bool REG0 = false>
 __device__ __forceinline__ void fft_tile(cf32 (&v)[16], cf32* lds, int slot, int lam,
                                          const cf32* __restrict__ tw) {
-    run_passes<SF, 0, TRIV, AG>(v, lds, slot, lam, tw);
+    run_passes<SF, 0, TRIV, AG, REG0>(v, lds, slot, lam, tw);
+}
+
+// Sample index that element e of lane lam holds at the start of the first
+// pass (KISS leaf permutation): lane part | compile-time part.
+template <int SF>
+__host__ __device__ constexpr int first_pass_index(int e, int lam) {
+    constexpr Passes<SF> PS{};
+    return Group<SF, PS.hi[0], PS.lo[0]>::inidx(e, lam);
 }
 
 // Whether any of the lane's bins has a NaN part: the trigger for re-running

@@ -998,37 +998,41 @@ __device__ __forceinline__ bool fast_certified(const ArgMax2& b, const SymCtx& c
 // stage_mixed (no rotation).  Returns the lane's max(|Re y|, |Im y|) over its
 // symbol samples: mode 0's certificate amplitude, and for modes 1/2 the
 // samples' share of the frame's max-abs (speculative normalisation).
+//
+// The samples are held in first-pass order (element e of lane lam is sample
+// fl + first_pass_index<SF>(e, 0), fl = the lane part): the staged values
+// stay in registers and the transform starts there (fft_tile REG0).
 template <int SF, int MODE, bool MIXED>
-__device__ __forceinline__ float stage_fast(cf32* lds, const Stage<SF>& stg, const cf32 (&raw)[16],
-                                            const SymCtx& c, int lam, const cf32* down,
-                                            const float* win, const cf32* rt,
+__device__ __forceinline__ float stage_fast(cf32 (&v)[16], const cf32 (&raw)[16], const SymCtx& c, int fl,
+                                            const cf32* down, const float* win, const cf32* rt,
                                             const cf32 (&rreg)[16], bool est) {
     using G = Geo<SF>;
     constexpr int N = G::N;
     constexpr bool RLDS = SF <= 8;
     float amax = 0.0f;
-    const cf32* dl = down + (c.base & (N - 1)) + lam;
+    const cf32* dl = down + (c.base & (N - 1)) + fl;  // doubled table: no wrap
+    const cf32* rtl = rt + fl;
+    const float* wl = win + fl;
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
-        const int i = lam + e * G::LPS;
+        const int ce = first_pass_index<SF>(e, 0);
         const cf32 x = raw[e];
         cf32 y;
         if (MIXED && est) {
             cf32 p = x;
             if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) {
-                if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
-                    p = cmul(p, down[((unsigned)c.base + (unsigned)i) & (N - 1)]);
+                if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) p = cmul(p, dl[ce]);
                 p = cscale(p, c.scale);
             }
             y = c.ok ? p : czero();
-            if constexpr ((MODE & kWinBit) != 0) y = cscale(y, win[i]);
+            if constexpr ((MODE & kWinBit) != 0) y = cscale(y, wl[ce]);
         } else {
             cf32 p = x;
-            if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) p = cmul(x, dl[e * G::LPS]);
+            if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) p = cmul(x, dl[ce]);
             amax = max3_abs(amax, p.x, p.y);
-            y = cmul_fma(p, RLDS ? rt[i] : rreg[e]);
+            y = cmul_fma(p, RLDS ? rtl[ce] : rreg[e]);
         }
-        stg.put(lds, e, y);
+        v[e] = y;
     }
     return amax;
 }
@@ -1076,7 +1080,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     const int lane = tid & 63, wv = tid >> 6;
     const int slot = tid / G::LPS, lam = tid % G::LPS;
     const unsigned wslot = (unsigned)(slot % WT);
-    const Stage<SF> stg(slot, lam);
+    const int fl = first_pass_index<SF>(0, lam);  // lane part of the sample index
     const unsigned nframes = (unsigned)A.frames;
     const unsigned S = (unsigned)A.total_syms, SL = U + S;
     // offset of E(k+1) inside slice k: as late as the two-tile lead over
@@ -1175,11 +1179,11 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         }
     };
     scan_ahead(kind, fk);
-    cf32 raw[16];
+    cf32 raw[16];  // the next unit's samples, first-pass order
     {
-        const cf32* src = A.iq + (unsigned long long)c.f * A.frame_samples + c.base;
+        const cf32* src = A.iq + (unsigned long long)c.f * A.frame_samples + c.base + fl;
 #pragma unroll
-        for (int e = 0; e < G::E; ++e) raw[e] = src[lam + e * G::LPS];
+        for (int e = 0; e < G::E; ++e) raw[e] = src[first_pass_index<SF>(e, 0)];
     }
     cf32 rreg[16];                 // SF 9-10: the team's table ...
     unsigned rreg_fk = 0xffffffffu;  // ... of this frame
@@ -1191,12 +1195,13 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     unsigned sp_fl0 = 0u, sp_fl1 = 0u;
 
     for (unsigned t = 0; t < ntiles; ++t) {
+        cf32 v[16];  // this tile's unit: staged samples, then its bins
         // SF 9-10: a team entering a new frame builds its table entries
         if constexpr (!RLDS) {
             if (kind == kUnitSym && fk != rreg_fk) {
 #pragma unroll
                 for (int e = 0; e < G::E; ++e) {
-                    const int i = lam + e * G::LPS;
+                    const int i = fl + first_pass_index<SF>(e, 0);
                     float sn, cs;
                     lphy_libm::sincosf_exact(c.rate * (float)i, &sn, &cs);
                     cf32 tv = cf32{cs, sn};
@@ -1224,9 +1229,9 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
                 }
                 c.ok = c.live;  // estimate this unit (else stage zeros)
             }
-            amax = stage_fast<SF, MODE, true>(lds, stg, raw, c, lam, down, win, rt, rreg, kind != kUnitSym);
+            amax = stage_fast<SF, MODE, true>(v, raw, c, fl, down, win, rt, rreg, kind != kUnitSym);
         } else {
-            amax = stage_fast<SF, MODE, false>(lds, stg, raw, c, lam, down, win, rt, rreg, false);
+            amax = stage_fast<SF, MODE, false>(v, raw, c, fl, down, win, rt, rreg, false);
         }
         if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) {
 #pragma unroll
@@ -1258,17 +1263,16 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         if (t + 1 < ntiles) scan_ahead(nkind, nfk);
         const SymCtx nc = ctx_of(nkind, nfk, nsu);
         if (t + 1 < ntiles) {
-            const cf32* nsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base;
+            const cf32* nsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base + fl;
 #pragma unroll
-            for (int e = 0; e < G::E; ++e) raw[e] = nsrc[lam + e * G::LPS];
+            for (int e = 0; e < G::E; ++e) raw[e] = nsrc[first_pass_index<SF>(e, 0)];
         }
 
-        cf32 v[16];
         // tiles of symbol units only: magnitude-only transform (fft_tile TRIV)
         // (measured alternative: a packed-key max/min tournament for the top
         // two, 3 % slower than this ordered scan)
-        if (emask) fft_tile<SF>(v, lds, slot, lam, twl);
-        else fft_tile<SF, true>(v, lds, slot, lam, twl);
+        if (emask) fft_tile<SF, false, false, true>(v, lds, slot, lam, twl);
+        else fft_tile<SF, true, false, true>(v, lds, slot, lam, twl);
         const ArgMax2 b2 = symbol_argmax2<SF>(local_argmax2<SF>(v, lam));
         ArgMax best{b2.v, b2.i};
         if (emask) {
