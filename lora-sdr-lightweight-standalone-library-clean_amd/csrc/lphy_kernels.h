@@ -789,12 +789,14 @@ __device__ __forceinline__ float wave_maxabs(const DemodArgs& A, unsigned f, con
         bad |= !(__builtin_isfinite(x.x) && __builtin_isfinite(x.y));
         maxabs_acc(mx, x);
     };
-    // loads in flight per lane (measured at SF7: 16, 24, 32 and 33 - two
-    // rounds per 66-symbol frame - within 1 %; 16 spills least)
+    // loads in flight per lane (round 1, whole-frame scan at SF7: 16, 24,
+    // 32 and 33 within 1 %; round 2, with the samples staged in registers:
+    // 8 spills 6 VGPRs where 16 spills 15, 4 % faster under speculation and
+    // 1 % with the whole-frame scan)
 #ifdef LPHY_MAXABS_U
     constexpr int U = LPHY_MAXABS_U;
 #else
-    constexpr int U = 16;
+    constexpr int U = 8;
 #endif
     // chirp index of sample 2 (b + 64 u + lane) for a round base b = 64 U r:
     // the 128 U r term vanishes mod N
