@@ -535,7 +535,9 @@ __device__ __forceinline__ ArgMax2 local_argmax2(const cf32 (&v)[16], int lam) {
         const int e = BO.e[k];
         const cf32 sq = v[e] * v[e];
         const float m2 = sq.x + sq.y;
-        best.v2 = fmaxf(best.v2, fminf(m2, best.v));
+        // runner-up = max(v2, min(m2, v)) = med3(v, v2, m2) as v >= v2 (one
+        // v_med3; a NaN m2 only arises with every bin NaN, where v stays 0)
+        best.v2 = __builtin_amdgcn_fmed3f(best.v, best.v2, m2);
         const bool take = m2 > best.v;
         best.v = take ? m2 : best.v;
         best.i = take ? (lane_bin | bin_of<SF>(e, 0)) : best.i;
