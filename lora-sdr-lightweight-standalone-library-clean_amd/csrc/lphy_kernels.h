@@ -1015,26 +1015,30 @@ __device__ __forceinline__ float stage_fast(cf32 (&v)[16], const cf32 (&raw)[16]
     const cf32* dl = down + (c.base & (N - 1)) + fl;  // doubled table: no wrap
     const cf32* rtl = rt + fl;
     const float* wl = win + fl;
+    // one branch per tile, not per element (per-element branches serialise
+    // the table reads behind their own waits)
+    if (MIXED && est) {
 #pragma unroll
-    for (int e = 0; e < G::E; ++e) {
-        const int ce = first_pass_index<SF>(e, 0);
-        const cf32 x = raw[e];
-        cf32 y;
-        if (MIXED && est) {
-            cf32 p = x;
+        for (int e = 0; e < G::E; ++e) {
+            const int ce = first_pass_index<SF>(e, 0);
+            cf32 p = raw[e];
             if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) {
                 if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) p = cmul(p, dl[ce]);
                 p = cscale(p, c.scale);
             }
-            y = c.ok ? p : czero();
+            cf32 y = c.ok ? p : czero();
             if constexpr ((MODE & kWinBit) != 0) y = cscale(y, wl[ce]);
-        } else {
-            cf32 p = x;
-            if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) p = cmul(x, dl[ce]);
-            amax = max3_abs(amax, p.x, p.y);
-            y = cmul_fma(p, RLDS ? rtl[ce] : rreg[e]);
+            v[e] = y;
         }
-        v[e] = y;
+    } else {
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) {
+            const int ce = first_pass_index<SF>(e, 0);
+            cf32 p = raw[e];
+            if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) p = cmul(p, dl[ce]);
+            amax = max3_abs(amax, p.x, p.y);
+            v[e] = cmul_fma(p, RLDS ? rtl[ce] : rreg[e]);
+        }
     }
     return amax;
 }
