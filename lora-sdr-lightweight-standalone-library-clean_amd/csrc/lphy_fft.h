@@ -565,4 +565,39 @@ __device__ __forceinline__ ArgMax2 symbol_argmax2(ArgMax2 a) {
     return a;
 }
 
+// Workgroup form for teams spanning wavefronts (LPS > 64: SF 11-12): the
+// waves reduce in registers, then combine through `red` (one entry per wave;
+// contains barriers, every thread of the tile calls it).
+template <int SF>
+__device__ __forceinline__ ArgMax2 symbol_argmax2_wg(ArgMax2 a, ArgMax2* red) {
+    using G = Geo<SF>;
+    static_assert(G::LPS > 64, "teams inside one wavefront use symbol_argmax2");
+    auto comb = [](ArgMax2 x, ArgMax2 o) __attribute__((always_inline)) {
+        x.v2 = fmaxf(fmaxf(x.v2, o.v2), fminf(x.v, o.v));
+        const bool take = (o.v > x.v) | ((o.v == x.v) & (o.i < x.i));
+        x.v = take ? o.v : x.v;
+        x.i = take ? o.i : x.i;
+        return x;
+    };
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        ArgMax2 o;
+        o.v = __shfl_xor(a.v, off, 64);
+        o.i = __shfl_xor(a.i, off, 64);
+        o.v2 = __shfl_xor(a.v2, off, 64);
+        a = comb(a, o);
+    }
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[wave] = a;
+    __syncthreads();
+    constexpr int WPS = G::LPS / 64;
+    const int first = (wave / WPS) * WPS;
+    ArgMax2 b = red[first];
+#pragma unroll
+    for (int w = 1; w < WPS; ++w) b = comb(b, red[first + w]);
+    __syncthreads();
+    if (!(b.v > 0.0f)) b.i = 0;
+    return b;
+}
+
 }  // namespace lphy

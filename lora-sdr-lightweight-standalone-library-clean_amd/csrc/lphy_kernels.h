@@ -573,6 +573,72 @@ __device__ __forceinline__ void store_symbol(const DemodArgs& A, const SymCtx& c
     }
 }
 
+// (shared by k_demod's fast path and k_frames; see the certified fast
+// rotation comment below k_frames' max-abs scan)
+__device__ __forceinline__ float max3_abs(float m, float a, float b) {
+    float r;
+    asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
+
+constexpr float kU = 5.9604645e-8f;  // 2^-24
+
+// Table of frame `rec` (rate, scale, t_off): t_i for i = lane, lane+64, ...
+template <int SF, int MODE>
+__device__ __forceinline__ void build_rtab(cf32* tab, float rate, float scale, int t_off,
+                                           const cf32* down, const float* win, int lane) {
+    constexpr int N = 1 << SF;
+    (void)t_off;
+    for (int i = lane; i < N; i += 64) {
+        float sn, cs;
+        lphy_libm::sincosf_exact(rate * (float)i, &sn, &cs);
+        cf32 t = cf32{cs, sn};
+        if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) t = cmul(down[i], t);
+        if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) t = cscale(t, scale);
+        if constexpr ((MODE & kWinBit) != 0) t = cscale(t, win[i]);
+        tab[i] = t;
+    }
+}
+
+// Whether the fast path may take this symbol unit: every window (mode 2
+// dechirps each sample exactly at its own chirp index before the table).
+template <int SF, int MODE>
+__device__ __forceinline__ bool fast_applies(const SymCtx& c, int t_off) {
+    (void)c;
+    (void)t_off;
+    return true;
+}
+
+// The certificate of the header comment.  amax bounds max(|Re y|, |Im y|)
+// over the symbol's samples before rotation (modes 1/2: <= 1 after the
+// frame's normalisation; mode 0: measured).
+//
+// Range guards keep every rounding relative: amax >= 1e-20 (denormal
+// arithmetic stays negligible against B), b.v >= 1e-30 (a normal |X|^2), and
+// a runner-up below 1e-30 is taken as 1e-30.
+// extra: further u-multiples of a sample's rotation error (the two-table
+// rotation of k_demod's fast path)
+template <int SF>
+__device__ __forceinline__ float cert_bound(float rate, float start, float amax, float extra = 0.0f) {
+    constexpr int N = 1 << SF, L = (SF + 1) / 2;
+    const float A = (float)N * 1.41421366f * amax * 1.0001f;
+    const float ar = fabsf(rate) * (float)N;
+    const float P = fabsf(start) + ar;
+    return kU * A * ((24.0f + 12.0f * L + extra) + 2.0f * ar + P) * 1.001f;
+}
+// winner's lead over the runner-up, less the |X|^2 roundings
+__device__ __forceinline__ float cert_gap(const ArgMax2& b) {
+    return sqrtf(b.v) * (1.0f - 8.0f * kU) - sqrtf(fmaxf(b.v2, 1e-30f)) * (1.0f + 8.0f * kU);
+}
+template <int SF>
+__device__ __forceinline__ bool fast_certified(const ArgMax2& b, const SymCtx& c, float amax,
+                                               float extra = 0.0f) {
+    constexpr int N = 1 << SF;
+    const float A = (float)N * 1.41421366f * amax * 1.0001f;
+    const float B = cert_bound<SF>(c.rate, c.start, amax, extra);
+    return cert_gap(b) > 4.0f * B && A < 1e18f && amax >= 1e-20f && b.v >= 1e-30f;
+}
+
 // Stage 2: per-symbol demodulation, persistent grid.  The workgroup stages
 // the twiddles (and, up to N = 1024, the down-chirp and window) in LDS once.
 //  * SF <= 10 (a symbol's LPS <= 64 lanes sit in one wavefront): every
@@ -580,6 +646,12 @@ __device__ __forceinline__ void store_symbol(const DemodArgs& A, const SymCtx& c
 //    workgroup barrier in its loop; it software-pipelines the next tile's
 //    frame record (during staging) and IQ (during the FFT).
 //  * SF 11-12: workgroup tiles with barriers (a symbol spans wavefronts).
+//    Symbols take the certified fast rotation (as k_frames) with
+//    a two-table rotation: e^{j rate i} = e^{j rate 64h} e^{j rate l} for
+//    i = 64h + l, whose 64 + N/64 entries the team computes per tile (exact
+//    sincos) instead of one sincos per sample; uncertified symbols are left
+//    to k_post (kSymRecheck, kStatusRecheck).  LPHY_F_EXACT_ROTATION and
+//    osr > 1 keep the per-sample rotation.
 template <int SF, int MODE, int OCC>
 __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
     using G = Geo<SF>;
@@ -587,11 +659,18 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
     constexpr bool TAB = N <= 1024;  // chirp + window tables in LDS
     constexpr bool WAVE = G::LPS <= 64;
     constexpr int WT = WAVE ? 64 / G::LPS : G::T;  // symbols per worker tile
+    constexpr bool FASTB = !WAVE && (MODE & kOsrBit) == 0;  // two-table fast path
+    constexpr int NH = N / 64;                               // high-part entries
     __shared__ cf32 lds[G::T * G::SSTRIDE];
     __shared__ cf32 twl[N];
     __shared__ cf32 dnl[TAB ? N : 1];
     __shared__ float wnl[TAB ? N : 1];
     __shared__ ArgMax red[kTile / 64];
+    __shared__ ArgMax2 red2[FASTB ? kTile / 64 : 1];
+    __shared__ float redm[FASTB ? kTile / 64 : 1];
+    __shared__ cf32 thi[FASTB ? G::T : 1][FASTB ? NH : 1];
+    __shared__ cf32 tlo[FASTB ? G::T : 1][FASTB ? 64 : 1];
+    const bool fastb = FASTB && !A.exact_rotation;
 
     const int tid = threadIdx.x;
     for (int i = tid; i < N; i += kTile) {
@@ -653,8 +732,42 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
         const lphy_frame_meta nm = A.meta[nlive ? nf : 0];
 
         if constexpr (!WAVE) __syncthreads();  // previous tile's readers done
-        stage_symbol<SF, MODE>(lds, stg, raw, A.iq + (unsigned long long)c.f * A.frame_samples + c.base,
-                               c, lam, down, win, (int)osr);
+        float amax = 0.0f;  // fast path, mode 0: the team's max(|Re x|, |Im x|)
+        if (FASTB && fastb) {
+            // the symbol's two rotation tables (scale folded into the low one)
+            if (c.ok) {
+                float sn, cs;
+                if (lam < NH) {
+                    lphy_libm::sincosf_exact(c.rate * (float)(64 * lam), &sn, &cs);
+                    thi[slot][lam] = cf32{cs, sn};
+                } else if (lam < NH + 64) {
+                    const int l = lam - NH;
+                    lphy_libm::sincosf_exact(c.rate * (float)l, &sn, &cs);
+                    cf32 t = cf32{cs, sn};
+                    if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) t = cscale(t, c.scale);
+                    tlo[slot][l] = t;
+                }
+            }
+            __syncthreads();
+            const cf32 tl = tlo[slot][lam & 63];
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) {
+                const int i = lam + e * G::LPS;
+                cf32 p = raw[e];
+                if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) {
+                    amax = max3_abs(amax, p.x, p.y);
+                    p = cmul(p, down[i]);
+                }
+                if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+                    p = cmul(p, down[(c.base + (unsigned)i) & (N - 1)]);
+                cf32 q = cmul_fma(cmul_fma(p, tl), thi[slot][(lam >> 6) + e * (G::LPS / 64)]);
+                if constexpr ((MODE & kWinBit) != 0) q = cscale(q, win[i]);
+                stg.put(lds, e, c.ok ? q : czero());
+            }
+        } else {
+            stage_symbol<SF, MODE>(lds, stg, raw, A.iq + (unsigned long long)c.f * A.frame_samples + c.base,
+                                   c, lam, down, win, (int)osr);
+        }
         team_sync<SF>();
 #ifdef LPHY_PROFILE_PHASES
         const unsigned long long p1 = clock64();
@@ -682,8 +795,37 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
             for (int e = 0; e < G::E; ++e) v[e] = lds_ld(lds, G::at8(st2.lb8, G::cpart(e * G::LPS) << 3));
         }
 #else
-        fft_tile<SF>(v, lds, slot, lam, twl);
+        if (FASTB && fastb) fft_tile<SF, true>(v, lds, slot, lam, twl);
+        else fft_tile<SF>(v, lds, slot, lam, twl);
 #endif
+        if constexpr (FASTB) {
+            if (fastb) {
+                // certificate (fast_certified, with the two-table rotation's
+                // further 6u); a NaN or near-tie leaves the symbol to k_post
+                const ArgMax2 b2 = symbol_argmax2_wg<SF>(local_argmax2<SF>(v, lam), red2);
+                float am = 1.0f;  // modes 1/2: normalised frame
+                if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) {
+#pragma unroll
+                    for (int off = 32; off >= 1; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
+                    if ((tid & 63) == 0) redm[tid >> 6] = amax;
+                    __syncthreads();
+                    constexpr int WPS = G::LPS / 64;
+                    const int first = ((tid >> 6) / WPS) * WPS;
+                    am = redm[first];
+#pragma unroll
+                    for (int w = 1; w < WPS; ++w) am = fmaxf(am, redm[first + w]);
+                    __syncthreads();
+                }
+                const bool redo = !fast_certified<SF>(b2, c, am, 6.0f);
+                if (c.ok && lam == 0) {
+                    store_symbol(A, c, redo ? kSymRecheck : (uint16_t)b2.i);
+                    if (redo) A.meta[c.f].status = kStatusRecheck;
+                }
+                c = nc;
+                f = nf; s = ns; fw = nfw; sw = nsw;
+                continue;
+            }
+        }
         // a NaN bin may hide a (NaN, NaN) product, where the reference's
         // Annex G product differs: the frame goes to the exact re-run
         if (fft_has_nan<SF>(v) && c.ok) A.meta[c.f].status = kStatusFixup;
@@ -767,11 +909,6 @@ __device__ __forceinline__ void meta_put_est(lphy_frame_meta* dst, const lphy_fr
 // sample) v_max3 does not have.  In mode 2 only the whole symbols are
 // scanned: the zeros the reference's dechirp leaves past them never raise
 // the maximum.
-__device__ __forceinline__ float max3_abs(float m, float a, float b) {
-    float r;
-    asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
-    return r;
-}
 
 template <int SF, int MODE>
 __device__ __forceinline__ float wave_maxabs(const DemodArgs& A, unsigned f, const cf32* down,
@@ -938,60 +1075,6 @@ enum : int { kUnitDead = 0, kUnitEst = 1, kUnitSym = 2 };
 // time shift is not applied to every symbol - is recomputed with the exact
 // per-sample path.  The check below uses 4B (a factor 2 of slack).
 // ---------------------------------------------------------------------------
-constexpr float kU = 5.9604645e-8f;  // 2^-24
-
-// Table of frame `rec` (rate, scale, t_off): t_i for i = lane, lane+64, ...
-template <int SF, int MODE>
-__device__ __forceinline__ void build_rtab(cf32* tab, float rate, float scale, int t_off,
-                                           const cf32* down, const float* win, int lane) {
-    constexpr int N = 1 << SF;
-    (void)t_off;
-    for (int i = lane; i < N; i += 64) {
-        float sn, cs;
-        lphy_libm::sincosf_exact(rate * (float)i, &sn, &cs);
-        cf32 t = cf32{cs, sn};
-        if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) t = cmul(down[i], t);
-        if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) t = cscale(t, scale);
-        if constexpr ((MODE & kWinBit) != 0) t = cscale(t, win[i]);
-        tab[i] = t;
-    }
-}
-
-// Whether the fast path may take this symbol unit: every window (mode 2
-// dechirps each sample exactly at its own chirp index before the table).
-template <int SF, int MODE>
-__device__ __forceinline__ bool fast_applies(const SymCtx& c, int t_off) {
-    (void)c;
-    (void)t_off;
-    return true;
-}
-
-// The certificate of the header comment.  amax bounds max(|Re y|, |Im y|)
-// over the symbol's samples before rotation (modes 1/2: <= 1 after the
-// frame's normalisation; mode 0: measured).
-//
-// Range guards keep every rounding relative: amax >= 1e-20 (denormal
-// arithmetic stays negligible against B), b.v >= 1e-30 (a normal |X|^2), and
-// a runner-up below 1e-30 is taken as 1e-30.
-template <int SF>
-__device__ __forceinline__ float cert_bound(float rate, float start, float amax) {
-    constexpr int N = 1 << SF, L = (SF + 1) / 2;
-    const float A = (float)N * 1.41421366f * amax * 1.0001f;
-    const float ar = fabsf(rate) * (float)N;
-    const float P = fabsf(start) + ar;
-    return kU * A * ((24.0f + 12.0f * L) + 2.0f * ar + P) * 1.001f;
-}
-// winner's lead over the runner-up, less the |X|^2 roundings
-__device__ __forceinline__ float cert_gap(const ArgMax2& b) {
-    return sqrtf(b.v) * (1.0f - 8.0f * kU) - sqrtf(fmaxf(b.v2, 1e-30f)) * (1.0f + 8.0f * kU);
-}
-template <int SF>
-__device__ __forceinline__ bool fast_certified(const ArgMax2& b, const SymCtx& c, float amax) {
-    constexpr int N = 1 << SF;
-    const float A = (float)N * 1.41421366f * amax * 1.0001f;
-    const float B = cert_bound<SF>(c.rate, c.start, amax);
-    return cert_gap(b) > 4.0f * B && A < 1e18f && amax >= 1e-20f && b.v >= 1e-30f;
-}
 
 // Fast staging of one tile: symbol units q_i = y_i * t_i from the frame's
 // rotation table t (LDS ring for SF <= 8, the lane's registers above) with a
