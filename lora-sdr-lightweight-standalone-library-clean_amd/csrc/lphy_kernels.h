@@ -1090,7 +1090,7 @@ enum : int { kUnitDead = 0, kUnitEst = 1, kUnitSym = 2 };
 template <int SF, int MODE, bool MIXED>
 __device__ __forceinline__ float stage_fast(cf32 (&v)[16], const cf32 (&raw)[16], const SymCtx& c, int fl,
                                             const cf32* down, const float* win, const cf32* rt,
-                                            const cf32 (&rreg)[16], bool est) {
+                                            const cf32* thl, bool est) {
     using G = Geo<SF>;
     constexpr int N = G::N;
     constexpr bool RLDS = SF <= 8;
@@ -1120,7 +1120,17 @@ __device__ __forceinline__ float stage_fast(cf32 (&v)[16], const cf32 (&raw)[16]
             cf32 p = raw[e];
             if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) p = cmul(p, dl[ce]);
             amax = max3_abs(amax, p.x, p.y);
-            v[e] = cmul_fma(p, RLDS ? rtl[ce] : rreg[e]);
+            if constexpr (RLDS) {
+                v[e] = cmul_fma(p, rtl[ce]);
+            } else {
+                // SF 9-10: two-table rotation (build_rtab2): thl[0..63] the low
+                // part e^{j rate l} [* scale], thl[64..] the high part
+                const int i = fl + ce;
+                if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) p = cmul(p, down[i]);
+                cf32 q = cmul_fma(cmul_fma(p, thl[i & 63]), thl[64 + (i >> 6)]);
+                if constexpr ((MODE & kWinBit) != 0) q = cscale(q, win[i]);
+                v[e] = q;
+            }
         }
     }
     return amax;
@@ -1153,6 +1163,9 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     __shared__ float4 ring[WPB][3];  // frame records: rate, scale, t_off, flags
     __shared__ float ringmx[WPB][3];  // ... and the max-abs their normalisation used
     __shared__ cf32 rtab[RLDS ? WPB : 1][2][RLDS ? N : 1];
+    // SF 9-10: two-table rotation per frame (64 low + N/64 high entries): a
+    // whole-symbol table per lane cost 32 VGPRs and spilled
+    __shared__ cf32 rtab2[RLDS ? 1 : WPB][2][RLDS ? 1 : 64 + N / 64];
 
     const int tid = threadIdx.x;
     for (int i = tid; i < N; i += kTile) {
@@ -1274,8 +1287,6 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
 #pragma unroll
         for (int e = 0; e < G::E; ++e) raw[e] = src[first_pass_index<SF>(e, 0)];
     }
-    cf32 rreg[16];                 // SF 9-10: the team's table ...
-    unsigned rreg_fk = 0xffffffffu;  // ... of this frame
     // speculative normalisation: the lane's running state for the two frames
     // whose symbols can be in flight (by parity of the frame): max-abs of the
     // symbol samples, least certificate ratio, flags (1 NaN, 2 symbol open)
@@ -1285,24 +1296,8 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
 
     for (unsigned t = 0; t < ntiles; ++t) {
         cf32 v[16];  // this tile's unit: staged samples, then its bins
-        // SF 9-10: a team entering a new frame builds its table entries
-        if constexpr (!RLDS) {
-            if (kind == kUnitSym && fk != rreg_fk) {
-#pragma unroll
-                for (int e = 0; e < G::E; ++e) {
-                    const int i = fl + first_pass_index<SF>(e, 0);
-                    float sn, cs;
-                    lphy_libm::sincosf_exact(c.rate * (float)i, &sn, &cs);
-                    cf32 tv = cf32{cs, sn};
-                    if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) tv = cmul(down[i], tv);
-                    if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) tv = cscale(tv, c.scale);
-                    if constexpr ((MODE & kWinBit) != 0) tv = cscale(tv, win[i]);
-                    rreg[e] = tv;
-                }
-                rreg_fk = fk;
-            }
-        }
         const cf32* rt = rtab[RLDS ? wv : 0][RLDS ? (fk & 1) : 0];
+        const cf32* thl = rtab2[RLDS ? 0 : wv][RLDS ? 0 : (fk & 1)];
         // estimate units in this tile (all of one frame): its max-abs first
         const unsigned long long emask = __ballot(kind == kUnitEst);
         unsigned ke = 0;
@@ -1318,9 +1313,9 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
                 }
                 c.ok = c.live;  // estimate this unit (else stage zeros)
             }
-            amax = stage_fast<SF, MODE, true>(v, raw, c, fl, down, win, rt, rreg, kind != kUnitSym);
+            amax = stage_fast<SF, MODE, true>(v, raw, c, fl, down, win, rt, thl, kind != kUnitSym);
         } else {
-            amax = stage_fast<SF, MODE, false>(v, raw, c, fl, down, win, rt, rreg, false);
+            amax = stage_fast<SF, MODE, false>(v, raw, c, fl, down, win, rt, thl, false);
         }
         if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) {
 #pragma unroll
@@ -1382,7 +1377,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         // symbols the certificate does not cover: exact per-sample rotation
         const bool redo = kind == kUnitSym && c.ok &&
                           (exact_only || !fast_applies<SF, MODE>(c, c.toff) ||
-                           !fast_certified<SF>(b2, c, amax));
+                           !fast_certified<SF>(b2, c, amax, RLDS ? 0.0f : 6.0f));
         // (no exact re-run here: it would keep a second transform's state
         // live beside the prefetch.  The symbol is left as kSymRecheck and
         // its frame as kStatusRecheck; k_post recomputes it exactly.)
@@ -1438,13 +1433,25 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             meta_put_est(&A.meta[w + ke * W], m);
         }
         team_sync<SF>();
-        if constexpr (RLDS) {
-            // the folded frame's rotation table, first read two tiles later
-            // (its slot's previous frame, ke - 2, has no units left)
-            if (folding) {
-                const float4 r = ring[wv][ke % 3];
-                if (__float_as_uint(r.w) & 1u)
+        // the folded frame's rotation table, first read two tiles later (its
+        // slot's previous frame, ke - 2, has no units left)
+        if (folding) {
+            const float4 r = ring[wv][ke % 3];
+            if (__float_as_uint(r.w) & 1u) {
+                if constexpr (RLDS) {
                     build_rtab<SF, MODE>(rtab[wv][ke & 1], r.x, r.y, __float_as_int(r.z), down, win, lane);
+                } else {
+                    cf32* tb = rtab2[wv][ke & 1];
+                    for (int j = lane; j < 64 + N / 64; j += 64) {
+                        const int ph = j < 64 ? j : 64 * (j - 64);
+                        float sn, cs;
+                        lphy_libm::sincosf_exact(r.x * (float)ph, &sn, &cs);
+                        cf32 t = cf32{cs, sn};
+                        if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE)
+                            if (j < 64) t = cscale(t, r.y);
+                        tb[j] = t;
+                    }
+                }
             }
         }
         // speculative normalisation: the tile holding a frame's last symbol
