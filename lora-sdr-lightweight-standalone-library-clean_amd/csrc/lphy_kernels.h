@@ -1348,8 +1348,14 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         const SymCtx nc = ctx_of(nkind, nfk, nsu);
         if (t + 1 < ntiles) {
             const cf32* nsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base + fl;
+#ifdef LPHY_ABLATE_FRAME_LOAD  // timing experiments only: no IQ traffic
+            (void)nsrc;
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) raw[e] = raw[e] * 0.999f + cf32{(float)e, (float)t};
+#else
 #pragma unroll
             for (int e = 0; e < G::E; ++e) raw[e] = nsrc[first_pass_index<SF>(e, 0)];
+#endif
         }
 
         // tiles of symbol units only: magnitude-only transform (fft_tile TRIV)
