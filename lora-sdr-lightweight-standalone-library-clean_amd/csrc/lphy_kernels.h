@@ -475,12 +475,13 @@ __device__ __forceinline__ SymCtx sym_ctx(const DemodArgs& A, unsigned f, unsign
     const unsigned step = (unsigned)N * osr, count = (unsigned)A.frame_samples;
     unsigned base = s * step;
     const int t = m.t_off;
+    // all in 32 bits without overflow: count < 2^31 (lphy_hip_demod_batch),
+    // base + step <= count for a symbol of the frame, |INT_MIN| = 2^31
     if (t > 0) {
-        if ((unsigned long long)base + (unsigned)t + step <= count) base += (unsigned)t;
+        if (base + step <= count && (unsigned)t <= count - step - base) base += (unsigned)t;
     } else if (t < 0) {
-        const unsigned long long off = (t == (int)0x80000000u) ? (unsigned long long)(long long)t
-                                                               : (unsigned long long)(-(long long)t);
-        if (off <= base) base -= (unsigned)off;
+        const unsigned off = 0u - (unsigned)t;
+        if (off <= base) base -= off;
     }
     c.base = base;
     c.rate = m.rate;
