@@ -565,6 +565,45 @@ __device__ __forceinline__ ArgMax2 symbol_argmax2(ArgMax2 a) {
     return a;
 }
 
+// DPP row shift (v_mov_b32_dpp row_shl:n): lane i receives lane i + n of
+// its 16-lane row (lanes past the row keep `old`).
+template <int N>
+__device__ __forceinline__ int dpp_row_shl(int v) {
+    static_assert(N >= 1 && N <= 15, "row_shl range");
+    return __builtin_amdgcn_update_dpp(v, v, 0x100 | N, 0xF, 0xF, false);
+}
+template <int N>
+__device__ __forceinline__ float dpp_row_shl(float v) {
+    return __builtin_bit_cast(float, dpp_row_shl<N>(__builtin_bit_cast(int, v)));
+}
+
+// Team reduction toward the team's first lane (LPS <= 16: the team sits in
+// one DPP row), no LDS traffic: the result is valid in lane lam == 0 only
+// (the lanes above read across into the next team).
+template <int SF, int OFF = Geo<SF>::LPS / 2>
+__device__ __forceinline__ ArgMax2 team_argmax2_first(ArgMax2 a) {
+    static_assert(Geo<SF>::LPS <= 16, "team inside one DPP row");
+    if constexpr (OFF >= 1) {
+        ArgMax2 o;
+        o.v = dpp_row_shl<OFF>(a.v);
+        o.i = dpp_row_shl<OFF>(a.i);
+        o.v2 = dpp_row_shl<OFF>(a.v2);
+        a.v2 = fmaxf(fmaxf(a.v2, o.v2), fminf(a.v, o.v));
+        const bool take = (o.v > a.v) | ((o.v == a.v) & (o.i < a.i));
+        a.v = take ? o.v : a.v;
+        a.i = take ? o.i : a.i;
+        return team_argmax2_first<SF, OFF / 2>(a);
+    } else {
+        if (!(a.v > 0.0f)) a.i = 0;  // nothing beat maxValue = 0
+        return a;
+    }
+}
+template <int SF, int OFF = Geo<SF>::LPS / 2>
+__device__ __forceinline__ float team_max_first(float a) {
+    if constexpr (OFF >= 1) return team_max_first<SF, OFF / 2>(fmaxf(a, dpp_row_shl<OFF>(a)));
+    else return a;
+}
+
 // Workgroup form for teams spanning wavefronts (LPS > 64: SF 11-12): the
 // waves reduce in registers, then combine through `red` (one entry per wave;
 // contains barriers, every thread of the tile calls it).

@@ -1319,8 +1319,12 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             amax = stage_fast<SF, MODE, false>(v, raw, c, fl, down, win, rt, thl, false);
         }
         if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) {
+            if constexpr (G::LPS <= 16) {
+                amax = team_max_first<SF>(amax);  // the certificate reads lane lam == 0
+            } else {
 #pragma unroll
-            for (int off = G::LPS / 2; off >= 1; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
+                for (int off = G::LPS / 2; off >= 1; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
+            }
         } else {
             // normalised frame: max(|I|,|Q|) <= 1 (see fast_certified); under
             // speculation the frame end confirms it or settles the frame
@@ -1364,7 +1368,11 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         // two, 3 % slower than this ordered scan)
         if (emask) fft_tile<SF, false, false, true>(v, lds, slot, lam, twl);
         else fft_tile<SF, true, false, true>(v, lds, slot, lam, twl);
-        const ArgMax2 b2 = symbol_argmax2<SF>(local_argmax2<SF>(v, lam));
+        // (SF <= 8: reduced toward lane lam == 0 by DPP, the only lane that
+        // reads it; above, every lane of the team holds it)
+        ArgMax2 b2;
+        if constexpr (G::LPS <= 16) b2 = team_argmax2_first<SF>(local_argmax2<SF>(v, lam));
+        else b2 = symbol_argmax2<SF>(local_argmax2<SF>(v, lam));
         ArgMax best{b2.v, b2.i};
         if (emask) {
             // detector outputs of the estimate units (LoRaDetector.hpp:60-71)
@@ -1390,13 +1398,16 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         // its frame as kStatusRecheck; k_post recomputes it exactly.)
         if (spec && kind == kUnitSym && c.ok) {
             // a NaN sample reaches every bin (fft_has_nan); the certificate's
-            // lead over its bound, for the frame end's rate check
+            // lead over its bound, for the frame end's rate check (from the
+            // team's first lane, which holds the team's top two)
             const cf32 q = v[0] * v[0];
             const float q2 = q.x + q.y;
             unsigned fl = q2 == q2 ? 0u : 1u;
             float r = kBig;
-            if (redo) fl |= 2u;
-            else r = cert_gap(b2) / cert_bound<SF>(c.rate, c.start, 1.0f);
+            if (lam == 0) {
+                if (redo) fl |= 2u;
+                else r = cert_gap(b2) / cert_bound<SF>(c.rate, c.start, 1.0f);
+            }
             if (fk & 1) {
                 sp_fl1 |= fl;
                 sp_r1 = fminf(sp_r1, r);
