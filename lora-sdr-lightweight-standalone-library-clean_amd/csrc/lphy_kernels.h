@@ -801,6 +801,9 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
 #endif
         if constexpr (FASTB) {
             if (fastb) {
+#ifdef LPHY_PROFILE_PHASES
+                const unsigned long long q2 = clock64();
+#endif
                 // certificate (fast_certified, with the two-table rotation's
                 // further 6u); a NaN or near-tie leaves the symbol to k_post
                 const ArgMax2 b2 = symbol_argmax2_wg<SF>(local_argmax2<SF>(v, lam), red2);
@@ -824,6 +827,10 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
                 }
                 c = nc;
                 f = nf; s = ns; fw = nfw; sw = nsw;
+#ifdef LPHY_PROFILE_PHASES
+                const unsigned long long q3 = clock64();
+                ph_stage += p1 - p0; ph_fft += q2 - p1; ph_tail += q3 - q2;
+#endif
                 continue;
             }
         }

@@ -47,9 +47,10 @@ def run(sf, names):
         if hasattr(lib, "lphy_hip_phase_cycles"):
             import ctypes as C
             out = (C.c_ulonglong * 4)()
-            lib.lphy_hip_phase_cycles(out)  # clear
+            lib.lphy_hip_phase_cycles.argtypes = [C.c_void_p, C.c_void_p]
+            lib.lphy_hip_phase_cycles(wl.dem.ctx, out)  # clear
             wl._event_ms(mode, D | lphy.F_UNFUSED | lphy.F_STAGE_SYMBOLS, 1)
-            lib.lphy_hip_phase_cycles(out)
+            lib.lphy_hip_phase_cycles(wl.dem.ctx, out)
             tot = sum(out[:3]) or 1
             extra = " phases stage/fft/tail = " + "/".join(f"{out[i] / tot:.2f}" for i in range(3))
         wl.run(mode)
