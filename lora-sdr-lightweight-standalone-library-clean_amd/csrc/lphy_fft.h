@@ -608,7 +608,8 @@ __device__ __forceinline__ float team_max_first(float a) {
 // waves reduce in registers, then combine through `red` (one entry per wave;
 // contains barriers, every thread of the tile calls it).
 template <int SF>
-__device__ __forceinline__ ArgMax2 symbol_argmax2_wg(ArgMax2 a, ArgMax2* red) {
+__device__ __forceinline__ ArgMax2 symbol_argmax2_wg(ArgMax2 a, ArgMax2* red, float* m = nullptr,
+                                                     float* redm = nullptr) {
     using G = Geo<SF>;
     static_assert(G::LPS > 64, "teams inside one wavefront use symbol_argmax2");
     auto comb = [](ArgMax2 x, ArgMax2 o) __attribute__((always_inline)) {
@@ -626,14 +627,28 @@ __device__ __forceinline__ ArgMax2 symbol_argmax2_wg(ArgMax2 a, ArgMax2* red) {
         o.v2 = __shfl_xor(a.v2, off, 64);
         a = comb(a, o);
     }
+    // m (optional): a per-lane max reduced over the team alongside
+    if (m) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) *m = fmaxf(*m, __shfl_xor(*m, off, 64));
+    }
     const int wave = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) red[wave] = a;
+    if ((threadIdx.x & 63) == 0) {
+        red[wave] = a;
+        if (m) redm[wave] = *m;
+    }
     __syncthreads();
     constexpr int WPS = G::LPS / 64;
     const int first = (wave / WPS) * WPS;
     ArgMax2 b = red[first];
 #pragma unroll
     for (int w = 1; w < WPS; ++w) b = comb(b, red[first + w]);
+    if (m) {
+        float mm = redm[first];
+#pragma unroll
+        for (int w = 1; w < WPS; ++w) mm = fmaxf(mm, redm[first + w]);
+        *m = mm;
+    }
     __syncthreads();
     if (!(b.v > 0.0f)) b.i = 0;
     return b;

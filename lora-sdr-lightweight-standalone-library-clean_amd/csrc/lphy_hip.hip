@@ -61,6 +61,12 @@ struct lphy_hip_ctx {
     void* d_stage = nullptr;
     unsigned long long* d_counters = nullptr;  // [0] rechecks, [1..4] phase clocks
     size_t stage_bytes = 0;
+    // per-frame speculation records of the SF 11-12 separate launches
+    // (DemodArgs::spec_big), grown on demand; batch calls on one context are
+    // ordered on its stream(s) by the caller, like its other device state
+    std::mutex spec_mu;
+    void* d_spec = nullptr;
+    size_t spec_bytes = 0;
     // (the producer / compensation kernels take their scratch per call from
     // the stream-ordered allocator, so concurrent calls on different streams
     // or threads never share it)
@@ -266,6 +272,7 @@ void lphy_hip_ctx_destroy(lphy_hip_ctx* c) {
     if (c->d_win) (void)hipFree(c->d_win);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->d_counters) (void)hipFree(c->d_counters);
+    if (c->d_spec) (void)hipFree(c->d_spec);
     delete c;
 }
 
@@ -329,6 +336,26 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     const bool fused = (all || (stages & both) == both) && !(flags & LPHY_F_UNFUSED) &&
                        fused_enabled() && frames_fit(c->sf, c->osr, A.est_units, total);
     A.sentinels = fused ? 1 : 0;  // k_cuframe marks open symbols in the output only
+    // SF 11-12 separate launches, modes 1/2: the speculative normalisation
+    // of k_frames across workgroups (k_maxabs scans the two estimate
+    // symbols, k_demod folds the rest, k_post closes each frame); needs the
+    // prologue, the symbols and the fix-up in this one call
+    if (!fused && A.spec && c->sf >= 11 && c->osr == 1 && !A.exact_rotation && total >= 2 &&
+        (all || (stages & both) == both)) {
+        std::lock_guard<std::mutex> lk(c->spec_mu);
+        const size_t need = frames * sizeof(uint4);
+        if (c->spec_bytes < need) {
+            if (c->d_spec) {
+                HIP_OK(hipDeviceSynchronize());  // a previous call may still use it
+                (void)hipFree(c->d_spec);
+            }
+            c->d_spec = nullptr;
+            c->spec_bytes = 0;
+            HIP_OK(hipMalloc(&c->d_spec, need));
+            c->spec_bytes = need;
+        }
+        A.spec_big = static_cast<uint4*>(c->d_spec);
+    }
     int rc = fused ? launch_frames(c->sf, A, st)
                    : launch_demod(c->sf, A, st, all || (stages & LPHY_F_STAGE_PROLOGUE),
                                   all || (stages & LPHY_F_STAGE_SYMBOLS));

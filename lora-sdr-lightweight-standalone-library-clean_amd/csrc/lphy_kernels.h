@@ -70,6 +70,11 @@ struct DemodArgs {
     int sentinels;           // k_post: look for kSymRecheck in frames with status 0 (k_cuframe)
     int resident;            // LPHY_F_RESIDENT: k_cuframe where it applies
     int spec;                // k_frames modes 1/2: speculative normalisation (no whole-frame pre-scan)
+    // separate launches, SF 11-12 fast path, modes 1/2: the same speculation
+    // across workgroups, per frame {max-abs of the two estimate symbols,
+    // max-abs of the symbol windows, least certificate ratio (float bits,
+    // atomic max / min), flags (1 NaN, 2 symbol left open)}; nullptr = off
+    uint4* spec_big;
     // persistent demod workers: symbol stride per step split into whole
     // frames + symbols (host-computed, so the kernel never divides)
     unsigned stride_f, stride_s;
@@ -204,7 +209,8 @@ __global__ __launch_bounds__(kTile) void k_maxabs(DemodArgs A) {
     const unsigned long long f = blockIdx.x;
     const int tid = threadIdx.x;
     const cf32* fr = A.iq + f * A.frame_samples;
-    const unsigned long long count = A.frame_samples;
+    // spec_big: the two estimate symbols only (the symbols fold the rest)
+    const unsigned long long count = A.spec_big ? 2ull * N : A.frame_samples;
     const unsigned long long dech_end = A.total_syms * N;  // whole symbols
     const bool dech = A.mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     float mx = 0.0f;
@@ -256,6 +262,7 @@ __global__ __launch_bounds__(kTile) void k_maxabs(DemodArgs A) {
             mx = wmax[w] > mx ? wmax[w] : mx;
         }
         A.meta[f] = norm_meta_hot(nf ? __builtin_nanf("") : mx, A.total_syms >= 2, A.no_scratch);
+        if (A.spec_big) A.spec_big[f] = make_uint4(__float_as_uint(nf ? 0.0f : mx), 0u, 0x7f7fffffu, nf ? 1u : 0u);
     }
 }
 
@@ -761,6 +768,8 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
                 }
                 if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
                     p = cmul(p, down[(c.base + (unsigned)i) & (N - 1)]);
+                // modes 1/2 (spec_big): the [dechirped] samples' max-abs
+                if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) amax = max3_abs(amax, p.x, p.y);
                 cf32 q = cmul_fma(cmul_fma(p, tl), thi[slot][(lam >> 6) + e * (G::LPS / 64)]);
                 if constexpr ((MODE & kWinBit) != 0) q = cscale(q, win[i]);
                 stg.put(lds, e, c.ok ? q : czero());
@@ -806,24 +815,30 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
 #endif
                 // certificate (fast_certified, with the two-table rotation's
                 // further 6u); a NaN or near-tie leaves the symbol to k_post
-                const ArgMax2 b2 = symbol_argmax2_wg<SF>(local_argmax2<SF>(v, lam), red2);
-                float am = 1.0f;  // modes 1/2: normalised frame
-                if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) {
-#pragma unroll
-                    for (int off = 32; off >= 1; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
-                    if ((tid & 63) == 0) redm[tid >> 6] = amax;
-                    __syncthreads();
-                    constexpr int WPS = G::LPS / 64;
-                    const int first = ((tid >> 6) / WPS) * WPS;
-                    am = redm[first];
-#pragma unroll
-                    for (int w = 1; w < WPS; ++w) am = fmaxf(am, redm[first + w]);
-                    __syncthreads();
-                }
+                // the team's top two and its samples' max-abs in one exchange
+                const bool tm = (MODE & 3) == LPHY_MODE_DEMODULATE || A.spec_big != nullptr;
+                const ArgMax2 b2 = symbol_argmax2_wg<SF>(local_argmax2<SF>(v, lam), red2, tm ? &amax : nullptr,
+                                                         redm);
+                // modes 1/2: normalised frame (under spec_big, k_post's close
+                // confirms the normalisation or settles the frame)
+                const float am = (MODE & 3) == LPHY_MODE_DEMODULATE ? amax : 1.0f;
                 const bool redo = !fast_certified<SF>(b2, c, am, 6.0f);
                 if (c.ok && lam == 0) {
                     store_symbol(A, c, redo ? kSymRecheck : (uint16_t)b2.i);
                     if (redo) A.meta[c.f].status = kStatusRecheck;
+                }
+                if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) {
+                    if (A.spec_big && c.ok) {
+                        uint4* r = &A.spec_big[c.f];
+                        const cf32 q = v[0] * v[0];
+                        const float q2 = q.x + q.y;
+                        if (!(q2 == q2)) atomicOr(&r->w, 1u);  // a NaN sample reaches every bin
+                        if (lam == 0) {
+                            atomicMax(&r->y, __float_as_uint(amax));
+                            if (redo) atomicOr(&r->w, 2u);
+                            else atomicMin(&r->z, __float_as_uint(cert_gap(b2) / cert_bound<SF>(c.rate, c.start, 1.0f, 6.0f)));
+                        }
+                    }
                 }
                 c = nc;
                 f = nf; s = ns; fw = nfw; sw = nsw;
@@ -1620,6 +1635,7 @@ struct PostShared {
     unsigned list[kTile];
     unsigned listf[kTile];
     unsigned count;
+    UnitResult ures2[kTile][2];  // settle_frames: both estimate units of each frame
 };
 
 template <int SF, int MODE>
@@ -1811,7 +1827,7 @@ __device__ void recheck_frames(const DemodArgs& A, unsigned long long fb, bool m
 template <int SF, int MODE>
 __device__ void settle_frames(const DemodArgs& A, unsigned long long fb, bool mine, PostShared<SF>& sh) {
     using G = Geo<SF>;
-    constexpr int N = G::N, T = G::T, FPT = T / 2;
+    constexpr int N = G::N, T = G::T;
     const int tid = threadIdx.x;
     const int slot = tid / G::LPS, lam = tid % G::LPS;
     if (tid == 0) sh.count = 0;
@@ -1819,9 +1835,11 @@ __device__ void settle_frames(const DemodArgs& A, unsigned long long fb, bool mi
     if (mine) sh.list[atomicAdd(&sh.count, 1u)] = (unsigned)tid;
     __syncthreads();
     const unsigned n = sh.count;
-    for (unsigned k0 = 0; k0 < n; k0 += FPT) {
-        const unsigned k = k0 + (unsigned)slot / 2, s = (unsigned)slot & 1u;
-        const bool live = k < n;
+    // units (frame k, estimate symbol s) = 2k + s, T per tile pass
+    for (unsigned u0 = 0; u0 < 2 * n; u0 += T) {
+        const unsigned u = u0 + (unsigned)slot;
+        const bool live = u < 2 * n;
+        const unsigned k = live ? u / 2 : 0u, s = u & 1u;
         const unsigned long long f = fb + (live ? sh.list[k] : 0u);
         const lphy_frame_meta m = norm_meta(A.meta[f].cfo, true, 0);  // cfo holds the max-abs
         const cf32* fr = A.iq + f * A.frame_samples;
@@ -1838,36 +1856,36 @@ __device__ void settle_frames(const DemodArgs& A, unsigned long long fb, bool mi
         for (int e = 0; e < G::E; ++e) sh.lds[G::addr(slot, bin_of<SF>(e, lam))] = v[e];
         const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), sh.red);
         __syncthreads();
-        if (lam == 0) sh.units[slot] = live ? unit_result<SF>(sh.lds, slot, best) : UnitResult{0, 0, 0.0f, 0.0f, 0};
-        __syncthreads();
-        if (tid < FPT && k0 + (unsigned)tid < n) {
-            const unsigned long long g = fb + sh.list[k0 + tid];
-            const lphy_frame_meta sm = A.meta[g];
-            lphy_frame_meta e = norm_meta(sm.cfo, true, 0);
-            EstFold fold;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const UnitResult r = sh.units[2 * tid + u];
-                if (r.valid) fold.add(r.idx, r.findex, 0, r.phase);
-                else fold.add(0, 0.0f, 0, 0.0f);
-            }
-            fold.finish(e, 2, N, 1);
-            // amplitude bound of the speculatively scaled samples, and the
-            // smallest bound of any symbol (|start| grows with the symbol)
-            const float a = fmaxf(1.0f, sm.cfo * sm.scale) * 1.0001f;
-            const float b1 = cert_bound<SF>(sm.rate, sm.rate * (float)sm.t_off, 1.0f);
-            const float d = fabsf(e.rate - sm.rate) * (1.0f + 4.0f * kU);
-            const float A1 = (float)N * 1.41421366f * 1.0001f;
-            const bool ok = e.t_off == sm.t_off && sm.t_off >= -N && sm.t_off <= N &&
-                            sm.time_offset > 4.0f * a + 4.0f * d * (float)N * A1 * a / b1;
-            lphy_frame_meta r = e;
-            r.sw0 = sm.sw0;
-            r.sw1 = sm.sw1;
-            r.status = !ok ? kStatusFixup : (sm.status == kStatusSettleRecheck ? kStatusRecheck : 0);
-            A.meta[g] = r;
-        }
+        if (lam == 0 && live) sh.ures2[k][s] = unit_result<SF>(sh.lds, slot, best);
         __syncthreads();
     }
+    if ((unsigned)tid < n) {
+        const unsigned long long g = fb + sh.list[tid];
+        const lphy_frame_meta sm = A.meta[g];
+        lphy_frame_meta e = norm_meta(sm.cfo, true, 0);
+        EstFold fold;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const UnitResult r = sh.ures2[tid][u];
+            if (r.valid) fold.add(r.idx, r.findex, 0, r.phase);
+            else fold.add(0, 0.0f, 0, 0.0f);
+        }
+        fold.finish(e, 2, N, 1);
+        // amplitude bound of the speculatively scaled samples, and the
+        // smallest bound of any symbol (|start| grows with the symbol)
+        const float a = fmaxf(1.0f, sm.cfo * sm.scale) * 1.0001f;
+        const float b1 = cert_bound<SF>(sm.rate, sm.rate * (float)sm.t_off, 1.0f);
+        const float d = fabsf(e.rate - sm.rate) * (1.0f + 4.0f * kU);
+        const float A1 = (float)N * 1.41421366f * 1.0001f;
+        const bool ok = e.t_off == sm.t_off && sm.t_off >= -N && sm.t_off <= N &&
+                        sm.time_offset > 4.0f * a + 4.0f * d * (float)N * A1 * a / b1;
+        lphy_frame_meta r = e;
+        r.sw0 = sm.sw0;
+        r.sw1 = sm.sw1;
+        r.status = !ok ? kStatusFixup : (sm.status == kStatusSettleRecheck ? kStatusRecheck : 0);
+        A.meta[g] = r;
+    }
+    __syncthreads();
 }
 
 // Whether frame f holds a symbol left open by k_cuframe, which marks them in
@@ -1878,6 +1896,104 @@ __device__ __forceinline__ bool has_sentinel(const DemodArgs& A, unsigned long l
     const uint16_t* o = A.syms + f * A.out_per_frame;
     for (unsigned long long i = 0; i < A.out_per_frame; ++i) any |= o[i] == kSymRecheck;
     return any;
+}
+
+// Separate launches with spec_big (SF 11-12, modes 1/2): the frame-end
+// check k_frames makes in-kernel, one workgroup per frame (so the exact
+// estimates of settled frames run in parallel).  The samples no symbol
+// window covers are scanned; the frame's true max-abs then confirms the
+// two-symbol normalisation, or - NaN / inf - sends the frame to k_post's
+// exact re-run, or settles it here: both estimate FFTs again with the exact
+// scale (the reference's arithmetic, as exact_frame) and the certificate
+// check of settle_frames against the exact rate, else the exact re-run.
+template <int SF, int MODE>
+__global__ __launch_bounds__(kTile) void k_spec_settle(DemodArgs A) {
+    using G = Geo<SF>;
+    constexpr int N = G::N, T = G::T;
+    constexpr bool DECH = MODE == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    __shared__ PostShared<SF> sh;
+    const unsigned long long f = blockIdx.x;
+    const int tid = threadIdx.x;
+    const lphy_frame_meta m = A.meta[f];
+    if (!(m.status == 0 || m.status == kStatusRecheck)) return;  // uniform
+    const unsigned S = (unsigned)A.total_syms;
+    const unsigned cnt = DECH ? S * N : (unsigned)A.frame_samples;
+    const unsigned end = covered_end(S, N, cnt, m.t_off);
+    const cf32* fr = A.iq + f * A.frame_samples;
+    float frag = 0.0f;
+    bool fbad = false;
+    if (end < cnt) {
+        float mx = 0.0f;
+        bool bad = false;
+        for (unsigned i = end + (unsigned)tid; i < cnt; i += kTile) {
+            cf32 x = fr[i];
+            if constexpr (DECH) x = cmul(x, A.down[i & (N - 1)]);
+            bad |= !(__builtin_isfinite(x.x) && __builtin_isfinite(x.y));
+            maxabs_acc(mx, x);
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const float o = __shfl_xor(mx, off, 64);
+            mx = o > mx ? o : mx;
+        }
+        fbad = __syncthreads_or(bad);
+        if ((tid & 63) == 0) sh.wmax[tid >> 6] = mx;
+        __syncthreads();
+        frag = sh.wmax[0];
+        for (int w = 1; w < kTile / 64; ++w) frag = sh.wmax[w] > frag ? sh.wmax[w] : frag;
+    }
+    const uint4 r = A.spec_big[f];
+    const float mx01 = __uint_as_float(r.x);
+    const float mt = fmaxf(fmaxf(mx01, __uint_as_float(r.y)), frag);
+    const lphy_frame_meta mg = norm_meta(mx01, true, 0), me = norm_meta(mt, true, 0);
+    if ((r.w & 1u) || fbad || !(mt <= 3.40282347e38f)) {
+        if (tid == 0) A.meta[f].status = kStatusFixup;
+        return;
+    }
+    if (me.scale == mg.scale && me.normalised == mg.normalised) return;  // confirmed
+    // settle: the two estimate units, T per pass
+    const int slot = tid / G::LPS, lam = tid % G::LPS;
+    for (unsigned u0 = 0; u0 < 2; u0 += T) {
+        const unsigned s = u0 + (unsigned)slot;
+        const bool live = s < 2;
+        const Stage<SF> st(slot, lam);
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) {
+            const int i = lam + e * G::LPS;
+            st.put(sh.lds, e, live ? est_sample(A, fr, (unsigned long long)s * N + (unsigned)i, i, N, me) : czero());
+        }
+        __syncthreads();
+        cf32 v[16];
+        fft_tile<SF, false, true>(v, sh.lds, slot, lam, A.tw);
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) sh.lds[G::addr(slot, bin_of<SF>(e, lam))] = v[e];
+        const ArgMax best = symbol_argmax<SF>(local_argmax<SF>(v, lam), sh.red);
+        __syncthreads();
+        if (lam == 0 && live) sh.ures2[0][s] = unit_result<SF>(sh.lds, slot, best);
+        __syncthreads();
+    }
+    if (tid == 0) {
+        lphy_frame_meta e = me;
+        EstFold fold;
+        for (int u = 0; u < 2; ++u) {
+            const UnitResult ur = sh.ures2[0][u];
+            if (ur.valid) fold.add(ur.idx, ur.findex, 0, ur.phase);
+            else fold.add(0, 0.0f, 0, 0.0f);
+        }
+        fold.finish(e, 2, N, 1);
+        const float a = fmaxf(1.0f, mt * m.scale) * 1.0001f;
+        const float b1 = cert_bound<SF>(m.rate, m.rate * (float)m.t_off, 1.0f);
+        const float d = fabsf(e.rate - m.rate) * (1.0f + 4.0f * kU);
+        const float A1 = (float)N * 1.41421366f * 1.0001f;
+        const float R = __uint_as_float(r.z);
+        const bool ok = e.t_off == m.t_off && m.t_off >= -N && m.t_off <= N &&
+                        R > 4.0f * a + 4.0f * d * (float)N * A1 * a / b1;
+        lphy_frame_meta out = e;
+        out.sw0 = m.sw0;
+        out.sw1 = m.sw1;
+        out.status = !ok ? kStatusFixup : (((r.w & 2u) || m.status == kStatusRecheck) ? kStatusRecheck : 0);
+        A.meta[f] = out;
+    }
 }
 
 // After the symbol kernels: the exact re-run of the frames they flagged
@@ -2215,6 +2331,14 @@ int launch_frames_sf(const DemodArgs& A, hipStream_t st) {
 template <int SF>
 int launch_post_sf(int mode, const DemodArgs& A, const FinalArgs& F, bool fix, bool fin, hipStream_t st) {
     const dim3 grid((unsigned)((A.frames + kTile - 1) / kTile));
+    if (fix && A.spec_big) {
+        if (mode == LPHY_MODE_LORA_DEMODULATE)
+            hipLaunchKernelGGL((k_spec_settle<SF, LPHY_MODE_LORA_DEMODULATE>), dim3((unsigned)A.frames), dim3(kTile), 0,
+                               st, A);
+        else if (mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE)
+            hipLaunchKernelGGL((k_spec_settle<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>), dim3((unsigned)A.frames),
+                               dim3(kTile), 0, st, A);
+    }
     switch (mode) {
         case LPHY_MODE_DEMODULATE:
             hipLaunchKernelGGL((k_post<SF, LPHY_MODE_DEMODULATE>), grid, dim3(kTile), 0, st, A, F, (int)fix, (int)fin);

@@ -1,4 +1,5 @@
-"""Speculative normalisation of the fused kernel (k_frames, modes 1/2): the
+"""Speculative normalisation of the fused kernel (k_frames, modes 1/2; for
+SF 11-12 the separate launches with DemodArgs::spec_big): the
 frame is estimated with the max-abs of its first two symbols, each symbol
 unit folds its own samples' max-abs, and the frame end either confirms the
 normalisation or settles the frame in k_post (exact estimate + certificate
@@ -54,7 +55,7 @@ def _build(oracle, sf, nf, seed, tail=0):
     return iq
 
 
-@pytest.mark.parametrize("sf,nf", [(7, 515), (5, 301), (8, 203), (9, 97), (10, 41)])
+@pytest.mark.parametrize("sf,nf", [(7, 515), (5, 301), (8, 203), (9, 97), (10, 41), (11, 29), (12, 15)])
 @pytest.mark.parametrize("mode", [1, 2])
 def test_speculative_normalisation(oracle, lphy, sf, nf, mode):
     tail = (1 << sf) // 2 + 3 if mode == 1 else 0  # a partial last symbol
