@@ -607,7 +607,9 @@ __device__ __forceinline__ float team_max_first(float a) {
 // Workgroup form for teams spanning wavefronts (LPS > 64: SF 11-12): the
 // waves reduce in registers, then combine through `red` (one entry per wave;
 // contains barriers, every thread of the tile calls it).
-template <int SF>
+// TAIL_SYNC = false: the caller alternates `red` / `redm` between tiles, so
+// the trailing barrier that protects their reuse is not needed.
+template <int SF, bool TAIL_SYNC = true>
 __device__ __forceinline__ ArgMax2 symbol_argmax2_wg(ArgMax2 a, ArgMax2* red, float* m = nullptr,
                                                      float* redm = nullptr) {
     using G = Geo<SF>;
@@ -649,7 +651,7 @@ __device__ __forceinline__ ArgMax2 symbol_argmax2_wg(ArgMax2 a, ArgMax2* red, fl
         for (int w = 1; w < WPS; ++w) mm = fmaxf(mm, redm[first + w]);
         *m = mm;
     }
-    __syncthreads();
+    if constexpr (TAIL_SYNC) __syncthreads();
     if (!(b.v > 0.0f)) b.i = 0;
     return b;
 }

@@ -674,11 +674,14 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
     __shared__ cf32 dnl[TAB ? N : 1];
     __shared__ float wnl[TAB ? N : 1];
     __shared__ ArgMax red[kTile / 64];
-    __shared__ ArgMax2 red2[FASTB ? kTile / 64 : 1];
-    __shared__ float redm[FASTB ? kTile / 64 : 1];
-    __shared__ cf32 thi[FASTB ? G::T : 1][FASTB ? NH : 1];
-    __shared__ cf32 tlo[FASTB ? G::T : 1][FASTB ? 64 : 1];
+    // double-buffered by tile parity: the next tile's tables are built at the
+    // end of this one, and the reductions need no trailing barrier
+    __shared__ ArgMax2 red2[2][FASTB ? kTile / 64 : 1];
+    __shared__ float redm[2][FASTB ? kTile / 64 : 1];
+    __shared__ cf32 thi[2][FASTB ? G::T : 1][FASTB ? NH : 1];
+    __shared__ cf32 tlo[2][FASTB ? G::T : 1][FASTB ? 64 : 1];
     const bool fastb = FASTB && !A.exact_rotation;
+    unsigned tp = 0;  // tile parity
 
     const int tid = threadIdx.x;
     for (int i = tid; i < N; i += kTile) {
@@ -718,6 +721,26 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
     const unsigned osr = OSR ? (unsigned)A.osr : 1u;  // sample stride of a symbol
     lphy_frame_meta m = A.meta[f < nframes ? f : 0];
     SymCtx c = sym_ctx<OSR>(A, f < nframes ? f : 0, f < nframes ? s : 0, f < nframes, N, m);
+    // the two rotation tables of a tile's symbol (scale folded into the low
+    // one), written by the team's first NH + 64 lanes
+    auto build_tables = [&](const SymCtx& cc, unsigned b) __attribute__((always_inline)) {
+        if constexpr (FASTB) {
+            if (cc.ok) {
+                float sn, cs;
+                if (lam < NH) {
+                    lphy_libm::sincosf_exact(cc.rate * (float)(64 * lam), &sn, &cs);
+                    thi[b][slot][lam] = cf32{cs, sn};
+                } else if (lam < NH + 64) {
+                    const int l = lam - NH;
+                    lphy_libm::sincosf_exact(cc.rate * (float)l, &sn, &cs);
+                    cf32 t = cf32{cs, sn};
+                    if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) t = cscale(t, cc.scale);
+                    tlo[b][slot][l] = t;
+                }
+            }
+        }
+    };
+    if (FASTB && fastb) build_tables(c, 0);  // visible after the loop's first barrier
     cf32 raw[16];
     {
         const cf32* src = A.iq + (unsigned long long)c.f * A.frame_samples + c.base;
@@ -742,22 +765,8 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
         if constexpr (!WAVE) __syncthreads();  // previous tile's readers done
         float amax = 0.0f;  // fast path, mode 0: the team's max(|Re x|, |Im x|)
         if (FASTB && fastb) {
-            // the symbol's two rotation tables (scale folded into the low one)
-            if (c.ok) {
-                float sn, cs;
-                if (lam < NH) {
-                    lphy_libm::sincosf_exact(c.rate * (float)(64 * lam), &sn, &cs);
-                    thi[slot][lam] = cf32{cs, sn};
-                } else if (lam < NH + 64) {
-                    const int l = lam - NH;
-                    lphy_libm::sincosf_exact(c.rate * (float)l, &sn, &cs);
-                    cf32 t = cf32{cs, sn};
-                    if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) t = cscale(t, c.scale);
-                    tlo[slot][l] = t;
-                }
-            }
-            __syncthreads();
-            const cf32 tl = tlo[slot][lam & 63];
+            // this tile's tables were built at the end of the previous one
+            const cf32 tl = tlo[tp][slot][lam & 63];
 #pragma unroll
             for (int e = 0; e < G::E; ++e) {
                 const int i = lam + e * G::LPS;
@@ -770,7 +779,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
                     p = cmul(p, down[(c.base + (unsigned)i) & (N - 1)]);
                 // modes 1/2 (spec_big): the [dechirped] samples' max-abs
                 if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) amax = max3_abs(amax, p.x, p.y);
-                cf32 q = cmul_fma(cmul_fma(p, tl), thi[slot][(lam >> 6) + e * (G::LPS / 64)]);
+                cf32 q = cmul_fma(cmul_fma(p, tl), thi[tp][slot][(lam >> 6) + e * (G::LPS / 64)]);
                 if constexpr ((MODE & kWinBit) != 0) q = cscale(q, win[i]);
                 stg.put(lds, e, c.ok ? q : czero());
             }
@@ -817,8 +826,8 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
                 // further 6u); a NaN or near-tie leaves the symbol to k_post
                 // the team's top two and its samples' max-abs in one exchange
                 const bool tm = (MODE & 3) == LPHY_MODE_DEMODULATE || A.spec_big != nullptr;
-                const ArgMax2 b2 = symbol_argmax2_wg<SF>(local_argmax2<SF>(v, lam), red2, tm ? &amax : nullptr,
-                                                         redm);
+                const ArgMax2 b2 = symbol_argmax2_wg<SF, false>(local_argmax2<SF>(v, lam), red2[tp],
+                                                                tm ? &amax : nullptr, redm[tp]);
                 // modes 1/2: normalised frame (under spec_big, k_post's close
                 // confirms the normalisation or settles the frame)
                 const float am = (MODE & 3) == LPHY_MODE_DEMODULATE ? amax : 1.0f;
@@ -840,6 +849,8 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
                         }
                     }
                 }
+                build_tables(nc, tp ^ 1u);  // the next tile's, behind its first barrier
+                tp ^= 1u;
                 c = nc;
                 f = nf; s = ns; fw = nfw; sw = nsw;
 #ifdef LPHY_PROFILE_PHASES
