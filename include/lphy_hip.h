@@ -120,7 +120,9 @@ size_t lphy_hip_syms_per_frame(const lphy_hip_ctx* ctx, size_t frame_samples,
  * `stream`).  d_bytes may be NULL unless LPHY_F_DECODE.  d_meta is
  * required.  Returns 0 or -EINVAL/-ERANGE for shape errors (the per-frame
  * conditions the reference reports through its return value are in
- * lphy_frame_meta.status). */
+ * lphy_frame_meta.status).  At SF 11-12 in modes 1/2 a call keeps per-frame
+ * state in the context until its kernels finish: calls on one context run
+ * in stream order (one stream, or the caller orders them). */
 int lphy_hip_demod_batch(lphy_hip_ctx* ctx, const float* d_iq, size_t frames,
                          size_t frame_samples, uint16_t* d_syms,
                          uint8_t* d_bytes, lphy_frame_meta* d_meta, int mode,
