@@ -524,12 +524,26 @@ struct ArgMax2 {
     float v2;
 };
 
+// The winning element index is tracked (an inline constant per select) and
+// mapped to its bin once at the end: bin_of(e, 0) = (e % GS) * MH + (e / GS)
+// * bin_of(GS, 0) with the last pass's group size GS (checked at compile
+// time below).
 template <int SF>
 __device__ __forceinline__ ArgMax2 local_argmax2(const cf32 (&v)[16], int lam) {
     using G = Geo<SF>;
     constexpr BinOrder<SF> BO{};
+    constexpr Passes<SF> PS{};
+    using PG = PassGeo<SF, PS.hi[PS.n - 1], PS.lo[PS.n - 1]>;
+    constexpr int GS = PG::GS < G::E ? PG::GS : G::E;
+    constexpr int MH = bin_of<SF>(1, 0);
+    constexpr int XS = GS < G::E ? bin_of<SF>(GS, 0) : 0;
+    static_assert([] {
+        for (int e = 0; e < G::E; ++e)
+            if (bin_of<SF>(e, 0) != (e % GS) * MH + (e / GS) * XS) return false;
+        return true;
+    }(), "bin_of separable in the element's digits");
     ArgMax2 best{0.0f, 0x7fffffff, 0.0f};
-    const int lane_bin = bin_of<SF>(0, lam);
+    int best_e = -1;
 #pragma unroll
     for (int k = 0; k < G::E; ++k) {
         const int e = BO.e[k];
@@ -540,8 +554,9 @@ __device__ __forceinline__ ArgMax2 local_argmax2(const cf32 (&v)[16], int lam) {
         best.v2 = __builtin_amdgcn_fmed3f(best.v, best.v2, m2);
         const bool take = m2 > best.v;
         best.v = take ? m2 : best.v;
-        best.i = take ? (lane_bin | bin_of<SF>(e, 0)) : best.i;
+        best_e = take ? e : best_e;
     }
+    if (best_e >= 0) best.i = bin_of<SF>(0, lam) | ((best_e % GS) * MH + (best_e / GS) * XS);
     return best;
 }
 
