@@ -1423,9 +1423,14 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             team_sync<SF>();  // slot reads done before a re-check restages
         }
         // symbols the certificate does not cover: exact per-sample rotation
+        // certificate (fast_certified, written out so that the speculation
+        // below reuses its lead and bound): B is linear in amax
+        const float cb1 = cert_bound<SF>(c.rate, c.start, 1.0f, RLDS ? 0.0f : 6.0f);
+        const float cgap = cert_gap(b2);
+        const bool cert = cgap > 4.0f * (cb1 * amax) && (float)N * 1.41421366f * amax * 1.0001f < 1e18f &&
+                          amax >= 1e-20f && b2.v >= 1e-30f;
         const bool redo = kind == kUnitSym && c.ok &&
-                          (exact_only || !fast_applies<SF, MODE>(c, c.toff) ||
-                           !fast_certified<SF>(b2, c, amax, RLDS ? 0.0f : 6.0f));
+                          (exact_only || !fast_applies<SF, MODE>(c, c.toff) || !cert);
         // (no exact re-run here: it would keep a second transform's state
         // live beside the prefetch.  The symbol is left as kSymRecheck and
         // its frame as kStatusRecheck; k_post recomputes it exactly.)
@@ -1438,8 +1443,9 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             unsigned fl = q2 == q2 ? 0u : 1u;
             float r = kBig;
             if (lam == 0) {
+                // a lower bound of the lead / bound ratio (v_rcp within 1 ulp)
                 if (redo) fl |= 2u;
-                else r = cert_gap(b2) / cert_bound<SF>(c.rate, c.start, 1.0f);
+                else r = cgap * __builtin_amdgcn_rcpf(cb1) * (1.0f - 4.0f * kU);
             }
             if (fk & 1) {
                 sp_fl1 |= fl;
