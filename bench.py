@@ -55,8 +55,8 @@ def bytes_per_data_symbol(N: int) -> float:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--sf", type=int, default=7)
     ap.add_argument("--bw", type=int, default=125000)
     ap.add_argument("--frames", type=int, default=0, help="frames per GPU (0 = config default)")
@@ -99,10 +99,12 @@ class Workload:
                              flags, payload=self.pay,
                              stream=torch.cuda.current_stream().cuda_stream)
 
-    def _event_ms(self, mode: int, flags: int, reps: int) -> float:
+    def _event_ms(self, mode: int, flags: int, reps: int, warmup: int = 20) -> float:
         """Average device time of one demod_batch call with `flags` (HIP
-        events recorded on the stream the kernels are launched on)."""
-        self.run(mode, flags)
+        events recorded on the stream the kernels are launched on), after
+        `warmup` untimed calls (the clocks settle after a change of load)."""
+        for _ in range(warmup):
+            self.run(mode, flags)
         torch.cuda.synchronize()
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
@@ -113,7 +115,7 @@ class Workload:
         torch.cuda.synchronize()
         return a.elapsed_time(b) / reps
 
-    def stage_times(self, mode: int, reps: int = 5) -> dict:
+    def stage_times(self, mode: int, reps: int = 20) -> dict:
         """Device time per launch of each kernel of the product path: the
         fused prologue+symbols kernel (k_frames, PROLOGUE|SYMBOLS selects it
         alone) and k_finalize; plus the separate-launch path's stages
