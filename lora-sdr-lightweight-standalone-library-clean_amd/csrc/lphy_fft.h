@@ -613,6 +613,75 @@ __device__ __forceinline__ ArgMax2 team_argmax2_first(ArgMax2 a) {
         return a;
     }
 }
+// Keyed top two for the certified symbol-only tiles (LPS <= 16).  A bin's
+// key is its |X|^2 bit pattern (>= 0, so ordered like the value as an
+// unsigned integer) with the KB low bits replaced by an id: the element e in
+// bits 0-3, the team lane in the bits above.  Top two of the keys is one
+// v_max_u32 and one v_med3_u32 per bin, the team merge two DPP moves, a max
+// and a med3 per step.  The result is a bound, not the detector's argmax:
+// with T(k) = k & ~MASK (the value truncated to its high bits), every step
+// is monotone in T, so T(k1) is the largest truncated value and T(k2) the
+// second largest (counted with multiplicity).  When T(k1) > T(k2) the bin of
+// k1 is the unique maximum, v = T(k1) <= its |X|^2 and v2 = T(k2) | MASK >=
+// every other bin's |X|^2; otherwise v <= v2 and the certificate fails (a
+// tie or near-tie goes to the exact recheck, as before).  NaN bins key above
+// every number (v = NaN fails the certificate).  Valid in lane lam == 0.
+__device__ __forceinline__ unsigned med3_u32(unsigned a, unsigned b, unsigned c) {
+    unsigned r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+template <int SF, int OFF = Geo<SF>::LPS / 2>
+__device__ __forceinline__ void team_top2_keys(unsigned& k1, unsigned& k2) {
+    if constexpr (OFF >= 1) {
+        const unsigned o1 = (unsigned)dpp_row_shl<OFF>((int)k1);
+        const unsigned o2 = (unsigned)dpp_row_shl<OFF>((int)k2);
+        k2 = med3_u32(k1, o1, k2 > o2 ? k2 : o2);
+        k1 = k1 > o1 ? k1 : o1;
+        team_top2_keys<SF, OFF / 2>(k1, k2);
+    }
+}
+template <int SF>
+__device__ __forceinline__ ArgMax2 team_argmax2_keyed_first(const cf32 (&v)[16], int lam) {
+    using G = Geo<SF>;
+    static_assert(G::LPS <= 16 && G::E <= 16, "team inside one DPP row, 4 element bits");
+    constexpr Passes<SF> PS{};
+    using PG = PassGeo<SF, PS.hi[PS.n - 1], PS.lo[PS.n - 1]>;
+    constexpr int GS = PG::GS < G::E ? PG::GS : G::E;
+    constexpr int MH = bin_of<SF>(1, 0);
+    constexpr int XS = GS < G::E ? bin_of<SF>(GS, 0) : 0;
+    constexpr int LB = G::LPS >= 16 ? 4 : G::LPS >= 8 ? 3 : G::LPS >= 4 ? 2 : G::LPS >= 2 ? 1 : 0;
+    constexpr unsigned MASK = (1u << (4 + LB)) - 1u;
+    // a lane's first bin (bin_of(0, lam)) as arithmetic on lam
+    constexpr int LMH = PG::MH, LSPAN = PG::SPAN;
+    static_assert([] {
+        for (int l = 0; l < G::LPS; ++l)
+            if (bin_of<SF>(0, l) != (l / LMH) * LSPAN + l % LMH) return false;
+        for (int e = 0; e < G::E; ++e)
+            if (bin_of<SF>(e, 0) != (e % GS) * MH + (e / GS) * XS) return false;
+        return true;
+    }(), "bin_of separable in the lane and element digits");
+    unsigned k1 = 0u, k2 = 0u;
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) {
+        const cf32 sq = v[e] * v[e];
+        const float m2 = sq.x + sq.y;
+        const unsigned key = (__float_as_uint(m2) & ~15u) | (unsigned)e;
+        k2 = med3_u32(k1, k2, key);
+        k1 = k1 > key ? k1 : key;
+    }
+    if constexpr (LB > 0) {
+        k1 = (k1 & ~(MASK & ~15u)) | ((unsigned)lam << 4);
+        team_top2_keys<SF>(k1, k2);
+    }
+    ArgMax2 r;
+    r.v = __uint_as_float(k1 & ~MASK);
+    r.v2 = __uint_as_float(k2 | MASK);
+    const int e = (int)(k1 & 15u), lw = (int)((k1 >> 4) & (MASK >> 4));
+    r.i = ((lw / LMH) * LSPAN + lw % LMH) | ((e % GS) * MH + (e / GS) * XS);
+    return r;
+}
+
 template <int SF, int OFF = Geo<SF>::LPS / 2>
 __device__ __forceinline__ float team_max_first(float a) {
     if constexpr (OFF >= 1) return team_max_first<SF, OFF / 2>(fmaxf(a, dpp_row_shl<OFF>(a)));

@@ -1403,9 +1403,19 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         else fft_tile<SF, true, false, true>(v, lds, slot, lam, twl);
         // (SF <= 8: reduced toward lane lam == 0 by DPP, the only lane that
         // reads it; above, every lane of the team holds it)
+        // (symbol-only tiles: keyed top two, a bound that only certified
+        // symbols use; estimate units need the detector's exact argmax)
         ArgMax2 b2;
-        if constexpr (G::LPS <= 16) b2 = team_argmax2_first<SF>(local_argmax2<SF>(v, lam));
-        else b2 = symbol_argmax2<SF>(local_argmax2<SF>(v, lam));
+        if constexpr (G::LPS <= 16) {
+#ifdef LPHY_EXACT_TOP2  // A/B experiments: the exact top two everywhere
+            b2 = team_argmax2_first<SF>(local_argmax2<SF>(v, lam));
+#else
+            if (emask) b2 = team_argmax2_first<SF>(local_argmax2<SF>(v, lam));
+            else b2 = team_argmax2_keyed_first<SF>(v, lam);
+#endif
+        } else {
+            b2 = symbol_argmax2<SF>(local_argmax2<SF>(v, lam));
+        }
         ArgMax best{b2.v, b2.i};
         if (emask) {
             // detector outputs of the estimate units (LoRaDetector.hpp:60-71)
