@@ -207,42 +207,54 @@ LPHY_HD void sincosf_exact(float y, float* sinp, float* cosp) {
 // atan2f (fdlibm single precision)
 // ---------------------------------------------------------------------------
 LPHY_HD float atanf_exact(float x) {
-    const float atanhi[4] = {4.6364760399e-01f, 7.8539812565e-01f,
-                             9.8279368877e-01f, 1.5707962513e+00f};
-    const float atanlo[4] = {5.0121582440e-09f, 3.7748947079e-08f,
-                             3.4473217170e-08f, 7.5497894159e-08f};
+    // atanhi / atanlo of fdlibm as constants chosen in the argument reduction
+    // (no table: on the GPU an indexed load from a constant table waits for
+    // every load in flight, the fused kernel's prefetched samples included)
     const float aT0 = 3.3333334327e-01f, aT1 = -2.0000000298e-01f,
                 aT2 = 1.4285714924e-01f, aT3 = -1.1111110449e-01f,
                 aT4 = 9.0908870101e-02f, aT5 = -7.6918758452e-02f,
                 aT6 = 6.6610731184e-02f, aT7 = -5.8335702866e-02f,
                 aT8 = 4.9768779427e-02f, aT9 = -3.6531571299e-02f,
                 aT10 = 1.6285819933e-02f;
+    const float hi3 = 1.5707962513e+00f, lo3 = 7.5497894159e-08f;
     int32_t hx = (int32_t)f2u(x);
     int32_t ix = hx & 0x7fffffff;
-    int id;
+    bool red;
+    float hi = 0.0f, lo = 0.0f;
     if (ix >= 0x4c000000) {
         if (ix > 0x7f800000) return x + x;
-        return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+        return hx > 0 ? hi3 + lo3 : -hi3 - lo3;
     }
     if (ix < 0x3ee00000) {
         if (ix < 0x31000000) return x;
-        id = -1;
+        red = false;
     } else {
+        red = true;
         x = u2f(f2u(x) & 0x7fffffffu);
         if (ix < 0x3f980000) {
-            if (ix < 0x3f300000) { id = 0; x = (2.0f * x - 1.0f) / (2.0f + x); }
-            else                 { id = 1; x = (x - 1.0f) / (x + 1.0f); }
+            if (ix < 0x3f300000) {
+                hi = 4.6364760399e-01f; lo = 5.0121582440e-09f;
+                x = (2.0f * x - 1.0f) / (2.0f + x);
+            } else {
+                hi = 7.8539812565e-01f; lo = 3.7748947079e-08f;
+                x = (x - 1.0f) / (x + 1.0f);
+            }
         } else {
-            if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (1.0f + 1.5f * x); }
-            else                 { id = 3; x = -1.0f / x; }
+            if (ix < 0x401c0000) {
+                hi = 9.8279368877e-01f; lo = 3.4473217170e-08f;
+                x = (x - 1.5f) / (1.0f + 1.5f * x);
+            } else {
+                hi = hi3; lo = lo3;
+                x = -1.0f / x;
+            }
         }
     }
     float z = x * x;
     float w = z * z;
     float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
     float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
-    if (id < 0) return x - x * (s1 + s2);
-    z = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    if (!red) return x - x * (s1 + s2);
+    z = hi - ((x * (s1 + s2) - lo) - x);
     return hx < 0 ? -z : z;
 }
 
