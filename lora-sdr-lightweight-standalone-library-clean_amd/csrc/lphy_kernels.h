@@ -896,9 +896,9 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
 // The wave works through a stream of "units" in tiles of WT = 64/LPS, one
 // unit per team of LPS lanes:
 //   [E(0) x2, pad, one spacer tile] then per frame k (a "slice"):
-//   [D(k) x PE, E(k+1) x2, D(k) x (S - PE)],   PE = S + 1 - 2 WT
+//   [D(k) x PE, E(k+1) x2, D(k) x (S - PE)],   PE <= S + 1 - 2 WT
 // so the estimate of frame k+1 shares tiles with symbols of frame k and no
-// team idles, and E(k+1) leads D(k+1) by 2 WT units (two tiles: what the
+// team idles, and E(k+1) leads D(k+1) by >= 2 WT units (two tiles: what the
 // one-tile-ahead IQ prefetch needs).  M(k+1) runs right before the tile
 // holding E(k+1)'s first unit, one slice before D(k+1) re-reads the frame
 // (Infinity-Cache distance).  Measured alternatives, all slower at SF7 than
@@ -1220,8 +1220,23 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     const unsigned nframes = (unsigned)A.frames;
     const unsigned S = (unsigned)A.total_syms, SL = U + S;
     // offset of E(k+1) inside slice k: as late as the two-tile lead over
-    // D(k+1) allows (frames_fit guarantees S + 1 >= 2 WT)
-    const unsigned PE = S + 1 - 2 * WT;
+    // D(k+1) allows (frames_fit guarantees S + 1 >= 2 WT), and moved up to
+    // g - 1 units earlier where that keeps the pair out of two tiles for
+    // every k: unit PT WT + k SL + PE sits at a tile's last team iff its
+    // residue mod g = gcd(SL mod WT, WT) is (WT - 1) mod g.  A straddling
+    // pair makes two mixed tiles (estimate staging, exact transform and top
+    // two for the whole wave) where one suffices: at S = 66, WT = 8 every
+    // other frame straddled at PE = S + 1 - 2 WT.
+    const unsigned PE = [&] {
+        const unsigned pe0 = S + 1 - 2 * WT;
+        if (WT < 2) return pe0;
+        unsigned r = SL % WT, g = WT;
+        while (r) { const unsigned q = g % r; g = r; r = q; }
+        if (g < 2) return pe0;
+        for (unsigned d = 0; d < g && d <= pe0; ++d)
+            if ((PT * WT + pe0 - d) % g != (WT - 1) % g) return pe0 - d;
+        return pe0;
+    }();
     const unsigned W = P.waves;
     const unsigned w = blockIdx.x * WPB + wv;
     if (w >= nframes) return;
@@ -1327,8 +1342,15 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     constexpr float kBig = 3.0e38f;
     float sp_mx0 = 0.0f, sp_mx1 = 0.0f, sp_r0 = kBig, sp_r1 = kBig;
     unsigned sp_fl0 = 0u, sp_fl1 = 0u;
+#ifdef LPHY_PROFILE_PHASES  // timing experiments only: mixed / symbol-only tile clocks
+    unsigned long long ph_mix = 0, ph_sym = 0, ph_fold = 0, n_mix = 0;
+#endif
 
     for (unsigned t = 0; t < ntiles; ++t) {
+#ifdef LPHY_PROFILE_PHASES
+        const unsigned long long p0 = clock64();
+        unsigned long long pf = 0;
+#endif
         cf32 v[16];  // this tile's unit: staged samples, then its bins
         const cf32* rt = rtab[RLDS ? wv : 0][RLDS ? (fk & 1) : 0];
         const cf32* thl = rtab2[RLDS ? 0 : wv][RLDS ? 0 : (fk & 1)];
@@ -1474,6 +1496,9 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             if (redo) A.meta[c.f].status = kStatusRecheck;
         }
         team_sync<SF>();  // slot reads (and ures) done
+#ifdef LPHY_PROFILE_PHASES
+        pf = clock64();
+#endif
         // the frame whose last estimate unit was in this tile: fold
         const bool folding = __ballot(kind == kUnitEst && su == U - 1) != 0;
         if (folding && lane == 0) {
@@ -1566,7 +1591,20 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         fk = nfk;
         su = nsu;
         c = nc;
+#ifdef LPHY_PROFILE_PHASES
+        const unsigned long long p9 = clock64();
+        if (emask) { ph_mix += p9 - p0; ph_fold += p9 - pf; ++n_mix; }
+        else ph_sym += p9 - p0;
+#endif
     }
+#ifdef LPHY_PROFILE_PHASES
+    if (lane == 0) {
+        atomicAdd(&A.counters[1], ph_mix);
+        atomicAdd(&A.counters[2], ph_sym);
+        atomicAdd(&A.counters[3], ph_fold);
+        atomicAdd(&A.counters[4], n_mix);
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
