@@ -1179,9 +1179,14 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     static_assert(TAB, "LDS tables (the doubled down-chirp) for every fused SF");
     constexpr int WT = 64 / G::LPS;               // units per tile
     constexpr unsigned U = 2;                      // estimate units per frame
-    // prefix tiles: E of the first frame, then one tile that keeps its
-    // symbols two tiles behind it like every later frame's
-    constexpr unsigned PT = (U + WT - 1) / WT + 1;
+    // frames per group: the estimate units of F frames fill whole tiles
+    // (EBT estimate-only tiles), so no tile mixes estimates with symbols
+    constexpr unsigned F = WT >= (int)U ? (unsigned)WT / U : 1u;
+    constexpr unsigned EBU = U * F, EBT = (EBU + WT - 1) / WT;
+    // prefix tiles: EB(0), then one tile that keeps group 0's symbols two
+    // tiles behind it like every later group's
+    constexpr unsigned PT = EBT + 1;
+    constexpr unsigned NSLOT = 2 * F;  // frame slots: the group in demodulation, the next one
     constexpr int WPB = kTile / 64;
     // rotation tables: per-wave LDS ring of two frames up to SF 8, per-lane
     // registers (built when a team reaches a new frame) for SF 9-10
@@ -1193,13 +1198,13 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     // chirp indices t0 + i, i < N, need no wrap
     __shared__ cf32 dnl[TAB ? 2 * N : 1];
     __shared__ float wnl[TAB ? N : 1];
-    __shared__ UnitResult ures[WPB][U];
-    __shared__ float4 ring[WPB][3];  // frame records: rate, scale, t_off, flags
-    __shared__ float ringmx[WPB][3];  // ... and the max-abs their normalisation used
-    __shared__ cf32 rtab[RLDS ? WPB : 1][2][RLDS ? N : 1];
+    __shared__ UnitResult ures[WPB][F][U];
+    __shared__ float4 ring[WPB][NSLOT];  // frame records: rate, scale, t_off, flags
+    __shared__ float ringmx[WPB][NSLOT];  // ... and the max-abs their normalisation used
+    __shared__ cf32 rtab[RLDS ? WPB : 1][RLDS ? NSLOT : 1][RLDS ? N : 1];
     // SF 9-10: two-table rotation per frame (64 low + N/64 high entries): a
     // whole-symbol table per lane cost 32 VGPRs and spilled
-    __shared__ cf32 rtab2[RLDS ? 1 : WPB][2][RLDS ? 1 : 64 + N / 64];
+    __shared__ cf32 rtab2[RLDS ? 1 : WPB][RLDS ? 1 : NSLOT][RLDS ? 1 : 64 + N / 64];
 
     const int tid = threadIdx.x;
     for (int i = tid; i < N; i += kTile) {
@@ -1218,31 +1223,22 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     const unsigned wslot = (unsigned)(slot % WT);
     const int fl = first_pass_index<SF>(0, lam);  // lane part of the sample index
     const unsigned nframes = (unsigned)A.frames;
-    const unsigned S = (unsigned)A.total_syms, SL = U + S;
-    // offset of E(k+1) inside slice k: as late as the two-tile lead over
-    // D(k+1) allows (frames_fit guarantees S + 1 >= 2 WT), and moved up to
-    // g - 1 units earlier where that keeps the pair out of two tiles for
-    // every k: unit PT WT + k SL + PE sits at a tile's last team iff its
-    // residue mod g = gcd(SL mod WT, WT) is (WT - 1) mod g.  A straddling
-    // pair makes two mixed tiles (estimate staging, exact transform and top
-    // two for the whole wave) where one suffices: at S = 66, WT = 8 every
-    // other frame straddled at PE = S + 1 - 2 WT.
-    const unsigned PE = [&] {
-        const unsigned pe0 = S + 1 - 2 * WT;
-        if (WT < 2) return pe0;
-        unsigned r = SL % WT, g = WT;
-        while (r) { const unsigned q = g % r; g = r; r = q; }
-        if (g < 2) return pe0;
-        for (unsigned d = 0; d < g && d <= pe0; ++d)
-            if ((PT * WT + pe0 - d) % g != (WT - 1) % g) return pe0 - d;
-        return pe0;
-    }();
+    const unsigned S = (unsigned)A.total_syms;
     const unsigned W = P.waves;
     const unsigned w = blockIdx.x * WPB + wv;
     if (w >= nframes) return;
     const unsigned nk = (nframes - 1 - w) / W + 1;  // frames of this wave
-    const unsigned long long L = (unsigned long long)PT * WT + (unsigned long long)nk * SL;
-    const unsigned ntiles = (unsigned)((L + WT - 1) / WT);
+    // group g: D(g) = the F S symbol units of frames gF..gF+F-1 in DBT tiles
+    // (the last one padded with dead units), and EB(g+1) = the next group's
+    // estimate units in EBT tiles after D(g)'s first PB = DBT - 1 tiles, so
+    // that the last EB tile folds two tiles before D(g+1) starts (what the
+    // one-tile-ahead context and IQ prefetch need; frames_fit: S >= WT, so
+    // DBT >= 2 and the scan ahead of EB(g+1) runs in a D(g) tile)
+    const unsigned DBT = (F * S + WT - 1) / WT, GT = DBT + EBT, PB = DBT - 1;
+    const unsigned ng = (nk + F - 1) / F;
+    const unsigned dt_last = ((nk - (ng - 1) * F) * S + WT - 1) / WT;  // live D tiles of the last group
+    const unsigned ntiles = PT + (ng - 1) * GT + (dt_last <= PB ? dt_last : dt_last + EBT);
+    auto slot_of = [](unsigned kf) -> unsigned { return ((kf / F) & 1u) * F + kf % F; };
     const bool exact_only = A.exact_rotation != 0;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     // Speculative normalisation (modes 1/2).  The reference scales the whole
@@ -1257,29 +1253,33 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     // re-checked against the exact rate, else the whole-frame re-run).
     const bool spec = (MODE & 3) != LPHY_MODE_DEMODULATE && A.spec != 0;
 
-    // unit of this team in tile t; (k, o) = slice and offset for t >= PT
-    auto unit_of = [&](unsigned t, unsigned k, unsigned o, unsigned& kind, unsigned& fk,
-                       unsigned& s) {
+    // unit of this team in tile t; for t >= PT: group g, tile tg of the
+    // group, and the team's symbol unit (frame dj of the group, symbol ds)
+    // when tg is a D tile
+    auto unit_of = [&](unsigned t, unsigned g, unsigned tg, unsigned dj, unsigned ds, unsigned& kind,
+                       unsigned& fk, unsigned& s) {
         if (t < PT) {
             const unsigned q = t * WT + wslot;
-            kind = q < U ? kUnitEst : kUnitDead;
-            fk = 0;
-            s = q;
-        } else if (o >= PE && o < PE + U) {
-            kind = k + 1 < nk ? kUnitEst : kUnitDead;
-            fk = k + 1;
-            s = o - PE;
+            const bool e = t < EBT && q < EBU;
+            fk = e ? q / U : 0u;
+            s = e ? q % U : 0u;
+            kind = e && fk < nk ? kUnitEst : kUnitDead;
+        } else if (tg >= PB && tg < PB + EBT) {
+            const unsigned q = (tg - PB) * WT + wslot;
+            fk = (g + 1) * F + q / U;
+            s = q % U;
+            kind = q < EBU && fk < nk ? kUnitEst : kUnitDead;
         } else {
-            kind = k < nk ? kUnitSym : kUnitDead;
-            fk = k;
-            s = o < PE ? o : o - U;
+            fk = g * F + dj;
+            s = ds;
+            kind = dj < F && fk < nk ? kUnitSym : kUnitDead;
         }
     };
     // context of a unit; symbol units read their frame record from the ring
     auto ctx_of = [&](unsigned kind, unsigned fk, unsigned s) -> SymCtx {
         const unsigned f = w + fk * W;
         if (kind == kUnitSym) {
-            const float4 r = ring[wv][fk % 3];
+            const float4 r = ring[wv][slot_of(fk)];
             lphy_frame_meta m{};
             m.rate = r.x;
             m.scale = r.y;
@@ -1298,33 +1298,34 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         return c;
     };
 
-    unsigned k = 0, o = wslot;  // position of tile t (t >= PT)
+    unsigned g = 0, tg = 0, dj = 0, ds = wslot;  // position of tile t (t >= PT)
     unsigned kind, fk, su;
-    unit_of(0, k, o, kind, fk, su);
+    unit_of(0, g, tg, dj, ds, kind, fk, su);
     SymCtx c = ctx_of(kind, fk, su);
-    // M (modes 1/2): the max-abs scan of a frame runs in the tile before the
-    // one holding its first estimate unit, between that tile's staging and
-    // its IQ prefetch, when no tile data is held in registers; tile 0 holds
-    // E(0), scanned here.  (Measured alternative, 1.4x slower at SF7: the
-    // scan streamed one chunk per tile through a per-wave LDS buffer by
-    // LDS-DMA, issued after staging and folded a tile later - never behind
-    // the estimates, yet the chunk traffic and its folds cost more than the
-    // blocking scan's exposed latency.)
-    unsigned m_seq = 0xffffffffu;  // frame whose max-abs `mx` holds
-    float mx = 0.0f;
-    float mxe = 0.0f;              // max-abs of the frame estimated in this tile
+    // M (modes 1/2): the max-abs scans of a group's frames run in the tile
+    // before its first EB tile, between that tile's staging and its IQ
+    // prefetch, when no tile data is held in registers; tile 0 holds EB(0),
+    // scanned here.  Each frame's maximum goes to its slot of ringmx.
+    // (Measured alternative, 1.4x slower at SF7: the scan streamed one
+    // chunk per tile through a per-wave LDS buffer by LDS-DMA, issued after
+    // staging and folded a tile later.)
+    unsigned m_seq = 0xffffffffu;  // group whose frames are scanned
     auto scan_ahead = [&](unsigned nkind_, unsigned nfk_) {
         if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) {
             const unsigned long long nem = __ballot(nkind_ == kUnitEst);
             if (nem) {
-                const unsigned nke = (unsigned)__shfl((int)nfk_, __ffsll((long long)nem) - 1, 64);
-                if (nke != m_seq) {
+                const unsigned grp = (unsigned)__shfl((int)nfk_, __ffsll((long long)nem) - 1, 64) / F;
+                if (grp != m_seq) {
+                    for (unsigned j = 0; j < F && grp * F + j < nk; ++j) {
+                        const unsigned kk = grp * F + j;
 #ifdef LPHY_ABLATE_FRAME_SCAN  // timing experiments only
-                    mx = 1.0f;
+                        const float m = 1.0f;
 #else
-                    mx = wave_maxabs<SF, MODE>(A, w + nke * W, down, spec ? 2u * N : 0u);
+                        const float m = wave_maxabs<SF, MODE>(A, w + kk * W, down, spec ? 2u * N : 0u);
 #endif
-                    m_seq = nke;
+                        if (lane == 0) ringmx[wv][slot_of(kk)] = m;
+                    }
+                    m_seq = grp;
                 }
             }
         }
@@ -1352,18 +1353,16 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         unsigned long long pf = 0;
 #endif
         cf32 v[16];  // this tile's unit: staged samples, then its bins
-        const cf32* rt = rtab[RLDS ? wv : 0][RLDS ? (fk & 1) : 0];
-        const cf32* thl = rtab2[RLDS ? 0 : wv][RLDS ? 0 : (fk & 1)];
-        // estimate units in this tile (all of one frame): its max-abs first
+        const cf32* rt = rtab[RLDS ? wv : 0][RLDS ? slot_of(fk) : 0];
+        const cf32* thl = rtab2[RLDS ? 0 : wv][RLDS ? 0 : slot_of(fk)];
+        // an EB tile (estimate units of one group, and dead units): each
+        // unit's frame max-abs, scanned ahead, first
         const unsigned long long emask = __ballot(kind == kUnitEst);
-        unsigned ke = 0;
         float amax;
         if (emask) {
-            ke = (unsigned)__shfl((int)fk, __ffsll((long long)emask) - 1, 64);
-            mxe = mx;  // scanned ahead (frame ke == m_seq)
             if (kind == kUnitEst) {
                 if ((MODE & 3) != LPHY_MODE_DEMODULATE) {
-                    const lphy_frame_meta nm = norm_meta_hot(mxe, true, A.no_scratch);
+                    const lphy_frame_meta nm = norm_meta_hot(ringmx[wv][slot_of(fk)], true, A.no_scratch);
                     c.scale = nm.scale;
                     c.live = nm.status == 0;
                 }
@@ -1394,16 +1393,18 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         team_sync<SF>();
 
         // next tile's unit, context and IQ (in flight during the FFT)
-        unsigned nkk = k, no = o;
+        unsigned ng_ = g, ntg = tg, ndj = dj, nds = ds;
         if (t + 1 == PT) {
-            nkk = 0;
-            no = wslot;
+            ng_ = 0; ntg = 0; ndj = 0; nds = wslot;
         } else if (t + 1 > PT) {
-            no += WT;
-            if (no >= SL) { no -= SL; ++nkk; }
+            if (tg < PB || tg >= PB + EBT) {  // tile t was a D tile
+                nds += WT;
+                if (nds >= S) { nds -= S; ++ndj; }
+            }
+            if (++ntg == GT) { ntg = 0; ++ng_; ndj = 0; nds = wslot; }
         }
         unsigned nkind, nfk, nsu;
-        unit_of(t + 1, nkk, no, nkind, nfk, nsu);
+        unit_of(t + 1, ng_, ntg, ndj, nds, nkind, nfk, nsu);
         if (t + 1 < ntiles) scan_ahead(nkind, nfk);
         const SymCtx nc = ctx_of(nkind, nfk, nsu);
         if (t + 1 < ntiles) {
@@ -1449,8 +1450,9 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             // a NaN bin may hide an Annex G product: exact re-run (k_post)
             const unsigned long long nanm = __ballot(kind == kUnitEst && c.ok && fft_has_nan<SF>(v));
             if (kind == kUnitEst && lam == 0) {
-                ures[wv][su] = c.ok ? unit_result<SF>(lds, slot, best) : UnitResult{0, 0, 0.0f, 0.0f};
-                ures[wv][su].nan = ((nanm >> (slot * G::LPS)) & ((G::LPS == 64) ? ~0ull : ((1ull << G::LPS) - 1))) != 0;
+                UnitResult& ur = ures[wv][fk % F][su];
+                ur = c.ok ? unit_result<SF>(lds, slot, best) : UnitResult{0, 0, 0.0f, 0.0f};
+                ur.nan = ((nanm >> (slot * G::LPS)) & ((G::LPS == 64) ? ~0ull : ((1ull << G::LPS) - 1))) != 0;
             }
             team_sync<SF>();  // slot reads done before a re-check restages
         }
@@ -1499,19 +1501,22 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
 #ifdef LPHY_PROFILE_PHASES
         pf = clock64();
 #endif
-        // the frame whose last estimate unit was in this tile: fold
-        const bool folding = __ballot(kind == kUnitEst && su == U - 1) != 0;
-        if (folding && lane == 0) {
+        // the frames whose last estimate unit was in this tile: each folds on
+        // the first lane of the team holding that unit (F lanes at once)
+        const bool my_fold = kind == kUnitEst && su == U - 1 && lam == 0;
+        const unsigned long long fmask = __ballot(my_fold);
+        if (my_fold) {
+            const unsigned sl = slot_of(fk);
             lphy_frame_meta m{};
             m.scale = 1.0f;
             m.have_sync = 1;
-            if ((MODE & 3) != LPHY_MODE_DEMODULATE) m = norm_meta_hot(mxe, true, A.no_scratch);
+            if ((MODE & 3) != LPHY_MODE_DEMODULATE) m = norm_meta_hot(ringmx[wv][sl], true, A.no_scratch);
             if (m.status == 0) {
                 EstFold fold;
                 bool nan = false;
 #pragma unroll
                 for (unsigned u = 0; u < U; ++u) {
-                    const UnitResult r = ures[wv][u];
+                    const UnitResult r = ures[wv][fk % F][u];
                     nan |= r.nan != 0;
                     if (r.valid) fold.add(r.idx, r.findex, 0, r.phase);
                     else fold.add(0, 0.0f, 0, 0.0f);
@@ -1519,21 +1524,22 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
                 fold.finish(m, (int)U, N, 1);
                 if (nan) m.status = kStatusFixup;
             }
-            ring[wv][ke % 3] = float4{m.rate, m.scale, __int_as_float(m.t_off),
-                                      __uint_as_float((m.status == 0 ? 1u : 0u) | 2u)};
-            ringmx[wv][ke % 3] = mxe;
-            meta_put_est(&A.meta[w + ke * W], m);
+            ring[wv][sl] = float4{m.rate, m.scale, __int_as_float(m.t_off),
+                                  __uint_as_float((m.status == 0 ? 1u : 0u) | 2u)};
+            meta_put_est(&A.meta[w + fk * W], m);
         }
         team_sync<SF>();
-        // the folded frame's rotation table, first read two tiles later (its
-        // slot's previous frame, ke - 2, has no units left)
-        if (folding) {
-            const float4 r = ring[wv][ke % 3];
+        // the folded frames' rotation tables, first read two tiles later
+        // (their slots' previous frames, of group g - 1, have no units left)
+        for (unsigned long long fm = fmask; fm; fm &= fm - 1) {
+            const unsigned kf = (unsigned)__shfl((int)fk, __ffsll((long long)fm) - 1, 64);
+            const unsigned sl = slot_of(kf);
+            const float4 r = ring[wv][sl];
             if (__float_as_uint(r.w) & 1u) {
                 if constexpr (RLDS) {
-                    build_rtab<SF, MODE>(rtab[wv][ke & 1], r.x, r.y, __float_as_int(r.z), down, win, lane);
+                    build_rtab<SF, MODE>(rtab[wv][sl], r.x, r.y, __float_as_int(r.z), down, win, lane);
                 } else {
-                    cf32* tb = rtab2[wv][ke & 1];
+                    cf32* tb = rtab2[wv][sl];
                     for (int j = lane; j < 64 + N / 64; j += 64) {
                         const int ph = j < 64 ? j : 64 * (j - 64);
                         float sn, cs;
@@ -1563,7 +1569,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
                     r = fminf(r, __shfl_xor(r, off, 64));
                 }
                 const bool nan = __ballot(fl & 1u) != 0, open = __ballot(fl & 2u) != 0;
-                const float4 rr = ring[wv][kf % 3];
+                const float4 rr = ring[wv][slot_of(kf)];
                 if (__float_as_uint(rr.w) & 1u) {
                     const unsigned f = w + kf * W;
                     const unsigned cnt = DECH ? S * N : (unsigned)A.frame_samples;
@@ -1571,7 +1577,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
                     bool fbad = false;
                     if (end < cnt) m = fmaxf(m, wave_range_maxabs<SF, MODE>(A, f, end, cnt, down, fbad));
                     if (lane == 0) {
-                        const float mx01 = ringmx[wv][kf % 3];
+                        const float mx01 = ringmx[wv][slot_of(kf)];
                         const float mt = fmaxf(m, mx01);
                         const lphy_frame_meta mg = norm_meta(mx01, true, 0), me = norm_meta(mt, true, 0);
                         if (nan || fbad || !(mt <= 3.40282347e38f)) {
@@ -1585,8 +1591,10 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
                 }
             }
         }
-        k = nkk;
-        o = no;
+        g = ng_;
+        tg = ntg;
+        dj = ndj;
+        ds = nds;
         kind = nkind;
         fk = nfk;
         su = nsu;
