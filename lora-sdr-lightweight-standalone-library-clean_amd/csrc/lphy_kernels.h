@@ -894,19 +894,27 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
 //      fold into the frame's offsets
 //   D  the frame's symbols (rotation, FFT, argmax)
 // The wave works through a stream of "units" in tiles of WT = 64/LPS, one
-// unit per team of LPS lanes:
-//   [E(0) x2, pad, one spacer tile] then per frame k (a "slice"):
-//   [D(k) x PE, E(k+1) x2, D(k) x (S - PE)],   PE <= S + 1 - 2 WT
-// so the estimate of frame k+1 shares tiles with symbols of frame k and no
-// team idles, and E(k+1) leads D(k+1) by >= 2 WT units (two tiles: what the
-// one-tile-ahead IQ prefetch needs).  M(k+1) runs right before the tile
-// holding E(k+1)'s first unit, one slice before D(k+1) re-reads the frame
-// (Infinity-Cache distance).  Measured alternatives, all slower at SF7 than
-// this blocking 16-deep scan (2.3 ms per 65,536 frames): M streamed in row
-// chunks held in registers across the FFT (spills, 1.35x), M streamed by
-// LDS-DMA into a per-wave ring (1.15x), scan-only workgroups beside the
-// symbol waves (1.3-5x: they need ~25 % of the slots to stay ahead).
-// Frame records pass between teams through a 3-slot ring per wave in LDS.  Compared with separate launches this
+// unit per team of LPS lanes.  Its frames go in groups of F = WT/2 (at
+// least 1), whose 2F estimate units fill EBT whole tiles (EB):
+//   [EB(0), one spacer tile] then per group g:
+//   [D(g): DBT - 1 tiles, EB(g+1), D(g): its last tile]
+// where D(g) is the F S symbol units of the group (the last tile padded
+// with dead units).  No tile mixes estimate units with symbol units: a
+// mixed tile runs the estimate staging, the exact transform and the exact
+// top two for the whole wave (measured at SF7: one mixed tile per frame
+// cost 1.8x a symbol tile, 20 % of the wave's clocks; a whole EB tile for
+// four frames costs 2.1x, 6 %).  The F frames of an EB tile fold on the
+// first lanes of their teams at once.  EB(g+1) folds two tiles before
+// D(g+1) starts (what the one-tile-ahead context and IQ prefetch need).
+// M of group g+1's frames runs right before the EB tile.  Measured
+// alternatives, all slower at SF7 than this blocking 8-deep scan: M
+// streamed in row chunks held in registers across the FFT (spills, 1.35x),
+// M streamed by LDS-DMA into a per-wave ring (1.15x), scan-only workgroups
+// beside the symbol waves (1.3-5x: they need ~25 % of the slots to stay
+// ahead), the group's F scans with all their loads in flight at once (2 %
+// slower in mode 2).
+// Frame records pass between teams through a 2F-slot ring per wave in LDS
+// (the group in demodulation and the next one).  Compared with separate launches this
 // removes a whole-batch pass (the prologue kernels) and overlaps the
 // HBM-bound max-abs scans of some waves with the VALU-bound transforms of
 // the others.
