@@ -1129,10 +1129,10 @@ enum : int { kUnitDead = 0, kUnitEst = 1, kUnitSym = 2 };
 // The samples are held in first-pass order (element e of lane lam is sample
 // fl + first_pass_index<SF>(e, 0), fl = the lane part): the staged values
 // stay in registers and the transform starts there (fft_tile REG0).
-template <int SF, int MODE, bool MIXED>
-__device__ __forceinline__ float stage_fast(cf32 (&v)[16], const cf32 (&raw)[16], const SymCtx& c, int fl,
+template <int SF, int MODE, bool MIXED, bool EARLY>
+__device__ __forceinline__ float stage_fast(cf32 (&v)[16], cf32 (&raw)[16], const SymCtx& c, int fl,
                                             const cf32* down, const float* win, const cf32* rt,
-                                            const cf32* thl, bool est) {
+                                            const cf32* thl, bool est, const cf32* nsrc) {
     using G = Geo<SF>;
     constexpr int N = G::N;
     constexpr bool RLDS = SF <= 8;
@@ -1147,6 +1147,7 @@ __device__ __forceinline__ float stage_fast(cf32 (&v)[16], const cf32 (&raw)[16]
         for (int e = 0; e < G::E; ++e) {
             const int ce = first_pass_index<SF>(e, 0);
             cf32 p = raw[e];
+            if constexpr (EARLY) raw[e] = nsrc[ce];  // the next tile's sample, as this one is consumed
             if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) {
                 if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) p = cmul(p, dl[ce]);
                 p = cscale(p, c.scale);
@@ -1160,6 +1161,7 @@ __device__ __forceinline__ float stage_fast(cf32 (&v)[16], const cf32 (&raw)[16]
         for (int e = 0; e < G::E; ++e) {
             const int ce = first_pass_index<SF>(e, 0);
             cf32 p = raw[e];
+            if constexpr (EARLY) raw[e] = nsrc[ce];
             if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) p = cmul(p, dl[ce]);
             amax = max3_abs(amax, p.x, p.y);
             if constexpr (RLDS) {
@@ -1260,6 +1262,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     // the frame goes to k_post's settle_frames (exact estimate, certificates
     // re-checked against the exact rate, else the whole-frame re-run).
     const bool spec = (MODE & 3) != LPHY_MODE_DEMODULATE && A.spec != 0;
+    constexpr bool EARLY = (MODE & 3) == LPHY_MODE_DEMODULATE && SF == 7;
 
     // unit of this team in tile t; for t >= PT: group g, tile tg of the
     // group, and the team's symbol unit (frame dj of the group, symbol ds)
@@ -1363,6 +1366,34 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         cf32 v[16];  // this tile's unit: staged samples, then its bins
         const cf32* rt = rtab[RLDS ? wv : 0][RLDS ? slot_of(fk) : 0];
         const cf32* thl = rtab2[RLDS ? 0 : wv][RLDS ? 0 : slot_of(fk)];
+        // next tile's unit and context
+        unsigned ng_ = g, ntg = tg, ndj = dj, nds = ds;
+        unsigned nkind, nfk, nsu;
+        SymCtx nc;
+        auto next_unit = [&] {
+            if (t + 1 == PT) {
+                ng_ = 0; ntg = 0; ndj = 0; nds = wslot;
+            } else if (t + 1 > PT) {
+                if (tg < PB || tg >= PB + EBT) {  // tile t was a D tile
+                    nds += WT;
+                    if (nds >= S) { nds -= S; ++ndj; }
+                }
+                if (++ntg == GT) { ntg = 0; ++ng_; ndj = 0; nds = wslot; }
+            }
+            unit_of(t + 1, ng_, ntg, ndj, nds, nkind, nfk, nsu);
+            if (t + 1 < ntiles) scan_ahead(nkind, nfk);
+            nc = ctx_of(nkind, nfk, nsu);
+        };
+        // EARLY (mode 0 at SF7, measured): the next tile's IQ is loaded as
+        // this tile's staging consumes the registers, so it is in flight
+        // during staging and the FFT; the next group's scans run first,
+        // while only `raw` is live.  (In mode 2 this was 13 % slower.)  The
+        // last tile reloads a valid window: a dead unit's is frame w's first.
+        const cf32* nsrc = nullptr;
+        if constexpr (EARLY) {
+            next_unit();
+            nsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base + fl;
+        }
         // an EB tile (estimate units of one group, and dead units): each
         // unit's frame max-abs, scanned ahead, first
         const unsigned long long emask = __ballot(kind == kUnitEst);
@@ -1376,9 +1407,9 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
                 }
                 c.ok = c.live;  // estimate this unit (else stage zeros)
             }
-            amax = stage_fast<SF, MODE, true>(v, raw, c, fl, down, win, rt, thl, kind != kUnitSym);
+            amax = stage_fast<SF, MODE, true, EARLY>(v, raw, c, fl, down, win, rt, thl, kind != kUnitSym, nsrc);
         } else {
-            amax = stage_fast<SF, MODE, false>(v, raw, c, fl, down, win, rt, thl, false);
+            amax = stage_fast<SF, MODE, false, EARLY>(v, raw, c, fl, down, win, rt, thl, false, nsrc);
         }
         if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) {
             if constexpr (G::LPS <= 16) {
@@ -1400,31 +1431,14 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         }
         team_sync<SF>();
 
-        // next tile's unit, context and IQ (in flight during the FFT)
-        unsigned ng_ = g, ntg = tg, ndj = dj, nds = ds;
-        if (t + 1 == PT) {
-            ng_ = 0; ntg = 0; ndj = 0; nds = wslot;
-        } else if (t + 1 > PT) {
-            if (tg < PB || tg >= PB + EBT) {  // tile t was a D tile
-                nds += WT;
-                if (nds >= S) { nds -= S; ++ndj; }
+        if constexpr (!EARLY) {
+            // next tile's unit, context and IQ (in flight during the FFT)
+            next_unit();
+            if (t + 1 < ntiles) {
+                const cf32* lsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base + fl;
+#pragma unroll
+                for (int e = 0; e < G::E; ++e) raw[e] = lsrc[first_pass_index<SF>(e, 0)];
             }
-            if (++ntg == GT) { ntg = 0; ++ng_; ndj = 0; nds = wslot; }
-        }
-        unsigned nkind, nfk, nsu;
-        unit_of(t + 1, ng_, ntg, ndj, nds, nkind, nfk, nsu);
-        if (t + 1 < ntiles) scan_ahead(nkind, nfk);
-        const SymCtx nc = ctx_of(nkind, nfk, nsu);
-        if (t + 1 < ntiles) {
-            const cf32* nsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base + fl;
-#ifdef LPHY_ABLATE_FRAME_LOAD  // timing experiments only: no IQ traffic
-            (void)nsrc;
-#pragma unroll
-            for (int e = 0; e < G::E; ++e) raw[e] = raw[e] * 0.999f + cf32{(float)e, (float)t};
-#else
-#pragma unroll
-            for (int e = 0; e < G::E; ++e) raw[e] = nsrc[first_pass_index<SF>(e, 0)];
-#endif
         }
 
         // tiles of symbol units only: magnitude-only transform (fft_tile TRIV)
