@@ -236,3 +236,34 @@ def test_nonfinite_frames_maxabs(oracle, lphy):
                 np.testing.assert_array_equal(syms[f], osyms, err_msg=ctx)
                 assert _bits(meta["cfo"][f]) == _bits(omet[0]), ctx
                 assert _bits(meta["time_offset"][f]) == _bits(omet[1]), ctx
+
+
+@pytest.mark.parametrize("sf,nf,S", [(7, 2048 * 5 + 123, 19), (8, 2048 * 3 + 77, 11), (6, 2048 * 3 + 5, 33)])
+def test_fused_frame_groups(oracle, lphy, sf, nf, S):
+    """k_frames' frame groups (F = WT/2 frames share estimate-only tiles):
+    several groups per wave, a partial last group, and S with F*S not a
+    multiple of the tile (dead padding units), fused against the separate
+    launches on every output bit, the first frames against the oracle."""
+    rng = np.random.default_rng(sf * 7 + nf)
+    N = 1 << sf
+    base = oracle.modulate(oracle.encode(bytes(range(S // 2 - 1 if S % 2 == 0 else S // 2))), sf)
+    fs = S * N
+    base = np.resize(base, fs).astype(np.complex64)
+    t = np.arange(fs, dtype=np.float32)
+    cfo = rng.uniform(-0.4, 0.4, nf).astype(np.float32)
+    iq = base[None, :] * np.exp((2j * np.pi / N) * cfo[:, None] * t[None, :]).astype(np.complex64)
+    sig = np.array([0.0, 0.05, 0.5, 2.0], np.float32)[np.arange(nf) % 4]
+    iq += sig[:, None] * (rng.standard_normal((nf, fs), np.float32) +
+                          1j * rng.standard_normal((nf, fs), np.float32)).astype(np.complex64)
+    iq *= np.array([1.0, 0.5, 3.0], np.float32)[np.arange(nf) % 3][:, None]
+    iq = np.ascontiguousarray(iq.astype(np.complex64))
+    d = lphy.Demodulator(sf)
+    for mode in (lphy.MODE_DEMODULATE, lphy.MODE_DECHIRP_LORA_DEMODULATE):
+        a = d.demod_host(iq, nf, fs, mode, 0)
+        b = d.demod_host(iq, nf, fs, mode, lphy.F_UNFUSED)
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[2].view(np.uint8), b[2].view(np.uint8))
+    for f in (0, 1, nf - 1):
+        r, osyms, osync, omet = oracle.lora_demodulate(oracle.dechirp(iq[f], sf, 125000), sf)
+        np.testing.assert_array_equal(a[0][f], osyms)
+        assert _bits(a[2]["cfo"][f]) == _bits(omet[0])
