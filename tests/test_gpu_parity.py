@@ -267,3 +267,22 @@ def test_fused_frame_groups(oracle, lphy, sf, nf, S):
         r, osyms, osync, omet = oracle.lora_demodulate(oracle.dechirp(iq[f], sf, 125000), sf)
         np.testing.assert_array_equal(a[0][f], osyms)
         assert _bits(a[2]["cfo"][f]) == _bits(omet[0])
+
+
+@pytest.mark.parametrize("n", [8, 64, 66, 130, 512])
+def test_decode_finalize_vs_oracle(oracle, lphy, n):
+    """The finalisation's decode (Hamming 8,4 syndromes as parities, 16-byte
+    symbol loads with a scalar tail) and its byte-wise SX1272 checksum
+    against the oracle (LoRaDecoder.cpp:7-21, LoRaCodes.hpp:69-105, 250-281);
+    every low-byte value occurs in both nibble positions."""
+    rng = np.random.default_rng(n)
+    d = lphy.Demodulator(7)
+    for rep in range(4):
+        syms = rng.integers(0, 1 << 16, n, dtype=np.uint16)
+        if rep == 0:
+            syms[: min(n, 256)] = np.arange(min(n, 256), dtype=np.uint16) * 257
+        rc, out, meta = d.decode_host(syms)
+        r, obytes, ocrc = oracle.decode(syms)
+        assert rc == 0 and r == n // 2
+        np.testing.assert_array_equal(out, obytes)
+        assert meta["crc_ok"] == ocrc
