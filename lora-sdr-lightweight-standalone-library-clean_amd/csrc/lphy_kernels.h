@@ -1262,7 +1262,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     // the frame goes to k_post's settle_frames (exact estimate, certificates
     // re-checked against the exact rate, else the whole-frame re-run).
     const bool spec = (MODE & 3) != LPHY_MODE_DEMODULATE && A.spec != 0;
-    constexpr bool EARLY = (MODE & 3) == LPHY_MODE_DEMODULATE && SF == 7;
+    constexpr bool EARLY = (MODE & 3) == LPHY_MODE_DEMODULATE && (SF == 7 || SF == 8);
 
     // unit of this team in tile t; for t >= PT: group g, tile tg of the
     // group, and the team's symbol unit (frame dj of the group, symbol ds)
@@ -1370,7 +1370,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         unsigned ng_ = g, ntg = tg, ndj = dj, nds = ds;
         unsigned nkind, nfk, nsu;
         SymCtx nc;
-        auto next_unit = [&] {
+        auto next_pos = [&] {
             if (t + 1 == PT) {
                 ng_ = 0; ntg = 0; ndj = 0; nds = wslot;
             } else if (t + 1 > PT) {
@@ -1381,17 +1381,24 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
                 if (++ntg == GT) { ntg = 0; ++ng_; ndj = 0; nds = wslot; }
             }
             unit_of(t + 1, ng_, ntg, ndj, nds, nkind, nfk, nsu);
+        };
+        auto next_ctx = [&] {
             if (t + 1 < ntiles) scan_ahead(nkind, nfk);
             nc = ctx_of(nkind, nfk, nsu);
         };
-        // EARLY (mode 0 at SF7, measured): the next tile's IQ is loaded as
+        // EARLY (mode 0 at SF 7-8, measured): the next tile's IQ is loaded as
         // this tile's staging consumes the registers, so it is in flight
-        // during staging and the FFT; the next group's scans run first,
-        // while only `raw` is live.  (In mode 2 this was 13 % slower.)  The
-        // last tile reloads a valid window: a dead unit's is frame w's first.
+        // during staging and the FFT.  (Mode 2: 13 % slower at SF7, mode 0
+        // at SF9: 6 % slower.)  The last tile reloads a valid window: a
+        // dead unit's is frame w's first.
         const cf32* nsrc = nullptr;
-        if constexpr (EARLY) {
-            next_unit();
+        next_pos();
+        // (measured alternative: early in modes 1/2 too, except in the tile
+        // before an EB tile, whose scans need the registers: 4-5x slower,
+        // the two staging variants of one loop spilled)
+        constexpr bool early = EARLY;
+        if (early) {
+            next_ctx();
             nsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base + fl;
         }
         // an EB tile (estimate units of one group, and dead units): each
@@ -1407,9 +1414,11 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
                 }
                 c.ok = c.live;  // estimate this unit (else stage zeros)
             }
-            amax = stage_fast<SF, MODE, true, EARLY>(v, raw, c, fl, down, win, rt, thl, kind != kUnitSym, nsrc);
+            amax = early ? stage_fast<SF, MODE, true, true>(v, raw, c, fl, down, win, rt, thl, kind != kUnitSym, nsrc)
+                         : stage_fast<SF, MODE, true, false>(v, raw, c, fl, down, win, rt, thl, kind != kUnitSym, nsrc);
         } else {
-            amax = stage_fast<SF, MODE, false, EARLY>(v, raw, c, fl, down, win, rt, thl, false, nsrc);
+            amax = early ? stage_fast<SF, MODE, false, true>(v, raw, c, fl, down, win, rt, thl, false, nsrc)
+                         : stage_fast<SF, MODE, false, false>(v, raw, c, fl, down, win, rt, thl, false, nsrc);
         }
         if constexpr ((MODE & 3) == LPHY_MODE_DEMODULATE) {
             if constexpr (G::LPS <= 16) {
@@ -1431,9 +1440,9 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         }
         team_sync<SF>();
 
-        if constexpr (!EARLY) {
-            // next tile's unit, context and IQ (in flight during the FFT)
-            next_unit();
+        if (!early) {
+            // next tile's context and IQ (in flight during the FFT)
+            next_ctx();
             if (t + 1 < ntiles) {
                 const cf32* lsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base + fl;
 #pragma unroll
