@@ -474,7 +474,11 @@ __device__ __forceinline__ SymCtx sym_ctx(const DemodArgs& A, unsigned f, unsign
     SymCtx c;
     c.f = f;
     c.s = s;
-    c.ok = live && m.status == 0;
+    // kStatusRecheck only marks that some symbol of the frame left a
+    // sentinel for k_post (another team or workgroup may set it while this
+    // symbol's record is read): its estimate stands, and k_post recomputes
+    // the sentinels only, so every other symbol must still be demodulated
+    c.ok = live && (m.status == 0 || m.status == kStatusRecheck);
     c.live = live;
     c.have_sync = m.have_sync != 0;
     // LoRaDemod.cpp:144-151 / phy.cpp:208-216, in 32 bits
