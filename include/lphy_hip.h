@@ -94,11 +94,16 @@ enum lphy_flags {
                                     56..70 whole symbols per frame), the
                                     single-read kernel that keeps each frame
                                     on the CU (same results; experimental) */
-    LPHY_F_SCAN_FIRST = 256u     /* fused launch, modes 1/2: scan each whole
+    LPHY_F_SCAN_FIRST = 256u,    /* fused launch, modes 1/2: scan each whole
                                     frame's max-abs before its estimate (a
                                     second read of the frame) instead of the
                                     speculative normalisation checked at the
                                     frame's end (same results; comparison) */
+    LPHY_F_DEBUG_RECHECK = 512u  /* testing: separate launches mark every
+                                    estimated frame "has open symbols"
+                                    before the symbol kernel runs, so the
+                                    path a concurrent re-check takes is
+                                    exercised on every frame (same results) */
 };
 
 enum lphy_window { LPHY_WINDOW_NONE = 0, LPHY_WINDOW_HANN = 1 };
@@ -120,9 +125,16 @@ size_t lphy_hip_syms_per_frame(const lphy_hip_ctx* ctx, size_t frame_samples,
  * `stream`).  d_bytes may be NULL unless LPHY_F_DECODE.  d_meta is
  * required.  Returns 0 or -EINVAL/-ERANGE for shape errors (the per-frame
  * conditions the reference reports through its return value are in
- * lphy_frame_meta.status).  At SF 11-12 in modes 1/2 a call keeps per-frame
- * state in the context until its kernels finish: calls on one context run
- * in stream order (one stream, or the caller orders them). */
+ * lphy_frame_meta.status).
+ * Limits: frames * (frame_samples / (N*osr)) < 2^32 symbols per call and
+ * frame_samples < 2^31 (32-bit symbol bookkeeping in the kernels): larger
+ * batches give -ERANGE; split them across calls.
+ * Memory: the context holds only constant tables.  Per-call device scratch
+ * (SF 11-12 speculation records, 16 B per frame) is taken from the
+ * stream-ordered pool on `stream` and released in stream order, so calls on
+ * different streams of one context never share it.  Unlike the reference
+ * (API_SPEC.md:11-12, no allocation after init) a call may therefore
+ * allocate; see INTEGRATION.md. */
 int lphy_hip_demod_batch(lphy_hip_ctx* ctx, const float* d_iq, size_t frames,
                          size_t frame_samples, uint16_t* d_syms,
                          uint8_t* d_bytes, lphy_frame_meta* d_meta, int mode,
@@ -276,7 +288,8 @@ int lphy_hip_lora_encode_batch(const uint8_t* d_bytes, size_t frames, size_t str
  * LoRaWAN MAC helpers batched: lorawan::compute_mic
  * (lorawan.cpp:35-98, AES-128 CMAC over B0 || data) and parse_frame's
  * checks (lorawan.cpp:150-176) on the decoded bytes of many frames at once.
- * Keys are 16-byte records in device memory (d_keys, 4-byte aligned).
+ * Keys are 16-byte records in device memory (d_keys, 16-byte aligned;
+ * -EINVAL otherwise).
  * --------------------------------------------------------------------- */
 typedef struct lphy_lorawan_desc { /* one MIC job */
     uint64_t offset;   /* byte offset of the frame's MHDR..FRMPayload in d_bytes */
@@ -319,7 +332,9 @@ int lphy_hip_lorawan_mic_batch(uint8_t* d_bytes, const lphy_lorawan_desc* d_desc
 /* parse_frame's checks on `frames` rows of decoded bytes `stride` apart
  * (e.g. demod_batch's d_bytes): row i holds d_lens[i] bytes (d_lens NULL:
  * `len` each) and uses key d_key_index[i] (NULL: key 0).  Results in
- * d_out[i].  Lengths up to 65535 bytes. */
+ * d_out[i].  Lengths up to 65535 bytes and at most `stride`: a row whose
+ * d_lens[i] exceeds either gets status -ERANGE and nothing of it is read
+ * (a fixed `len` beyond them is -EINVAL for the whole call). */
 int lphy_hip_lorawan_parse_batch(const uint8_t* d_bytes, size_t frames, size_t stride,
                                  const uint32_t* d_lens, size_t len, const uint8_t* d_keys, size_t nkeys,
                                  const uint32_t* d_key_index, lphy_lorawan_frame* d_out, void* stream);

@@ -61,15 +61,10 @@ struct lphy_hip_ctx {
     void* d_stage = nullptr;
     unsigned long long* d_counters = nullptr;  // [0] rechecks, [1..4] phase clocks
     size_t stage_bytes = 0;
-    // per-frame speculation records of the SF 11-12 separate launches
-    // (DemodArgs::spec_big), grown on demand; batch calls on one context are
-    // ordered on its stream(s) by the caller, like its other device state
-    std::mutex spec_mu;
-    void* d_spec = nullptr;
-    size_t spec_bytes = 0;
-    // (the producer / compensation kernels take their scratch per call from
-    // the stream-ordered allocator, so concurrent calls on different streams
-    // or threads never share it)
+    // (per-call scratch - the SF 11-12 speculation records, the producer's
+    // phases, the compensation's shift buffer - comes from the stream-ordered
+    // allocator on the caller's stream, so concurrent calls on different
+    // streams or threads of one context never share it)
 };
 
 
@@ -176,19 +171,22 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 // Per-call device scratch.  On a caller's stream it is allocated and
 // released in that stream's order (hipMallocAsync / hipFreeAsync), so its
-// lifetime is exactly the call's kernels.  On the null stream the stream-
-// ordered pool is not used (a transcript run once read a recycled block
-// there): a plain hipMalloc, and the release waits for the stream.  The
+// lifetime is exactly the call's kernels.  The producer and compensation
+// entry points do not use the stream-ordered pool on the null stream (a
+// transcript run once read a recycled block there): a plain
+// hipMalloc, and the release waits for the stream.  demod_batch pools on
+// every stream (`pool_null`), so its device callers never synchronise.  The
 // *_host entry points lend a slice of their staging buffer instead (they
 // hold c->mu and synchronise before returning).
 struct StreamScratch {
     void* p = nullptr;
     hipStream_t st;
-    bool owned = false, pooled = false;
-    explicit StreamScratch(hipStream_t s, void* lent = nullptr) : p(lent), st(s) {}
+    bool owned = false, pooled = false, pool_null = false;
+    explicit StreamScratch(hipStream_t s, void* lent = nullptr, bool pool_on_null = false)
+        : p(lent), st(s), pool_null(pool_on_null) {}
     int get(size_t bytes) {
         if (p) return 0;  // lent by the caller
-        pooled = st != nullptr;
+        pooled = st != nullptr || pool_null;
         const hipError_t e = pooled ? hipMallocAsync(&p, bytes, st) : hipMalloc(&p, bytes);
         if (e != hipSuccess) {
             p = nullptr;
@@ -272,7 +270,6 @@ void lphy_hip_ctx_destroy(lphy_hip_ctx* c) {
     if (c->d_win) (void)hipFree(c->d_win);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->d_counters) (void)hipFree(c->d_counters);
-    if (c->d_spec) (void)hipFree(c->d_spec);
     delete c;
 }
 
@@ -283,9 +280,25 @@ size_t lphy_hip_syms_per_frame(const lphy_hip_ctx* c, size_t frame_samples, int 
     return total >= 2 ? total - 2 : total;
 }
 
+namespace {
+int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t frame_samples,
+                     uint16_t* d_syms, uint8_t* d_bytes, lphy_frame_meta* d_meta, int mode,
+                     unsigned flags, hipStream_t st, void* lent_spec);
+}
+
 int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
                          size_t frame_samples, uint16_t* d_syms, uint8_t* d_bytes,
                          lphy_frame_meta* d_meta, int mode, unsigned flags, void* stream) {
+    return demod_batch_impl(c, d_iq, frames, frame_samples, d_syms, d_bytes, d_meta, mode, flags,
+                            (hipStream_t)stream, nullptr);
+}
+
+namespace {
+// lent_spec: frames * 16 bytes of speculation records the caller owns
+// (the *_host entry point's staging), else per-call pooled scratch.
+int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t frame_samples,
+                     uint16_t* d_syms, uint8_t* d_bytes, lphy_frame_meta* d_meta, int mode,
+                     unsigned flags, hipStream_t st, void* lent_spec) {
     if (!c || !d_iq || !d_meta || !d_syms) return -EINVAL;
     if (mode < 0 || mode > 2) return -EINVAL;
     if ((flags & LPHY_F_DECODE) && !d_bytes) return -EINVAL;
@@ -299,7 +312,6 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     }
     if (mode == LPHY_MODE_DECHIRP_LORA_DEMODULATE && (c->osr != 1 || frame_samples % c->N)) return -EINVAL;
     HIP_OK(hipSetDevice(c->device));
-    hipStream_t st = (hipStream_t)stream;
     DemodArgs A{};
     A.iq = reinterpret_cast<const cf32*>(d_iq);
     A.tw = c->d_tw;
@@ -319,6 +331,7 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     A.counters = c->d_counters;
     A.resident = (flags & LPHY_F_RESIDENT) ? 1 : 0;
     A.spec = (mode != LPHY_MODE_DEMODULATE && !A.no_scratch && !(flags & LPHY_F_SCAN_FIRST)) ? 1 : 0;
+    A.debug_recheck = (flags & LPHY_F_DEBUG_RECHECK) ? 1 : 0;
     const size_t est_syms = mode == LPHY_MODE_DEMODULATE ? 2 : (total < 2 ? total : 2);
     A.est_units = (int)(est_syms * c->osr);
     // 32-bit symbol / sample bookkeeping in the kernels
@@ -340,21 +353,13 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     // of k_frames across workgroups (k_maxabs scans the two estimate
     // symbols, k_demod folds the rest, k_post closes each frame); needs the
     // prologue, the symbols and the fix-up in this one call
+    // (per call, in the caller's stream order: released after this call's
+    // last kernel, k_post, which is launched below while `spec` is in scope)
+    StreamScratch spec(st, lent_spec, true);
     if (!fused && A.spec && c->sf >= 11 && c->osr == 1 && !A.exact_rotation && total >= 2 &&
         (all || (stages & both) == both)) {
-        std::lock_guard<std::mutex> lk(c->spec_mu);
-        const size_t need = frames * sizeof(uint4);
-        if (c->spec_bytes < need) {
-            if (c->d_spec) {
-                HIP_OK(hipDeviceSynchronize());  // a previous call may still use it
-                (void)hipFree(c->d_spec);
-            }
-            c->d_spec = nullptr;
-            c->spec_bytes = 0;
-            HIP_OK(hipMalloc(&c->d_spec, need));
-            c->spec_bytes = need;
-        }
-        A.spec_big = static_cast<uint4*>(c->d_spec);
+        if (int rc = spec.get(frames * sizeof(uint4))) return rc;
+        A.spec_big = static_cast<uint4*>(spec.p);
     }
     int rc = fused ? launch_frames(c->sf, A, st)
                    : launch_demod(c->sf, A, st, all || (stages & LPHY_F_STAGE_PROLOGUE),
@@ -377,6 +382,7 @@ int lphy_hip_demod_batch(lphy_hip_ctx* c, const float* d_iq, size_t frames,
     F.set_sync = 1;
     return launch_post(c->sf, mode, A, F, fix, fin, st);
 }
+}  // namespace
 
 #ifdef LPHY_PROFILE_PHASES
 // experiments only: read and clear k_demod's per-phase clock sums
@@ -537,7 +543,8 @@ int lphy_hip_demod_host(lphy_hip_ctx* c, const float* h_iq, size_t frames,
     const size_t sym_b = align_up(std::max<size_t>(1, frames * per) * sizeof(uint16_t));
     const size_t byte_b = align_up(std::max<size_t>(1, frames * (per / 2)));
     const size_t meta_b = align_up(frames * sizeof(lphy_frame_meta));
-    int rc = ensure_stage(c, iq_b + sym_b + byte_b + meta_b);
+    const size_t spec_b = align_up(frames * sizeof(uint4));
+    int rc = ensure_stage(c, iq_b + sym_b + byte_b + meta_b + spec_b);
     if (rc) return rc;
     char* base = (char*)c->d_stage;
     float* d_iq = (float*)base;
@@ -546,9 +553,9 @@ int lphy_hip_demod_host(lphy_hip_ctx* c, const float* h_iq, size_t frames,
     lphy_frame_meta* d_meta = (lphy_frame_meta*)(base + iq_b + sym_b + byte_b);
     HIP_OK(hipMemcpy(d_iq, h_iq, frames * frame_samples * sizeof(cf32), hipMemcpyHostToDevice));
     HIP_OK(hipMemset(d_meta, 0, frames * sizeof(lphy_frame_meta)));
-    rc = lphy_hip_demod_batch(c, d_iq, frames, frame_samples, d_syms,
-                              (flags & LPHY_F_DECODE) ? d_bytes : nullptr, d_meta, mode, flags,
-                              nullptr);
+    rc = demod_batch_impl(c, d_iq, frames, frame_samples, d_syms,
+                          (flags & LPHY_F_DECODE) ? d_bytes : nullptr, d_meta, mode, flags, nullptr,
+                          base + iq_b + sym_b + byte_b + meta_b);
     if (rc) return rc;
     HIP_OK(hipDeviceSynchronize());
     HIP_OK(hipMemcpy(h_meta, d_meta, frames * sizeof(lphy_frame_meta), hipMemcpyDeviceToHost));

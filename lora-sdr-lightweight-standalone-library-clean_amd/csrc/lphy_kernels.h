@@ -75,6 +75,7 @@ struct DemodArgs {
     // max-abs of the symbol windows, least certificate ratio (float bits,
     // atomic max / min), flags (1 NaN, 2 symbol left open)}; nullptr = off
     uint4* spec_big;
+    int debug_recheck;       // LPHY_F_DEBUG_RECHECK: mark estimated frames kStatusRecheck before k_demod
     // persistent demod workers: symbol stride per step split into whole
     // frames + symbols (host-computed, so the kernel never divides)
     unsigned stride_f, stride_s;
@@ -450,6 +451,15 @@ __global__ __launch_bounds__(kTile) void k_estimate(DemodArgs A) {
         fold.finish(m, U / A.osr, N, A.osr);
         A.meta[fbase + tid] = m;
     }
+}
+
+// LPHY_F_DEBUG_RECHECK (tests): every frame the prologue estimated (status
+// 0) is marked as if another workgroup had already left a sentinel in it, the
+// state a symbol of the separate launches may observe at any time
+// (sym_ctx); k_post's recheck then finds no sentinel and clears the mark.
+__global__ void k_mark_recheck(lphy_frame_meta* meta, unsigned long long frames) {
+    const unsigned long long f = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < frames && meta[f].status == 0) meta[f].status = kStatusRecheck;
 }
 
 // ---------------------------------------------------------------------------
@@ -2421,6 +2431,9 @@ int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symb
         const unsigned long long blocks = (A.frames + fpt - 1) / fpt;
         hipLaunchKernelGGL(k_estimate<SF>, dim3((unsigned)blocks), dim3(kTile), 0, st, A);
     }
+    if (A.debug_recheck && symbols)
+        hipLaunchKernelGGL(k_mark_recheck, dim3((unsigned)((A.frames + kTile - 1) / kTile)), dim3(kTile), 0, st,
+                           A.meta, A.frames);
     if (symbols) {
         const unsigned long long nsym = A.frames * A.total_syms;
         const unsigned long long tiles = (nsym + G::T - 1) / G::T;

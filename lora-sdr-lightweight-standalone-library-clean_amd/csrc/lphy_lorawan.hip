@@ -249,7 +249,9 @@ __global__ void __launch_bounds__(kThreads) k_lw_parse(const uint8_t* bytes, uns
         const uint8_t* row = bytes + f * stride;
         uint32_t rec[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         const uint32_t kidx = key_index ? key_index[f] : 0u;
-        if (len < 12) {
+        // a row length past the row (or past the 16-bit record fields) would
+        // read beyond the row: -ERANGE, nothing read
+        if (len < 12 || len > stride || len > 65535u) {
             rec[0] = (uint32_t)-ERANGE;
         } else if (kidx >= nkeys) {
             rec[0] = (uint32_t)-ENOKEY;

@@ -23,14 +23,24 @@ uint32_t le32(const uint8_t* p) {
     return uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
 }
 
+// The MIC through the GPU CMAC, or the device error (-ENODEV, -EIO, ...):
+// build_frame / parse_frame return that error rather than a frame built or
+// accepted against a MIC of 0.
+int gpu_mic(const uint8_t nwk_skey[16], bool uplink, uint32_t devaddr, uint32_t fcnt, const uint8_t* data,
+            size_t len, uint32_t* mic) {
+    *mic = 0;
+    return lphy_hip_lorawan_mic_host(device_index(), nwk_skey, uplink ? 1 : 0, devaddr, fcnt, data, len, mic);
+}
+
 }  // namespace
 
+// compute_mic has no error channel in the reference's signature: a device
+// failure is reported on stderr and yields MIC 0 (the frame helpers below do
+// not rely on it).
 uint32_t compute_mic(const uint8_t nwk_skey[16], bool uplink, uint32_t devaddr, uint32_t fcnt,
                      const uint8_t* data, size_t len) {  // lorawan.cpp:35-98
     uint32_t mic = 0;
-    const int rc = lphy_hip_lorawan_mic_host(device_index(), nwk_skey, uplink ? 1 : 0, devaddr, fcnt, data,
-                                             len, &mic);
-    if (rc) {
+    if (const int rc = gpu_mic(nwk_skey, uplink, devaddr, fcnt, data, len, &mic)) {
         std::fprintf(stderr, "lorawan::compute_mic: GPU MIC failed (%d)\n", rc);
         return 0;
     }
@@ -53,7 +63,9 @@ ssize_t build_frame(lora_phy::lora_workspace* ws, const uint8_t nwk_skey[16], co
     for (uint8_t b : frame.payload) *p++ = b;
     const size_t n = static_cast<size_t>(p - tmp_bytes);
     const bool uplink = (static_cast<uint8_t>(frame.mhdr.mtype) & 1) == 0;
-    const uint32_t mic = compute_mic(nwk_skey, uplink, frame.fhdr.devaddr, frame.fhdr.fcnt, tmp_bytes, n);
+    uint32_t mic = 0;
+    if (const int rc = gpu_mic(nwk_skey, uplink, frame.fhdr.devaddr, frame.fhdr.fcnt, tmp_bytes, n, &mic))
+        return rc;
     for (int i = 0; i < 4; ++i) *p++ = static_cast<uint8_t>(mic >> (8 * i));
     return lora_phy::encode(ws, tmp_bytes, n + 4, symbols, symbol_cap);
 }
@@ -70,8 +82,10 @@ ssize_t parse_frame(lora_phy::lora_workspace* ws, const uint8_t nwk_skey[16], co
     const uint32_t devaddr = le32(tmp_bytes + 1);
     const uint16_t fcnt = static_cast<uint16_t>(tmp_bytes[6] | tmp_bytes[7] << 8);
     const uint32_t carried = le32(tmp_bytes + len - 4);
-    if (carried != compute_mic(nwk_skey, ((mhdr >> 5) & 1) == 0, devaddr, fcnt, tmp_bytes, len - 4))
-        return -EINVAL;
+    uint32_t calc = 0;
+    if (const int rc = gpu_mic(nwk_skey, ((mhdr >> 5) & 1) == 0, devaddr, fcnt, tmp_bytes, len - 4, &calc))
+        return rc;
+    if (carried != calc) return -EINVAL;
     // fields land in `out` in the reference's order, so an FOpts overrun
     // leaves the same partial update (:163-172)
     out.mhdr.mtype = static_cast<MType>(mhdr >> 5);

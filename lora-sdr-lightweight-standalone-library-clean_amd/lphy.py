@@ -32,6 +32,7 @@ F_UNFUSED = 32  # separate prologue / symbol launches (lphy_hip.h)
 F_EXACT_ROTATION = 64  # fused launch without the certified per-frame rotation table
 F_RESIDENT = 128  # fused launch: single-read CU-resident kernel where it applies (SF 7)
 F_SCAN_FIRST = 256  # fused launch, modes 1/2: whole-frame max-abs pre-scan (no speculation)
+F_DEBUG_RECHECK = 512  # separate launches: every estimated frame marked "open symbols" first (tests)
 WINDOW_NONE = 0
 WINDOW_HANN = 1
 

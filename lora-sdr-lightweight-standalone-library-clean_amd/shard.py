@@ -81,3 +81,35 @@ def gather_varlen(local: torch.Tensor, group=None) -> list[torch.Tensor]:
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf, group=group)
     return [p[:k] for p, k in zip(parts, sizes)]
+
+
+def mixed_plan(total: int, world: int, rank: int, seed: int = 0xC3, payload: int = 32,
+               sf_lo: int = 7, sf_hi: int = 12):
+    """The mixed-SF stream of BASELINE.json's C3 config, as every rank sees
+    it: `total` frames with SF drawn uniformly from [sf_lo, sf_hi] (seeded),
+    random payloads, the contiguous range of this rank cut by equal cost
+    sum(66 N log2 N), and its frames bucketed by SF.  Returns
+    (first, count, sfs of the range, payloads of the range, {sf: indices of
+    the bucket's frames within the range, in order})."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    sfs = rng.integers(sf_lo, sf_hi + 1, total)
+    cost = (1 << sfs) * sfs.astype(np.float64)
+    first, count = balanced_ranges(cost, world)[rank]
+    pays = np.random.default_rng(seed + 1).integers(0, 256, (total, payload), dtype=np.uint8)
+    mine = sfs[first:first + count]
+    buckets = {int(sf): np.nonzero(mine == sf)[0] for sf in range(sf_lo, sf_hi + 1)}
+    return first, count, mine, pays[first:first + count], {k: v for k, v in buckets.items() if v.size}
+
+
+def reassemble(buckets: dict, parts: dict, count: int, payload: int = 32):
+    """Inverse of the SF bucketing: `parts[sf]` holds the decoded payloads
+    of bucket sf (frames in bucket order, `payload` bytes each, numpy or
+    torch); returns the range's payloads in frame order (numpy)."""
+    import numpy as np
+    out = np.zeros((count, payload), np.uint8)
+    for sf, idx in buckets.items():
+        p = parts[sf]
+        p = p.cpu().numpy() if hasattr(p, "cpu") else np.asarray(p)
+        out[idx] = p.reshape(-1, payload)[: idx.size]
+    return out

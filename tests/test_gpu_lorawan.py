@@ -151,6 +151,24 @@ def test_gpu_parse_uniform_rows(oracle, lphy, dev):
     assert list(recs["status"][[1, 3]]) == [-126, -126]
 
 
+def test_gpu_parse_row_length_bounds(oracle, lphy, dev):
+    """A per-row length past the row (`stride`) or past 65535 is -ERANGE for
+    that row alone, with nothing of the row read; the other rows parse."""
+    torch, d = dev
+    rng = np.random.default_rng(14)
+    key = rng.integers(0, 256, 16, dtype=np.uint8)
+    L = 40
+    body = bytearray(rng.integers(0, 256, L - 4, dtype=np.uint8).tobytes())
+    body[5] &= 0xF0
+    mic = oracle.lorawan_mic(key, ((body[0] >> 5) & 1) == 0, int.from_bytes(body[1:5], "little"),
+                             int.from_bytes(body[6:8], "little"), bytes(body))
+    row = bytes(body) + mic.to_bytes(4, "little")
+    lens = [L, L + 1, 70000, 0x7FFFFFFF, L]
+    recs = _parse_rows(lphy, torch, d, [row] * len(lens), L, [key], lens=lens)
+    assert list(recs["status"]) == [L - 12, -34, -34, -34, L - 12]
+    assert (recs["mic"][1:4] == 0).all() and (recs["devaddr"][1:4] == 0).all()
+
+
 def test_gpu_uplink_chain(oracle, lphy, dev):
     """MIC append -> lora_encode -> modulate -> demodulate+decode -> parse,
     all on the device (SF7, 64-symbol frames, 32-byte LoRaWAN frames)."""
