@@ -63,7 +63,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-mode-a", action="store_true")
-    ap.add_argument("--sweep", action="store_true", help="also time SF8..SF12 (extra field)")
+    ap.add_argument("--sweep", action="store_true", help="also time SF8..SF12 BW125 (extra field)")
+    ap.add_argument("--csv", default="", help="write the perf CSV (reference schema + hbm_gbps, "
+                                             "roofline_frac) for the reference's profiles and SF9-12 BW125")
+    ap.add_argument("--run-id", default=os.environ.get("RUN_ID", "run"))
     ap.add_argument("--config", default="c1", choices=["c1", "c2", "c3", "c4"],
                     help="BASELINE.json config: c1 SF7 x 65,536 (headline, default), c2 SF12 x "
                          "4,096, c3 mixed SF7-12 (1M frames over the ranks), c4 SF9 AWGN BER")
@@ -215,27 +218,104 @@ def timed(wl: Workload, mode: int, steps: int, warmup: int, world: int, events: 
     return dt
 
 
-def cpu_baseline(wl: Workload, seconds: float) -> dict:
-    """Reference CPU path (mode B: dechirp + lora_demodulate + lora_decode)
-    on this host, one workspace per thread, on a bounded sample."""
+def usable_cpus() -> dict:
+    """Host CPUs as the process sees them: os.cpu_count() (the machine),
+    the affinity mask, and the cgroup CPU quota when one is set (a GPU box
+    gives each job a share of a larger host)."""
+    out = {"host_cpus": os.cpu_count() or 1}
+    try:
+        out["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        out["affinity_cpus"] = out["host_cpus"]
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    out["cgroup_cpu_quota"] = quota
+    return out
+
+
+def cpu_baseline(wl: Workload, seconds: float, runs: int = 5) -> dict:
+    """The reference CPU path on this host:
+    nproc threads, one workspace per thread, on a bounded sample of the same
+    resident frames; each of `runs` runs repeats the sample until
+    seconds / (2 runs) have passed, and the median rate is reported for
+    mode B (dechirp + lora_demodulate + lora_decode, the bench's path) and
+    mode A (demodulate + decode, phy.cpp)."""
     import checkers
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = os.cpu_count() or 1
     if checkers.reference_available():
         ck, kind = checkers.Reference(), "reference"
     else:
         ck, kind = checkers.Oracle(), "port"
-    nf = min(wl.frames, 2048)
+    nf = min(wl.frames, max(2048, 8 * threads))
     x = wl.iq[: nf * wl.fs * 2].cpu().numpy().view(np.complex64)
-    done, el = 0, 0.0
-    while el < seconds:
-        t, out = ck.bench(1, wl.sf, x, nf, wl.fs, threads, wl.bw)
-        el += t
-        done += nf
-    ok = bool((out.reshape(nf, PAYLOAD) == wl.payloads[:nf]).all())
-    return {"value": done * DATA_SYMS / el, "unit": "data symbols/s", "cores": threads,
-            "kind": kind,
-            "sample": f"{done} SF{wl.sf} BW{wl.bw // 1000} frames ({nf}-frame batches, "
-                      f"{el:.1f} s), dechirp+lora_demodulate+lora_decode, payloads ok={ok}"}
+    per_run = seconds / (2 * runs)
+    res = {}
+    for name, mode in (("mode_B", 1), ("mode_A", 0)):
+        rates, out, total = [], None, 0
+        for _ in range(runs):
+            done, el = 0, 0.0
+            while el < per_run or done == 0:
+                t, out = ck.bench(mode, wl.sf, x, nf, wl.fs, threads, wl.bw)
+                el += t
+                done += nf
+            rates.append(done * DATA_SYMS / el)
+            total += done
+        ok = bool((out.reshape(nf, PAYLOAD) == wl.payloads[:nf]).all())
+        res[name] = {"value": float(np.median(rates)), "runs": [float(r) for r in rates],
+                     "frames": total, "payloads_ok": ok}
+    b = res["mode_B"]
+    return {"value": b["value"], "unit": "data symbols/s", "cores": threads, "kind": kind,
+            "runs": len(b["runs"]), "modes": res, "cpus": usable_cpus(),
+            "sample": f"SF{wl.sf} BW{wl.bw // 1000}: {nf}-frame batches of the bench's resident frames, "
+                      f"{threads} threads (os.cpu_count()), median of {runs} runs of ~{per_run:.1f} s per "
+                      "mode; value = mode B (dechirp+lora_demodulate+lora_decode, payloads ok="
+                      f"{b['payloads_ok']}); mode A = demodulate+decode (phy.cpp, does not round-trip, "
+                      "SURVEY §0.3)"}
+
+
+# tests/profiles.yaml of the reference (name, sf, bw): the rows of its
+# performance CSV (performance_test.cpp:69-75)
+REF_PROFILES = [("sf7_bw125_cr45", 7, 125000), ("sf7_bw125_cr47", 7, 125000), ("sf8_bw125_cr45", 8, 125000),
+                ("sf9_bw250_cr48", 9, 250000), ("sf10_bw250_cr47", 10, 250000),
+                ("sf11_bw500_cr45", 11, 500000), ("sf12_bw500_cr45", 12, 500000)]
+CLOCK_HZ = 2.4e9  # MI355X max engine clock (MI355X_MICROARCH.md), for cycles_per_symbol
+
+
+def profile_row(wl: Workload, ms_step: float, steps: int) -> dict:
+    """One configuration's whole-step figures: frames (packets) per second,
+    device clock cycles per data symbol at the 2.4 GHz engine clock (the
+    whole chip's wall time per symbol, the analog of the reference's rdtsc
+    cycles per symbol), the step's algorithmic HBM GB/s (SURVEY §8d bytes
+    per data symbol) and its fraction of the 8 TB/s roofline; payloads
+    recovered as the correctness check."""
+    syms = wl.frames * DATA_SYMS
+    gbps = syms * bytes_per_data_symbol(wl.N) / (ms_step * 1e-3) / 1e9
+    chk = wl.check(lphy.MODE_DECHIRP_LORA_DEMODULATE)
+    return {"sf": wl.sf, "N": wl.N, "bw_hz": wl.bw, "frames": wl.frames, "steps": steps,
+            "ms_per_step": ms_step, "symbols_per_s": syms / (ms_step * 1e-3),
+            "pps": wl.frames / (ms_step * 1e-3),
+            "cycles_per_symbol": ms_step * 1e-3 * CLOCK_HZ / syms,
+            "hbm_gbps": gbps, "roofline_frac": gbps / HBM_PEAK_GBPS,
+            "payloads_recovered": chk["payloads_recovered"]}
+
+
+def write_perf_csv(path: str, run_id: str, rows: list) -> None:
+    """The reference's performance CSV (run_id,profile,sf,N,pps,
+    cycles_per_symbol; performance_test.cpp:69-75,144-148) plus hbm_gbps
+    and roofline_frac; tools/compare_perf.py gates on it."""
+    import csv
+    Path(path).parent.mkdir(parents=True, exist_ok=True)
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["run_id", "profile", "sf", "N", "pps", "cycles_per_symbol", "hbm_gbps", "roofline_frac"])
+        for r in rows:
+            w.writerow([run_id, r["profile"], r["sf"], r["N"], f"{r['pps']:.6g}", f"{r['cycles_per_symbol']:.6g}",
+                        f"{r['hbm_gbps']:.6g}", f"{r['roofline_frac']:.6g}"])
 
 
 def frames_fused(sf: int) -> bool:
@@ -287,18 +367,9 @@ def run_c3(args, baseline, world, rank, dev) -> dict:
     ranges (sum of 66 N log2 N), bucketed by SF on each rank
     (one resident batch and one launch per SF); payloads gathered."""
     total = args.total_frames or (1 << 17) * world  # weak scaling: 1 M frames at 8 ranks
-    rng = np.random.default_rng(0xC3)
-    sfs = rng.integers(7, 13, total)
-    cost = (1 << sfs) * sfs.astype(np.float64)
-    first, count = shard.balanced_ranges(cost, world)[rank]
-    mine = sfs[first:first + count]
-    pay_rng = np.random.default_rng(0xC3 + 1)
-    payloads = pay_rng.integers(0, 256, (total, PAYLOAD), dtype=np.uint8)[first:first + count]
-    buckets = []
-    for sf in range(7, 13):
-        idx = np.nonzero(mine == sf)[0]
-        if idx.size:
-            buckets.append(Workload(sf, args.bw, int(idx.size), rank, dev, payloads=payloads[idx]))
+    first, count, mine, payloads, plan = shard.mixed_plan(total, world, rank, payload=PAYLOAD)
+    buckets = [Workload(sf, args.bw, int(idx.size), rank, dev, payloads=payloads[idx])
+               for sf, idx in sorted(plan.items())]
     mode_b = lphy.MODE_DECHIRP_LORA_DEMODULATE
 
     def step():
@@ -313,6 +384,9 @@ def run_c3(args, baseline, world, rank, dev) -> dict:
     if world > 1:
         torch.distributed.all_reduce(syms)
     ok = sum(w.check(mode_b)["payloads_recovered"] for w in buckets)
+    # the buckets' payloads put back in frame order = this rank's stream
+    ordered = shard.reassemble(plan, {w.sf: w.pay for w in buckets}, count, PAYLOAD)
+    in_order = bool(np.array_equal(ordered, payloads))
     per_sf = {f"SF{w.sf}": w.frames for w in buckets}
     iq_gb = sum(w.frames * w.fs * 8 for w in buckets) / 1e9
     return {"metric": baseline["metric"], "value": float(syms.item()) * steps / dt,
@@ -324,7 +398,7 @@ def run_c3(args, baseline, world, rank, dev) -> dict:
                                    "cost-balanced shards, one launch per SF bucket",
                        "frames_this_rank": int(count), "frames_per_sf_rank0": per_sf,
                        "iq_gb_rank0": iq_gb, "parallelism": f"frames sharded x{world}"},
-            "check": {"payloads_recovered": ok, "frames": int(count)}}
+            "check": {"payloads_recovered": ok, "frames": int(count), "reassembled_in_order": in_order}}
 
 
 def run_c4(args, baseline, world, rank, dev) -> dict:
@@ -422,20 +496,22 @@ def main():
             "value": data_syms * max(3, args.steps // 2) / dta, "unit": "data symbols/s",
             "check": wl.check(lphy.MODE_DEMODULATE)}
         wl.run(mode_b)  # leave mode-B results in place
-    if args.sweep:
-        sweep = {}
-        for sf in range(8, 13):
-            w2 = Workload(sf, args.bw, DEFAULT_FRAMES[sf] // 4, rank, dev)
-            d2 = timed(w2, mode_b, 3, 1, 1)
-            k2 = w2._event_ms(mode_b, lphy.F_DECODE | lphy.F_STAGE_PROLOGUE | lphy.F_STAGE_SYMBOLS, 2)
-            sweep[f"SF{sf}"] = {"value": w2.frames * DATA_SYMS * 3 / d2,
-                                "frames": w2.frames,
-                                "kernel_frac_hbm": w2.frames * (w2.fs * 8 + DATA_SYMS * 2 + 32)
-                                / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBPS,
-                                "check": w2.check(mode_b)["payloads_recovered"]}
+    if (args.sweep or args.csv) and world == 1:
+        rows = []
+        profiles = [(f"sf{sf}_bw125", sf, 125000) for sf in range(8, 13)]
+        if args.csv:
+            profiles = REF_PROFILES + [p for p in profiles if p[1] >= 9]
+        head = {"profile": f"sf{args.sf}_bw{args.bw // 1000}", **profile_row(wl, ms, args.steps)}
+        for name, sf, bw in profiles:
+            w2 = Workload(sf, bw, DEFAULT_FRAMES[sf], rank, dev)
+            k = max(5, args.steps // 10)
+            d2 = timed(w2, mode_b, k, 2, 1, settle_s=0.05)
+            rows.append({"profile": name, **profile_row(w2, d2 / k * 1e3, k)})
             del w2
             torch.cuda.empty_cache()
-        extra["sweep"] = sweep
+        extra["sweep"] = {r["profile"]: r for r in [head] + rows}
+        if args.csv:
+            write_perf_csv(args.csv, args.run_id, [head] + rows)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
