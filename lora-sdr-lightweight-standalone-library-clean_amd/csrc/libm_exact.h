@@ -109,7 +109,9 @@ LPHY_HD void sincos_poly(double x, double x2, const SinCosCoef& p, int n,
 
 // 2/pi as 24 overlapping 32-bit windows (Payne-Hanek table).
 LPHY_HD uint32_t inv_pio4(int i) {
-    const uint32_t t[24] = {
+    // static: one read-only table (constant memory on the device), not a
+    // per-call private array (scratch) that every inlined copy would fill
+    static constexpr uint32_t t[24] = {
         0xa2u,       0xa2f9u,     0xa2f983u,   0xa2f9836eu,
         0xf9836e4eu, 0x836e4e44u, 0x6e4e4415u, 0x4e441529u,
         0x441529fcu, 0x1529fc27u, 0x29fc2757u, 0xfc2757d1u,

@@ -59,7 +59,7 @@ struct lphy_hip_ctx {
     // staging for the host convenience entry points
     std::mutex mu;
     void* d_stage = nullptr;
-    unsigned long long* d_counters = nullptr;  // [0] rechecks, [1..4] phase clocks
+    unsigned long long* d_counters = nullptr;  // [0] rechecks, [1..8] phase clocks (experiments)
     size_t stage_bytes = 0;
     // (per-call scratch - the SF 11-12 speculation records, the producer's
     // phases, the compensation's shift buffer - comes from the stream-ordered
@@ -122,6 +122,16 @@ inline bool frames_fit(unsigned sf, unsigned osr, int est_units, size_t total) {
     const size_t lps = ((size_t)1 << sf) / E;
     const size_t wt = 64 / lps;
     return total + 1 >= 2 * wt;
+}
+
+// Whether the fused SF 11-12 kernel (k_wave) takes this batch: a symbol per
+// wavefront (pair at SF 11), the two-symbol estimate, no window, the
+// certified rotation, and in modes 1/2 the speculative normalisation (its
+// scan covers the two estimate symbols only).
+inline bool wave_fit(unsigned sf, unsigned osr, int window, int est_units, size_t total, int mode,
+                     const DemodArgs& A) {
+    return (sf == 11 || sf == 12) && osr == 1 && window == LPHY_WINDOW_NONE && est_units == 2 && total >= 2 &&
+           !A.exact_rotation && (mode == LPHY_MODE_DEMODULATE || A.spec);
 }
 
 const SfOps* sf_ops(unsigned sf) {
@@ -242,13 +252,13 @@ int lphy_hip_ctx_create(lphy_hip_ctx** out, int device, unsigned sf, unsigned bw
     make_downchirp(down, (int)c->N, (float)bw_hz / 125000.0f);
     if (hipMalloc(&c->d_tw, c->N * sizeof(cf32)) != hipSuccess ||
         hipMalloc(&c->d_down, c->N * sizeof(cf32)) != hipSuccess ||
-        hipMalloc(&c->d_counters, 5 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->d_counters, 9 * sizeof(unsigned long long)) != hipSuccess) {
         lphy_hip_ctx_destroy(c);
         return -ENOMEM;
     }
     HIP_OK(hipMemcpy(c->d_tw, tw.data(), c->N * sizeof(cf32), hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(c->d_down, down.data(), c->N * sizeof(cf32), hipMemcpyHostToDevice));
-    HIP_OK(hipMemset(c->d_counters, 0, 5 * sizeof(unsigned long long)));
+    HIP_OK(hipMemset(c->d_counters, 0, 9 * sizeof(unsigned long long)));
     if (window == LPHY_WINDOW_HANN) {
         std::vector<float> w;
         make_hann(w, (int)c->N);
@@ -346,9 +356,11 @@ int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t f
     // (Measured alternative: the separate kernels pipelined over chunks on
     // two streams, prologue of chunk c+1 beside the symbol kernel of chunk
     // c: the co-running kernels slowed each other ~2x, 1.1x slower overall.)
-    const bool fused = (all || (stages & both) == both) && !(flags & LPHY_F_UNFUSED) &&
-                       fused_enabled() && frames_fit(c->sf, c->osr, A.est_units, total);
-    A.sentinels = fused ? 1 : 0;  // k_cuframe marks open symbols in the output only
+    const bool fused = (all || (stages & both) == both) && !(flags & LPHY_F_UNFUSED) && fused_enabled() &&
+                       (frames_fit(c->sf, c->osr, A.est_units, total) ||
+                        wave_fit(c->sf, c->osr, c->window, A.est_units, total, mode, A));
+    A.wave = fused && c->sf >= 11 ? 1 : 0;
+    A.sentinels = fused && !A.wave ? 1 : 0;  // k_cuframe marks open symbols in the output only
     // SF 11-12 separate launches, modes 1/2: the speculative normalisation
     // of k_frames across workgroups (k_maxabs scans the two estimate
     // symbols, k_demod folds the rest, k_post closes each frame); needs the
@@ -385,13 +397,13 @@ int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t f
 }  // namespace
 
 #ifdef LPHY_PROFILE_PHASES
-// experiments only: read and clear k_demod's per-phase clock sums
-int lphy_hip_phase_cycles(lphy_hip_ctx* c, unsigned long long* out4) {
-    if (!c || !out4) return -EINVAL;
+// experiments only: read and clear the kernels' per-phase clock sums (8)
+int lphy_hip_phase_cycles(lphy_hip_ctx* c, unsigned long long* out8) {
+    if (!c || !out8) return -EINVAL;
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(out4, c->d_counters + 1, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemset(c->d_counters + 1, 0, 4 * sizeof(unsigned long long)));
+    HIP_OK(hipMemcpy(out8, c->d_counters + 1, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemset(c->d_counters + 1, 0, 8 * sizeof(unsigned long long)));
     return 0;
 }
 #endif

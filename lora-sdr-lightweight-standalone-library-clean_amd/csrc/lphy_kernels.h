@@ -76,6 +76,7 @@ struct DemodArgs {
     // atomic max / min), flags (1 NaN, 2 symbol left open)}; nullptr = off
     uint4* spec_big;
     int debug_recheck;       // LPHY_F_DEBUG_RECHECK: mark estimated frames kStatusRecheck before k_demod
+    int wave;                // the fused SF 11-12 launch (k_wave) ran: k_post's fix-up starts with k_wsettle
     // persistent demod workers: symbol stride per step split into whole
     // frames + symbols (host-computed, so the kernel never divides)
     unsigned stride_f, stride_s;
@@ -2171,6 +2172,7 @@ __global__ __launch_bounds__(kTile) void k_post(DemodArgs A, FinalArgs F, int fi
 }
 
 #include "lphy_cuframe.h"
+#include "lphy_wave.h"
 
 // ---------------------------------------------------------------------------
 // lora_modulate (LoRaMod.cpp:8-43 + ChirpGenerator.hpp:24-51), bit-exact.
@@ -2449,9 +2451,31 @@ int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symb
     return 0;
 }
 
+// Fused SF 11-12 path (lphy_wave.h): one 256-thread workgroup per CU (its
+// LDS), four independent waves each.
+template <int SF, int MODE>
+int launch_wave_mode(const DemodArgs& A, hipStream_t st) {
+    FrameArgs P{};
+    P.A = A;
+    unsigned long long blocks = (unsigned long long)cu_count();
+    const unsigned long long need = (A.frames + WGeo<SF>::WPB - 1) / WGeo<SF>::WPB;
+    if (blocks > need) blocks = need;
+    P.waves = (unsigned)(blocks * WGeo<SF>::WPB);
+    hipLaunchKernelGGL((k_wave<SF, MODE>), dim3((unsigned)blocks), dim3(256), 0, st, P);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
 template <int SF>
 int launch_frames_sf(const DemodArgs& A, hipStream_t st) {
     if constexpr (Geo<SF>::LPS > 64) {
+        if constexpr (SF == 11 || SF == 12) {
+            switch (A.mode) {
+                case LPHY_MODE_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_DEMODULATE>(A, st);
+                case LPHY_MODE_LORA_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_LORA_DEMODULATE>(A, st);
+                default: return launch_wave_mode<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>(A, st);
+            }
+        }
         (void)A; (void)st;
         return -ENOTSUP;
     } else {
@@ -2472,6 +2496,15 @@ int launch_frames_sf(const DemodArgs& A, hipStream_t st) {
 template <int SF>
 int launch_post_sf(int mode, const DemodArgs& A, const FinalArgs& F, bool fix, bool fin, hipStream_t st) {
     const dim3 grid((unsigned)((A.frames + kTile - 1) / kTile));
+    if constexpr (SF == 11 || SF == 12) {
+        if (fix && A.wave && A.spec && mode != LPHY_MODE_DEMODULATE) {
+            const dim3 wg((unsigned)((A.frames + WGeo<SF>::WPB - 1) / WGeo<SF>::WPB));
+            if (mode == LPHY_MODE_LORA_DEMODULATE)
+                hipLaunchKernelGGL((k_wsettle<SF, LPHY_MODE_LORA_DEMODULATE>), wg, dim3(256), 0, st, A);
+            else
+                hipLaunchKernelGGL((k_wsettle<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>), wg, dim3(256), 0, st, A);
+        }
+    }
     if (fix && A.spec_big) {
         if (mode == LPHY_MODE_LORA_DEMODULATE)
             hipLaunchKernelGGL((k_spec_settle<SF, LPHY_MODE_LORA_DEMODULATE>), dim3((unsigned)A.frames), dim3(kTile), 0,

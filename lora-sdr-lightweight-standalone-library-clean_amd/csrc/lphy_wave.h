@@ -1,0 +1,933 @@
+// lphy_wave.h — fused single launch for SF 11-12 (N = 2048 / 4096): one
+// wavefront per symbol (SF 12) or per symbol pair (SF 11), no workgroup
+// barrier in the loop.  Included by lphy_kernels.h inside its anonymous
+// namespace, after k_frames (it reuses SymCtx, EstFold, the certificate and
+// the speculative normalisation of the SF <= 10 path).
+//
+// The reference demodulates a frame in one pass at every SF
+// (/root/reference/src/phy/LoRaDemod.cpp:142-176, phy.cpp:204-238) with
+// KISS's recursive radix-4 DIT (kissfft.hh:106-185).  Here a lane holds 64
+// complex values of one symbol (LPS = N/64 lanes per symbol: 64 at SF 12,
+// 32 at SF 11 where a wave carries two symbols):
+//
+//   staging  the unit's IQ was copied HBM -> LDS by LDS-DMA during the
+//            previous unit (global_load_lds_dwordx4, 1 KiB per wave
+//            instruction, natural sample order); lane (h, l) reads samples
+//            i = l + LPS m of symbol h, m = 0..63, applies the [exact]
+//            dechirp and the rotation, keeps them in registers;
+//   pass 1   KISS stages 5, 4, 3 (the innermost) on the lane's registers:
+//            the inputs with equal i mod 64 form one sub-transform of
+//            length LPS (one group per lane at SF 12, two at SF 11);
+//   exchange the 64 x LPS transpose through the wave's own LDS buffer (the
+//            one the IQ landed in: XOR-swizzled rows, conflict-free b64
+//            writes and reads), then the next unit's LDS-DMA is issued into
+//            it;
+//   pass 2   KISS stages 2, 1, 0 on the lane's registers: lane l ends with
+//            the bins l + LPS B', B' = 0..63;
+//   argmax   lane-local top two and a cross-lane merge (the keyed bound of
+//            the certified path, or the detector's exact first maximum for
+//            the estimate units).
+//
+// Symbol units take the certified fast rotation: the frame's
+// rotation is a per-lane table of 8 entries times a wave-uniform one of 8,
+// and pass 2's last stage forms its per-lane twiddle tw[(l + LPS r) q] as
+// tw[l q] tw[LPS r q].  Both deviations are charged to the certificate
+// (kWaveExtra below); an uncertified symbol is left to k_post as in k_frames.
+// Estimate units run KISS's own arithmetic: every twiddle from the table,
+// unfused products, the detector's exact argmax, bit-identical bins.
+//
+// Per wave, frames w, w + W, ... (W waves); per frame one blocking two-symbol
+// max-abs scan (modes 1/2), the estimate units (2 at SF 12, one pair unit at
+// SF 11), then the symbol units.  The next frame's estimate units run two
+// symbol units before the current frame's end, so its time shift is known
+// when its first symbol unit's LDS-DMA is issued:
+//   E(0) | D(0)_0..D(0)_{p-1}, E(1), D(0)_p..D(0)_{ND-1} | D(1)_0 ...
+// with ND symbol units per frame and p = max(0, ND - 2).
+//
+// LDS: 4 waves x 32 KiB buffers + the down-chirp (32 KiB at SF 12): the
+// whole 160 KiB of a CU at SF 12, one 256-thread workgroup per CU.
+
+template <int SF>
+struct WGeo {
+    static constexpr int N = 1 << SF;
+    static constexpr int LPS = N / 64;    // lanes per symbol
+    static constexpr int SPW = 64 / LPS;  // symbols per unit (1 | 2)
+    static constexpr int NE = 2 / SPW;    // estimate units per frame
+    static constexpr int M3 = N / 256;    // KISS M(3): pass-1 stage 3 butterfly span
+    static constexpr int M4 = N / 1024;   // KISS M(4)
+    static constexpr int R5 = (SF & 1) ? 2 : 4;  // radix of the innermost stage
+    static constexpr int PPS = N / 128;   // LDS-DMA pieces (1 KiB) per symbol
+    static constexpr int BUF = SPW * N;   // complex per wave buffer
+    static constexpr int WPB = 4;         // waves per workgroup
+    // block of pass-1 group c = i mod 64 in KISS's output order: base-4
+    // reversal of its three digits (c = d0 + 4 d1 + 16 d2 -> 16 d0 + 4 d1 + d2)
+    __host__ __device__ static constexpr int rev3(int c) {
+        return ((c & 3) << 4) | (((c >> 2) & 3) << 2) | ((c >> 4) & 3);
+    }
+    // in-group index m (i = c + 64 m) of pass-1 position p: m = d3 + 4 d4 + 16 d5,
+    // p = d3 M3 + d4 M4 + d5
+    __host__ __device__ static constexpr int minv(int p) {
+        return p / M3 + 4 * ((p % M3) / M4) + 16 * (p % M4);
+    }
+    // register of pass-1 group g, position p (element m'' = SPW m + g holds
+    // sample i = l + LPS m'')
+    __host__ __device__ static constexpr int reg1(int g, int p) { return SPW * minv(p) + g; }
+    // exchange row swizzle (complex units) of block B
+    __host__ __device__ static constexpr int sw(int B) { return (B >> 2) & 15; }
+};
+
+// u-multiples the certificate charges beyond KISS's 12 L, each
+// a bound on how far a twiddle (or rotation factor) of the symbol units'
+// transform lies from the KISS value it replaces, charged once per stage on
+// that stage's inputs like the stage's own 6 u:
+//   * KISS's table entry std::exp(i fl(k phinc)) lies within 7.3 u of the
+//     ideal root (phase rounding <= 2 pi u, phinc's rounding <= pi u, the
+//     float cos / sin <= 1 u);
+//   * pass 1's stages 4 and 3 use the correctly rounded ideal root (<= 1 u):
+//     <= 8.3 u from the table, 9 each;
+//   * pass 2's stages 1 and 0 use a table entry times a rounded root (the
+//     fused product: <= 7.3 + 1 + 2 u from the ideal): <= 18 u from the
+//     table, 18 each;
+//   * the two-table rotation, 6 (as k_demod's).
+// 9 + 9 + 18 + 18 + 6 = 60, rounded up.
+constexpr float kWaveExtra = 64.0f;
+
+// The KISS twiddle table as the constant address space: wave-uniform reads
+// become scalar loads (counted on lgkmcnt, so they never wait for the
+// LDS-DMA in flight on vmcnt).  The table is never written by a kernel.
+typedef const __attribute__((address_space(4))) cf32 ctw_t;
+__device__ __forceinline__ ctw_t* ctw(const cf32* p) { return (ctw_t*)p; }
+
+// Compiler-only fence: memory operations are not moved across it, so the
+// scheduler cannot hoist a whole loop's loads (and their registers) ahead.
+__device__ __forceinline__ void cfence() { asm volatile("" ::: "memory"); }
+
+// The wave-uniform twiddles of the symbol units' transform, all 64th roots
+// of unity e^{-2 pi i j / 64} (every uniform index is a multiple of N/64),
+// computed at compile time in double and rounded to float: literal operands
+// (SGPRs set by s_mov), no table load.  They differ from KISS's float table
+// (std::exp of a rounded phase, kissfft.hh:24-29) by a few u, which the
+// certificate charges (kWaveExtra); estimate units use the table itself.
+struct CTw {
+    float re, im;
+};
+struct Roots64 {
+    CTw t[64];
+    constexpr Roots64() : t{} {
+        constexpr double kPiD = 3.14159265358979323846;
+        for (int j = 0; j < 64; ++j) {
+            // angle 2 pi j / 64 = quadrant q (pi/2) + remainder r in [0, pi/2)
+            const int q = j / 16;
+            const double r = 2.0 * kPiD * (double)(j % 16) / 64.0;
+            // cos / sin of r by their Taylor series (|r| < pi/2, 20 terms)
+            double c = 0.0, sn = 0.0, tc = 1.0, ts = r;
+            for (int n = 0; n < 20; ++n) {
+                c += tc;
+                sn += ts;
+                tc *= -r * r / ((2.0 * n + 1.0) * (2.0 * n + 2.0));
+                ts *= -r * r / ((2.0 * n + 2.0) * (2.0 * n + 3.0));
+            }
+            double cq = c, sq = sn;  // rotate by q quarter turns
+            for (int k = 0; k < q; ++k) {
+                const double tmp = cq;
+                cq = -sq;
+                sq = tmp;
+            }
+            t[j] = CTw{(float)cq, (float)-sq};  // e^{-i angle}
+        }
+    }
+};
+constexpr Roots64 kRoots64{};
+__device__ __forceinline__ cf32 root64(int j) {
+    const CTw c = kRoots64.t[j & 63];
+    return cf32{c.re, c.im};
+}
+
+template <bool FAST>
+__device__ __forceinline__ cf32 wmul(cf32 x, cf32 t) {
+    if constexpr (FAST) return cmul_fma(x, t);
+    else return cmul(x, t);
+}
+
+// kf_bfly4 / kf_bfly2 (kissfft.hh:155-185) on registers; `one` (constant
+// after unrolling): every twiddle is tw[0] = (1, 0), skipped on the fast
+// path (magnitudes unchanged, see pass_butterflies' TRIV).
+template <bool FAST>
+__device__ __forceinline__ void wbfly4(cf32& x0, cf32& x1, cf32& x2, cf32& x3, cf32 w1, cf32 w2, cf32 w3,
+                                       bool one) {
+    const cf32 s0 = (FAST && one) ? x1 : wmul<FAST>(x1, w1);
+    const cf32 s1 = (FAST && one) ? x2 : wmul<FAST>(x2, w2);
+    const cf32 s2 = (FAST && one) ? x3 : wmul<FAST>(x3, w3);
+    const cf32 s5 = csub(x0, s1);
+    const cf32 a0 = cadd(x0, s1);
+    const cf32 s3 = cadd(s0, s2);
+    const cf32 s4 = csub(s0, s2);
+    x2 = csub(a0, s3);
+    x0 = cadd(a0, s3);
+    x1 = cadd_rot(s5, s4);
+    x3 = csub_rot(s5, s4);
+}
+template <bool FAST>
+__device__ __forceinline__ void wbfly2(cf32& x0, cf32& x1, cf32 w, bool one) {
+    const cf32 t = (FAST && one) ? x1 : wmul<FAST>(x1, w);
+    x1 = csub(x0, t);
+    x0 = cadd(x0, t);
+}
+
+// Pass 1: KISS stages 5, 4, 3 of every group of the lane.  Twiddle indices
+// are compile-time (wave-uniform loads from the KISS table).
+template <int SF, bool FAST>
+__device__ __forceinline__ void wpass1(cf32 (&v)[64], ctw_t* tab) {
+    using W = WGeo<SF>;
+    // twiddle tw[k] (k a multiple of N/64): the root on the fast path, the
+    // KISS table otherwise
+    auto tw = [&](int k) __attribute__((always_inline)) {
+        if constexpr (FAST) return root64(k / (W::N / 64));
+        else return cf32(tab[k]);
+    };
+    const cf32 t0 = tw(0);
+#pragma unroll
+    for (int g = 0; g < W::SPW; ++g) {
+        // stage 5: radix R5, M = 1 (k = 0)
+#pragma unroll
+        for (int b = 0; b < W::LPS / W::R5; ++b) {
+            if constexpr (W::R5 == 4)
+                wbfly4<FAST>(v[W::reg1(g, 4 * b)], v[W::reg1(g, 4 * b + 1)], v[W::reg1(g, 4 * b + 2)],
+                             v[W::reg1(g, 4 * b + 3)], t0, t0, t0, true);
+            else
+                wbfly2<FAST>(v[W::reg1(g, 2 * b)], v[W::reg1(g, 2 * b + 1)], t0, true);
+        }
+        // stage 4: radix 4, M = M4, twiddle stride 256
+#pragma unroll
+        for (int blk = 0; blk < 4; ++blk) {
+#pragma unroll
+            for (int k = 0; k < W::M4; ++k) {
+                const int b0 = blk * W::M3 + k;
+                wbfly4<FAST>(v[W::reg1(g, b0)], v[W::reg1(g, b0 + W::M4)], v[W::reg1(g, b0 + 2 * W::M4)],
+                             v[W::reg1(g, b0 + 3 * W::M4)], tw(256 * k), tw(512 * k), tw(768 * k), k == 0);
+            }
+        }
+        // stage 3: radix 4, M = M3, twiddle stride 64
+#pragma unroll
+        for (int k = 0; k < W::M3; ++k)
+            wbfly4<FAST>(v[W::reg1(g, k)], v[W::reg1(g, k + W::M3)], v[W::reg1(g, k + 2 * W::M3)],
+                         v[W::reg1(g, k + 3 * W::M3)], tw(64 * k), tw(128 * k), tw(192 * k), k == 0);
+    }
+}
+
+// Per-lane twiddles of pass 2's fast form (lane l of its symbol), q = 1..3:
+// stage 2 tw[16 l q]; the lane factors tw[4 l q] and tw[l q] of stages 1
+// and 0, whose twiddles tw[4 (l + LPS r) q] and tw[(l + LPS r) q] are taken
+// as products with the wave-uniform tw[4 LPS r q] / tw[LPS r q] (r > 0).
+template <int SF>
+struct WTw {
+    cf32 t2[3], t1[3], t0[3];
+    __device__ __forceinline__ void load(const cf32* __restrict__ tw, int l) {
+#pragma unroll
+        for (int q = 1; q <= 3; ++q) {
+            t2[q - 1] = tw[16 * l * q];
+            t1[q - 1] = tw[4 * l * q];
+            t0[q - 1] = tw[l * q];
+        }
+    }
+};
+
+// Pass 2: KISS stages 2, 1, 0 on elements B' (bins l + LPS B').  FAST: the
+// per-lane table above and products with wave-uniform twiddles; exact: every
+// twiddle from the KISS table (per-lane loads, one butterfly group at a time).
+template <int SF, bool FAST>
+__device__ __forceinline__ void wpass2(cf32 (&v)[64], const WTw<SF>& T, const cf32* __restrict__ tw, int l) {
+    using W = WGeo<SF>;
+    cf32 w2[3];
+#pragma unroll
+    for (int q = 1; q <= 3; ++q) w2[q - 1] = FAST ? T.t2[q - 1] : tw[16 * l * q];
+#pragma unroll
+    for (int b = 0; b < 16; ++b)
+        wbfly4<FAST>(v[4 * b], v[4 * b + 1], v[4 * b + 2], v[4 * b + 3], w2[0], w2[1], w2[2], false);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        cfence();
+        cf32 w[3];
+#pragma unroll
+        for (int q = 1; q <= 3; ++q) {
+            if constexpr (FAST) w[q - 1] = r == 0 ? T.t1[q - 1] : cmul_fma(T.t1[q - 1], root64(4 * r * q));
+            else w[q - 1] = tw[4 * (l + W::LPS * r) * q];
+        }
+#pragma unroll
+        for (int gm = 0; gm < 4; ++gm) {
+            const int b0 = 16 * gm + r;
+            wbfly4<FAST>(v[b0], v[b0 + 4], v[b0 + 8], v[b0 + 12], w[0], w[1], w[2], false);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        cfence();  // twiddle loads (and products) one butterfly group at a time
+        cf32 w[3];
+#pragma unroll
+        for (int q = 1; q <= 3; ++q) {
+            if constexpr (FAST) w[q - 1] = r == 0 ? T.t0[q - 1] : cmul_fma(T.t0[q - 1], root64(r * q));
+            else w[q - 1] = tw[(l + W::LPS * r) * q];
+        }
+        wbfly4<FAST>(v[r], v[r + 16], v[r + 32], v[r + 48], w[0], w[1], w[2], false);
+    }
+}
+
+// The 64 x LPS transpose between the passes through the wave's buffer.
+// Pass-1 group g of lane (h, l) is sub-transform c = l + LPS g, whose block
+// B = rev3(c) holds positions LPS B .. LPS B + LPS - 1; pass-2 lane (h, l')
+// takes position l' of every block.  Row B at h N + LPS B, column
+// swizzled by sw(B): b64 writes (16-lane groups) and reads (32-lane groups)
+// meet every bank once.
+template <int SF>
+__device__ __forceinline__ void wexchange(cf32 (&v)[64], cf32* buf, int h, int l) {
+    using W = WGeo<SF>;
+    char* b8 = reinterpret_cast<char*>(buf);
+#pragma unroll
+    for (int g = 0; g < W::SPW; ++g) {
+        const int B = W::rev3(l + W::LPS * g);
+        const int lb = ((h * W::N + B * W::LPS) << 3) | (W::sw(B) << 3);
+#pragma unroll
+        for (int p = 0; p < W::LPS; ++p) lds_st(buf, lb ^ (p << 3), v[W::reg1(g, p)]);
+    }
+    // a wave's LDS operations run in issue order: the reads see the writes
+    asm volatile("" ::: "memory");
+    (void)b8;
+    const int rb = (h * W::N) << 3;
+#pragma unroll
+    for (int Bp = 0; Bp < 64; ++Bp) v[Bp] = lds_ld(buf, rb + ((Bp * W::LPS) << 3) + ((l ^ W::sw(Bp)) << 3));
+}
+
+// LDS-DMA of one unit's windows into the wave's buffer: symbol h of the
+// unit from sample `base_h` of frame `f` (dead halves load a valid window).
+template <int SF>
+__device__ __forceinline__ void wdma(const DemodArgs& A, cf32* buf, unsigned f0, unsigned base0, unsigned f1,
+                                     unsigned base1, int lane) {
+    using W = WGeo<SF>;
+    typedef __attribute__((address_space(3))) void lds_void;
+    typedef __attribute__((address_space(1))) const void g_void;
+#pragma unroll
+    for (int h = 0; h < W::SPW; ++h) {
+        const unsigned f = h ? f1 : f0, base = h ? base1 : base0;
+        const cf32* src = A.iq + (unsigned long long)f * A.frame_samples + base + 2 * lane;
+#pragma unroll
+        for (int r = 0; r < W::PPS; ++r)
+            __builtin_amdgcn_global_load_lds((g_void*)(src + 128 * r), (lds_void*)(buf + h * W::N + 128 * r), 16, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }   // vmcnt(0)
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); } // lgkmcnt(0)
+
+// Max-abs of the frame's two estimate symbols (samples [0, 2N)), the
+// [dechirped] samples as the reference's normalisation scans them
+// (LoRaDemod.cpp:60-78), by the whole wave with all 16-byte loads in
+// flight at once; NaN when a sample is not finite (the frame then goes to
+// the exact re-run).  Same arithmetic as wave_maxabs.
+template <int SF, int MODE>
+__device__ __noinline__ float wscan2(const DemodArgs& A, unsigned f, const cf32* down, int lane) {
+    constexpr int N = 1 << SF;
+    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    constexpr int U = 32;                 // float4 per lane per round
+    constexpr int ROUNDS = N / (64 * U);  // 2N samples = N float4
+    static_assert((128 * U) % N == 0, "chirp index of the unrolled scan");
+    const float4* f4 = reinterpret_cast<const float4*>(A.iq + (unsigned long long)f * A.frame_samples);
+    float fm = 0.0f;
+    cf32 sum = czero();
+    if ((reinterpret_cast<uintptr_t>(f4) & 15) == 0) {
+#pragma unroll
+        for (int rd = 0; rd < ROUNDS; ++rd) {
+            float4 x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = f4[rd * 64 * U + u * 64 + lane];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                cf32 a = cf32{x[u].x, x[u].y}, b = cf32{x[u].z, x[u].w};
+                if constexpr (DECH) {
+                    const unsigned ci = (2u * (unsigned)lane + 128u * (unsigned)u) & (N - 1);
+                    a = cmul(a, down[ci]);
+                    b = cmul(b, down[ci + 1]);
+                }
+                fm = max3_abs(fm, a.x, a.y);
+                fm = max3_abs(fm, b.x, b.y);
+                sum = sum + a;
+                sum = sum + b;
+            }
+        }
+    } else {  // 8-byte aligned frames (odd frame length): one sample per load
+        const cf32* fr = A.iq + (unsigned long long)f * A.frame_samples;
+        for (int i = lane; i < 2 * N; i += 64) {
+            cf32 a = fr[i];
+            if constexpr (DECH) a = cmul(a, down[i & (N - 1)]);
+            fm = max3_abs(fm, a.x, a.y);
+            sum = sum + a;
+        }
+    }
+    // a NaN or inf sample (or an inf - inf) ends in the sum as NaN or in the
+    // maximum as inf: exact re-run (v_max3 lacks the reference's NaN rules)
+    const bool bad = !(sum.x == sum.x && sum.y == sum.y) || !(fm <= 3.40282347e38f);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) fm = fmaxf(fm, __shfl_xor(fm, off, 64));
+    return __ballot(bad) ? __builtin_nanf("") : fm;
+}
+
+// Element e (per-lane index, -1: none) of the lane's registers.
+__device__ __forceinline__ cf32 wpick(const cf32 (&v)[64], int e) {
+    cf32 r = czero();
+#pragma unroll
+    for (int k = 0; k < 64; ++k) r = e == k ? v[k] : r;
+    return r;
+}
+
+// Detector outputs of an estimate unit (LoRaDetector.hpp:39-74; as
+// unit_result): the exact first maximum of |X|^2 over the half's bins
+// l + LPS B', its neighbours' magnitudes and its phase.  Every lane of the
+// half gets the result.
+template <int SF>
+__device__ __forceinline__ UnitResult wunit_result(const cf32 (&v)[64], int h, int l, int lane) {
+    using W = WGeo<SF>;
+    constexpr int N = W::N;
+    ArgMax best{0.0f, 0x7fffffff};
+#pragma unroll
+    for (int e = 0; e < 64; ++e) {  // bins l + LPS e increase with e
+        const cf32 sq = v[e] * v[e];
+        const float m2 = sq.x + sq.y;
+        const bool take = m2 > best.v;
+        best.v = take ? m2 : best.v;
+        best.i = take ? l + W::LPS * e : best.i;
+    }
+#pragma unroll
+    for (int off = W::LPS / 2; off >= 1; off >>= 1) {
+        ArgMax o;
+        o.v = __shfl_xor(best.v, off, 64);
+        o.i = __shfl_xor(best.i, off, 64);
+        best = better(best, o);
+    }
+    if (!(best.v > 0.0f)) best.i = 0;  // nothing beat maxValue = 0
+    const int idx = best.i;
+    const int il = idx > 0 ? idx - 1 : N - 1, ir = idx < N - 1 ? idx + 1 : 0;
+    // the lanes holding bins il, idx, ir pick them; three broadcasts
+    int e = -1;
+    if (l == (il & (W::LPS - 1))) e = il / W::LPS;
+    if (l == (idx & (W::LPS - 1))) e = idx / W::LPS;
+    if (l == (ir & (W::LPS - 1))) e = ir / W::LPS;
+    const cf32 mine = wpick(v, e);
+    const int hb = h * W::LPS;
+    auto get = [&](int bin) {
+        const int src = hb + (bin & (W::LPS - 1));
+        return cf32{__shfl(mine.x, src, 64), __shfl(mine.y, src, 64)};
+    };
+    const cf32 lb = get(il), bn = get(idx), rb = get(ir);
+    (void)lane;
+    UnitResult r;
+    const float mv = best.v > 0.0f ? best.v : 0.0f;
+    const float fund = sqrtf(mv);
+    const float left = lphy_libm::cabsf_exact(lb.x, lb.y);
+    const float right = lphy_libm::cabsf_exact(rb.x, rb.y);
+    const double demon = (2.0 * (double)fund) - (double)right - (double)left;
+    r.idx = idx;
+    r.valid = mv > 0.0f;
+    r.findex = demon == 0.0 ? 0.0f : (float)(0.5 * (double)(right - left) / demon);
+    r.phase = lphy_libm::atan2f_exact(bn.y, bn.x);
+    r.nan = 0;
+    return r;
+}
+
+// The rare parts of k_wave live in functions of their own (not inlined):
+// their registers then never compete with the symbol units' 64-value
+// transform, and the few calls per frame cost a spill of the loop state.
+
+// An estimate unit from the wave's buffer (symbol h of the pair at SF 11):
+// KISS's exact transform and the detector outputs; .nan when a bin is NaN
+// (the frame then goes to the exact re-run, as in k_frames).
+template <int SF, int MODE>
+__device__ __noinline__ UnitResult west_unit(const DemodArgs& A, cf32* buf, const cf32* dnl, float scale,
+                                             bool live) {
+    using W = WGeo<SF>;
+    constexpr int N = W::N, LPS = W::LPS;
+    constexpr bool M0 = (MODE & 3) == LPHY_MODE_DEMODULATE;
+    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    const int lane = threadIdx.x & 63, h = lane / LPS, l = lane % LPS;
+    cf32 v[64];
+    const int rb = (h * N + l) << 3;
+#pragma unroll
+    for (int e = 0; e < 64; ++e) {
+        if ((e & 7) == 0) cfence();
+        cf32 x = lds_ld(buf, rb + ((LPS * e) << 3));
+        if constexpr (DECH) x = cmul(x, dnl[l + LPS * e]);
+        if constexpr (!M0) x = cscale(x, scale);
+        v[e] = live ? x : czero();
+    }
+    const WTw<SF> T{};  // unused by the exact pass
+    wpass1<SF, false>(v, ctw(A.tw));
+    wexchange<SF>(v, buf, h, l);
+    wpass2<SF, false>(v, T, A.tw, l);
+    float sumsq = 0.0f;
+#pragma unroll
+    for (int e = 0; e < 64; ++e) {
+        const cf32 sq = v[e] * v[e];
+        sumsq += sq.x + sq.y;
+    }
+    const unsigned long long nb = __ballot(!(sumsq == sumsq));
+    UnitResult ur = wunit_result<SF>(v, h, l, lane);
+    ur.nan = (LPS == 64 ? nb : ((nb >> (32 * h)) & 0xffffffffull)) != 0 ? 1 : 0;
+    if (!live) ur = UnitResult{0, 0, 0.0f, 0.0f, 0};
+    return ur;
+}
+
+// The frame's rotation tables: q[b] = [scale] e^{j rate (l + LPS b)} for the
+// lane, and p = e^{j rate 8 LPS (lane & 7)} (the caller takes p of lanes 0..7
+// as the wave-uniform table).
+struct WRot {
+    cf32 q[8];
+    cf32 p;
+};
+template <int SF, int MODE>
+__device__ __noinline__ WRot wrot(float rate, float scale) {
+    constexpr int LPS = WGeo<SF>::LPS;
+    const int lane = threadIdx.x & 63, l = lane % LPS;
+    WRot r;
+#pragma unroll 1
+    for (int b = 0; b < 8; ++b) {
+        float sn, cs;
+        lphy_libm::sincosf_exact(rate * (float)(l + LPS * b), &sn, &cs);
+        cf32 t = cf32{cs, sn};
+        if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) t = cscale(t, scale);
+        r.q[b] = t;
+    }
+    float sn, cs;
+    lphy_libm::sincosf_exact(rate * (float)(8 * LPS * (lane & 7)), &sn, &cs);
+    r.p = cf32{cs, sn};
+    return r;
+}
+
+// Frame end under the speculative normalisation (as k_frames' close): the
+// samples no symbol window covers are scanned, then the frame's true
+// max-abs confirms the two-symbol normalisation, sends the frame to the
+// exact re-run (NaN / inf), or marks it for k_wsettle.
+template <int SF, int MODE>
+__device__ __noinline__ void wclose(const DemodArgs& A, const cf32* dnl, unsigned f, int t_off, float mx01,
+                                    float m, float r, bool nan, bool open) {
+    constexpr int N = 1 << SF;
+    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    const unsigned S = (unsigned)A.total_syms;
+    const unsigned cnt = DECH ? S * N : (unsigned)A.frame_samples;
+    const unsigned end = covered_end(S, N, cnt, t_off);
+    bool fbad = false;
+    if (end < cnt) m = fmaxf(m, wave_range_maxabs<SF, MODE>(A, f, end, cnt, dnl, fbad));
+    if ((threadIdx.x & 63) == 0) {
+        const float mt = fmaxf(m, mx01);
+        const lphy_frame_meta mg = norm_meta(mx01, true, 0), me = norm_meta(mt, true, 0);
+        if (nan || fbad || !(mt <= 3.40282347e38f)) {
+            A.meta[f].status = kStatusFixup;
+        } else if (me.scale != mg.scale || me.normalised != mg.normalised) {
+            A.meta[f].cfo = mt;
+            A.meta[f].time_offset = r;
+            A.meta[f].status = open ? kStatusSettleRecheck : kStatusSettle;
+        }
+    }
+}
+
+// Timing experiments only (-DLPHY_PROFILE_PHASES, tools/ubench): per-wave
+// clock sums of the unit phases, added to A.counters[1..8] at the end.
+#ifdef LPHY_PROFILE_PHASES
+#define WPH_DECL unsigned long long wph[8] = {}, wpt = clock64();
+#define WPH(i)                                  \
+    do {                                        \
+        const unsigned long long t_ = clock64(); \
+        wph[i] += t_ - wpt;                     \
+        wpt = t_;                               \
+    } while (0)
+#define WPH_FLUSH(A)                                                  \
+    if ((threadIdx.x & 63) == 0)                                      \
+        for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&(A).counters[1 + i_], wph[i_]);
+#else
+#define WPH_DECL
+#define WPH(i) \
+    do {       \
+    } while (0)
+#define WPH_FLUSH(A)
+#endif
+
+// Unit kinds and the per-wave schedule cursor (see the header comment).
+enum : int { kWDead = 0, kWEst = 1, kWSym = 2 };
+
+struct WCursor {
+    int phase;      // 0: E(0); 1: D(k) before E(k+1); 2: E(k+1); 3: D(k) after; 4: done
+    unsigned k, j;  // frame (wave-local) of the D units; unit index within the phase
+};
+
+template <int SF>
+struct WSched {
+    unsigned nk, ND, p;
+    // first unit of a (possibly empty) phase
+    __device__ __forceinline__ void settle(WCursor& c) const {
+        for (;;) {
+            if (c.phase == 1 && c.j >= p) { c.phase = c.k + 1 < nk ? 2 : 3; c.j = c.phase == 2 ? 0 : p; continue; }
+            if (c.phase == 2 && c.j >= (unsigned)WGeo<SF>::NE) { c.phase = 3; c.j = p; continue; }
+            if (c.phase == 3 && c.j >= ND) {
+                if (++c.k >= nk) { c.phase = 4; return; }
+                c.phase = 1; c.j = 0; continue;
+            }
+            if (c.phase == 0 && c.j >= (unsigned)WGeo<SF>::NE) { c.phase = 1; c.j = 0; continue; }
+            return;
+        }
+    }
+    __device__ __forceinline__ WCursor first() const { WCursor c{0, 0, 0}; settle(c); return c; }
+    __device__ __forceinline__ WCursor next(WCursor c) const { ++c.j; settle(c); return c; }
+    // kind, wave-local frame, unit index (estimate unit / first symbol s = SPW j)
+    __device__ __forceinline__ int kind(const WCursor& c) const {
+        return c.phase == 4 ? kWDead : (c.phase == 0 || c.phase == 2) ? kWEst : kWSym;
+    }
+    __device__ __forceinline__ unsigned frame(const WCursor& c) const { return c.phase == 2 ? c.k + 1 : c.k; }
+};
+
+// Frame record the symbol units read (wave-uniform), kept per wave-local
+// frame parity: frame k's record is written by its fold, while frame k - 1's
+// symbol units still run.
+struct WFrame {
+    float rate, scale, mx;  // mx: the two estimate symbols' max-abs (modes 1/2)
+    int t_off;
+    int ok;                 // estimate folded, status 0
+};
+
+template <int SF, int MODE>
+__global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
+    using W = WGeo<SF>;
+    constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
+    constexpr bool M0 = (MODE & 3) == LPHY_MODE_DEMODULATE;
+    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    constexpr bool DN = (MODE & 3) != LPHY_MODE_LORA_DEMODULATE;  // down-chirp used
+    const DemodArgs& A = P.A;
+    __shared__ cf32 sbuf[W::WPB][W::BUF];
+    __shared__ cf32 dnl[DN ? N : 1];
+
+    const int tid = threadIdx.x;
+    if constexpr (DN) {
+        for (int i = tid; i < N; i += 256) dnl[i] = A.down[i];
+    }
+    __syncthreads();  // the only workgroup barrier: waves are independent below
+
+    const int lane = tid & 63, wv = tid >> 6;
+    const int h = lane / LPS, l = lane % LPS;
+    cf32* buf = sbuf[wv];
+    const unsigned nframes = (unsigned)A.frames;
+    const unsigned S = (unsigned)A.total_syms;
+    const unsigned Wn = P.waves;
+    const unsigned w = blockIdx.x * W::WPB + wv;
+    if (w >= nframes) return;
+    WSched<SF> sch;
+    sch.nk = (nframes - 1 - w) / Wn + 1;
+    sch.ND = (S + SPW - 1) / SPW;
+    sch.p = sch.ND >= 2 ? sch.ND - 2 : 0;
+    const bool spec = !M0 && A.spec != 0;
+
+    WTw<SF> T;
+    T.load(A.tw, l);
+
+    WFrame rec0{0.0f, 1.0f, 0.0f, 0, 0}, rec1 = rec0;
+    auto rec = [&](unsigned k) -> WFrame { return (k & 1) ? rec1 : rec0; };
+    auto set_rec = [&](unsigned k, const WFrame& r) {
+        if (k & 1) rec1 = r;
+        else rec0 = r;
+    };
+    auto fglob = [&](unsigned k) { return w + k * Wn; };
+    // window start of symbol s under time shift t (LoRaDemod.cpp:144-150, sym_ctx)
+    auto wbase = [&](unsigned s, int t) {
+        lphy_frame_meta m{};
+        m.t_off = t;
+        return sym_ctx(A, 0, s, true, N, m).base;
+    };
+    auto dma_unit = [&](const WCursor& c) {
+        const int kd = sch.kind(c);
+        if (kd == kWDead) return;
+        const unsigned k = sch.frame(c), f = fglob(k);
+        if (kd == kWEst) {  // SF 12: symbol j; SF 11: symbols 0 and 1
+            wdma<SF>(A, buf, f, SPW == 1 ? c.j * (unsigned)N : 0u, f, (unsigned)N, lane);
+        } else {
+            const WFrame R = rec(k);
+            const unsigned s0 = SPW * c.j, s1 = (SPW == 2 && s0 + 1 < S) ? s0 + 1 : s0;
+            wdma<SF>(A, buf, f, wbase(s0, R.t_off), f, wbase(s1, R.t_off), lane);
+        }
+    };
+
+    // rotation of the frame in demodulation: Qr[b] = [scale] e^{j rate (l + LPS b)}
+    // per lane, Pr[a] = e^{j rate 8 LPS a} wave-uniform (sample i = l + LPS (8a + b))
+    cf32 Qr[8], Pr[8];
+    unsigned rot_frame = 0xffffffffu;
+    // speculative normalisation of the frame in demodulation (lane state)
+    constexpr float kBig = 3.0e38f;
+    float sp_mx = 0.0f, sp_r = kBig;
+    unsigned sp_fl = 0u;
+    UnitResult ur0{0, 0, 0.0f, 0.0f, 0};  // SF 12: the first estimate unit's result
+
+    WCursor cu = sch.first();
+    WPH_DECL
+    if constexpr (!M0) {
+        const float m = wscan2<SF, MODE>(A, fglob(0), dnl, lane);
+        WFrame r = rec0;
+        r.mx = m;
+        rec0 = r;
+    }
+    dma_unit(cu);
+    while (sch.kind(cu) != kWDead) {
+        const WCursor nx = sch.next(cu);
+        const unsigned k = sch.frame(cu), f = fglob(k);
+        cf32 v[64];
+        WPH(7);
+        wait_vm0();  // this unit's IQ has landed
+        WPH(0);
+        if (sch.kind(cu) == kWSym) {
+            const WFrame R = rec(k);
+            if (k != rot_frame) {
+                rot_frame = k;
+                const WRot rt = wrot<SF, MODE>(R.rate, R.scale);
+#pragma unroll
+                for (int b = 0; b < 8; ++b) Qr[b] = rt.q[b];
+#pragma unroll
+                for (int a = 0; a < 8; ++a)
+                    Pr[a] = cf32{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(rt.p.x), a)),
+                                 __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rt.p.y), a))};
+            }
+            const unsigned s = SPW * cu.j + (unsigned)h;
+            const bool live = s < S;
+            lphy_frame_meta m{};
+            m.rate = R.rate;
+            m.scale = R.scale;
+            m.t_off = R.t_off;
+            m.status = R.ok ? 0 : -1;
+            m.have_sync = 1;
+            const SymCtx c = sym_ctx(A, f, live ? s : 0u, live, N, m);
+            // staging: [exact dechirp,] certified rotation, from the LDS copy
+            float amax = 0.0f;
+            const int rb = (h * N + l) << 3;
+#pragma unroll
+            for (int e = 0; e < 64; ++e) {
+                if ((e & 7) == 0) cfence();  // 8 samples' loads in flight at a time
+                const cf32 x = lds_ld(buf, rb + ((LPS * e) << 3));
+                cf32 p = x;
+                if constexpr (DECH) p = cmul(x, dnl[(c.base + (unsigned)(l + LPS * e)) & (N - 1)]);
+                amax = max3_abs(amax, p.x, p.y);
+                if constexpr (M0) p = cmul(p, dnl[l + LPS * e]);
+                // (a unit whose symbol is not demodulated transforms whatever
+                // its window holds; nothing of it is stored)
+                v[e] = cmul_fma(cmul_fma(p, Qr[e & 7]), Pr[e >> 3]);
+            }
+            WPH(1);
+            wpass1<SF, true>(v, ctw(A.tw));
+            WPH(2);
+            wexchange<SF>(v, buf, h, l);
+            wait_lgkm0();  // the exchange reads are done: the buffer is free
+            dma_unit(nx);  // the next unit's IQ lands during pass 2
+            WPH(3);
+            wpass2<SF, true>(v, T, A.tw, l);
+            WPH(4);
+            // keyed top two over the half's bins l + LPS e (key: |X|^2 bits,
+            // low 6 bits the element; see team_argmax2_keyed_first)
+            unsigned k1 = 0u, k2 = 0u;
+#pragma unroll
+            for (int e = 0; e < 64; ++e) {
+                const cf32 sq = v[e] * v[e];
+                const unsigned key = (__float_as_uint(sq.x + sq.y) & ~63u) | (unsigned)e;
+                k2 = med3_u32(k1, k2, key);
+                k1 = k1 > key ? k1 : key;
+            }
+            unsigned K1 = k1, K2 = k2;
+#pragma unroll
+            for (int off = 1; off < LPS; off <<= 1) {
+                const unsigned o1 = (unsigned)__shfl_xor((int)K1, off, 64);
+                const unsigned o2 = (unsigned)__shfl_xor((int)K2, off, 64);
+                K2 = med3_u32(K1, o1, K2 > o2 ? K2 : o2);
+                K1 = K1 > o1 ? K1 : o1;
+            }
+            const unsigned long long bm = __ballot(k1 == K1);
+            const unsigned long long hm = LPS == 64 ? bm : ((bm >> (32 * h)) & 0xffffffffull);
+            ArgMax2 b2;
+            b2.v = __uint_as_float(K1 & ~63u);
+            b2.v2 = __uint_as_float(K2 | 63u);
+            b2.i = (__ffsll((long long)hm) - 1) + LPS * (int)(K1 & 63u);
+            float am = 1.0f;  // modes 1/2: normalised frame (see fast_certified)
+            if constexpr (M0) {
+#pragma unroll
+                for (int off = 1; off < LPS; off <<= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
+                am = amax;
+            }
+            const float cb1 = cert_bound<SF>(c.rate, c.start, 1.0f, kWaveExtra);
+            const float cgap = cert_gap(b2);
+            const bool cert = cgap > 4.0f * (cb1 * am) && (float)N * 1.41421366f * am * 1.0001f < 1e18f &&
+                              am >= 1e-20f && b2.v >= 1e-30f;
+            const bool redo = c.ok && !cert;
+            if (live && l == 0) {
+                const uint16_t out = redo ? kSymRecheck : (uint16_t)b2.i;
+                if (c.have_sync && c.s < 2) store_symbol(A, c, c.ok ? out : (uint16_t)0);
+                else if (c.ok) store_symbol(A, c, out);
+                if (redo) A.meta[c.f].status = kStatusRecheck;
+            }
+            if (spec && c.ok) {
+                sp_mx = fmaxf(sp_mx, amax);
+                const cf32 q = v[0] * v[0];
+                const float q2 = q.x + q.y;
+                if (!(q2 == q2)) sp_fl |= 1u;  // a NaN sample reaches every bin
+                if (l == 0) {
+                    if (redo) sp_fl |= 2u;
+                    else sp_r = fminf(sp_r, cgap * __builtin_amdgcn_rcpf(cb1) * (1.0f - 4.0f * kU));
+                }
+            }
+            WPH(5);
+            // the frame's last symbol unit closes it (speculative normalisation)
+            if (spec && cu.phase == 3 && cu.j + 1 == sch.ND) {
+                float mm = sp_mx, rr = sp_r;
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    mm = fmaxf(mm, __shfl_xor(mm, off, 64));
+                    rr = fminf(rr, __shfl_xor(rr, off, 64));
+                }
+                const bool nan = __ballot(sp_fl & 1u) != 0, open = __ballot(sp_fl & 2u) != 0;
+                sp_mx = 0.0f;
+                sp_r = kBig;
+                sp_fl = 0u;
+                if (R.ok) wclose<SF, MODE>(A, dnl, f, R.t_off, R.mx, mm, rr, nan, open);
+            }
+        } else {
+            // estimate unit(s): KISS's arithmetic, bit for bit (LoRaDemod.cpp:80-136,
+            // phy.cpp:81-148); SF 12 symbol j, SF 11 symbol h of the pair
+            const WFrame R0 = rec(k);
+            lphy_frame_meta nm{};
+            nm.scale = 1.0f;
+            nm.have_sync = 1;
+            if constexpr (!M0) nm = norm_meta_hot(R0.mx, true, A.no_scratch);
+            const bool live = nm.status == 0;
+            const UnitResult ur = west_unit<SF, MODE>(A, buf, dnl, nm.scale, live);
+            bool fold_now = true;
+            UnitResult ua = ur, ub = ur;
+            if constexpr (SPW == 1) {
+                if (cu.j == 0) {
+                    ur0 = ur;
+                    fold_now = false;
+                } else {
+                    ua = ur0;
+                }
+            } else {  // the pair's second estimate unit from the upper half
+                ub.idx = __shfl(ur.idx, 32, 64);
+                ub.valid = __shfl(ur.valid, 32, 64);
+                ub.findex = __shfl(ur.findex, 32, 64);
+                ub.phase = __shfl(ur.phase, 32, 64);
+                ub.nan = __shfl(ur.nan, 32, 64);
+                ua.idx = __shfl(ur.idx, 0, 64);
+                ua.valid = __shfl(ur.valid, 0, 64);
+                ua.findex = __shfl(ur.findex, 0, 64);
+                ua.phase = __shfl(ur.phase, 0, 64);
+                ua.nan = __shfl(ur.nan, 0, 64);
+            }
+            if (fold_now) {
+                lphy_frame_meta m = nm;
+                if (m.status == 0) {
+                    EstFold fold;
+                    if (ua.valid) fold.add(ua.idx, ua.findex, 0, ua.phase);
+                    else fold.add(0, 0.0f, 0, 0.0f);
+                    if (ub.valid) fold.add(ub.idx, ub.findex, 0, ub.phase);
+                    else fold.add(0, 0.0f, 0, 0.0f);
+                    fold.finish(m, 2, N, 1);
+                    if (ua.nan || ub.nan) m.status = kStatusFixup;
+                }
+                if (lane == 0) meta_put_est(&A.meta[f], m);
+                WFrame r = R0;
+                r.rate = m.rate;
+                r.scale = m.scale;
+                r.t_off = m.t_off;
+                r.ok = m.status == 0 ? 1 : 0;
+                set_rec(k, r);
+            }
+            dma_unit(nx);  // after the fold: a symbol unit's window needs the time shift
+            WPH(6);
+        }
+        // the two-symbol scan of the frame whose estimate comes next
+        if constexpr (!M0) {
+            if (sch.kind(nx) == kWEst && nx.j == 0 && nx.phase == 2) {
+                const unsigned kn = sch.frame(nx);
+                WFrame r = rec(kn);
+                r.mx = wscan2<SF, MODE>(A, fglob(kn), dnl, lane);
+                set_rec(kn, r);
+            }
+        }
+        cu = nx;
+    }
+    WPH(7);
+    WPH_FLUSH(A)
+}
+
+// Frames k_wave closed with a normalisation its two-symbol scan did not
+// predict (status kStatusSettle[Recheck], record {cfo: the frame's max-abs,
+// time_offset: the symbols' least certificate ratio}): one wavefront per
+// frame re-runs the two estimate FFTs with the exact scale (KISS's
+// arithmetic, as the estimate units) and keeps the symbols when the time
+// shift is unchanged and every certified symbol's lead covers the larger
+// sample bound and the rate difference (settle_frames' rule); else the frame
+// goes to k_post's exact re-run.  Other frames return at once.
+template <int SF, int MODE>
+__global__ __launch_bounds__(256, 1) void k_wsettle(DemodArgs A) {
+    using W = WGeo<SF>;
+    constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
+    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    __shared__ cf32 sbuf[W::WPB][W::BUF];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const unsigned long long f = (unsigned long long)blockIdx.x * W::WPB + wv;
+    if (f >= A.frames) return;
+    const lphy_frame_meta sm = A.meta[f];
+    if (!(sm.status == kStatusSettle || sm.status == kStatusSettleRecheck)) return;
+    const int h = lane / LPS, l = lane % LPS;
+    const lphy_frame_meta e0 = norm_meta(sm.cfo, true, 0);
+    WTw<SF> T;
+    T.load(A.tw, l);
+    const cf32* fr = A.iq + f * A.frame_samples;
+    UnitResult ua{0, 0, 0.0f, 0.0f, 0}, ub = ua;
+#pragma unroll 1
+    for (int j = 0; j < W::NE; ++j) {
+        const unsigned sy = SPW == 1 ? (unsigned)j : (unsigned)h;
+        cf32 v[64];
+#pragma unroll
+        for (int e = 0; e < 64; ++e) {
+            if ((e & 15) == 0) cfence();
+            const int i = l + LPS * e;
+            cf32 x = fr[sy * N + i];
+            if constexpr (DECH) x = cmul(x, A.down[i]);
+            v[e] = cscale(x, e0.scale);
+        }
+        wpass1<SF, false>(v, ctw(A.tw));
+        wexchange<SF>(v, sbuf[wv], h, l);
+        wpass2<SF, false>(v, T, A.tw, l);
+        const UnitResult ur = wunit_result<SF>(v, h, l, lane);
+        if constexpr (SPW == 1) {
+            if (j == 0) ua = ur;
+            else ub = ur;
+        } else {
+            ua.idx = __shfl(ur.idx, 0, 64);
+            ua.valid = __shfl(ur.valid, 0, 64);
+            ua.findex = __shfl(ur.findex, 0, 64);
+            ua.phase = __shfl(ur.phase, 0, 64);
+            ub.idx = __shfl(ur.idx, 32, 64);
+            ub.valid = __shfl(ur.valid, 32, 64);
+            ub.findex = __shfl(ur.findex, 32, 64);
+            ub.phase = __shfl(ur.phase, 32, 64);
+        }
+    }
+    lphy_frame_meta e = e0;
+    EstFold fold;
+    if (ua.valid) fold.add(ua.idx, ua.findex, 0, ua.phase);
+    else fold.add(0, 0.0f, 0, 0.0f);
+    if (ub.valid) fold.add(ub.idx, ub.findex, 0, ub.phase);
+    else fold.add(0, 0.0f, 0, 0.0f);
+    fold.finish(e, 2, N, 1);
+    const float a = fmaxf(1.0f, sm.cfo * sm.scale) * 1.0001f;
+    const float b1 = cert_bound<SF>(sm.rate, sm.rate * (float)sm.t_off, 1.0f);
+    const float d = fabsf(e.rate - sm.rate) * (1.0f + 4.0f * kU);
+    const float A1 = (float)N * 1.41421366f * 1.0001f;
+    const bool ok = e.t_off == sm.t_off && sm.t_off >= -N && sm.t_off <= N &&
+                    sm.time_offset > 4.0f * a + 4.0f * d * (float)N * A1 * a / b1;
+    if (lane == 0) {
+        lphy_frame_meta r = e;
+        r.sw0 = sm.sw0;
+        r.sw1 = sm.sw1;
+        r.status = !ok ? kStatusFixup : (sm.status == kStatusSettleRecheck ? kStatusRecheck : 0);
+        A.meta[f] = r;
+    }
+}

@@ -1,5 +1,5 @@
-"""Concurrency and ordering of the separate-launch path (SF 11-12, and SF
-<= 10 with LPHY_F_UNFUSED):
+"""Concurrency and ordering at SF 11-12 (the fused wave kernel and the
+separate launches) and SF <= 10 with LPHY_F_UNFUSED:
 
 * two lphy_hip_demod_batch calls on ONE context issued on two streams at
   once give the single-stream results bit for bit (the SF 11-12
@@ -52,7 +52,8 @@ def _host(lphy, syms, pay, meta, nf, per):
 
 
 @pytest.mark.parametrize("sf,mode", [(12, 2), (11, 2), (12, 1), (11, 0)])
-def test_two_streams_one_context(oracle, lphy, sf, mode):
+@pytest.mark.parametrize("unfused", [False, True])
+def test_two_streams_one_context(oracle, lphy, sf, mode, unfused):
     nf = 40
     iq, fs = _noisy_frames(oracle, sf, nf, -8.0, seed=sf * 3 + mode)
     iq2 = np.ascontiguousarray(iq[::-1])  # a different batch on the other stream
@@ -61,7 +62,7 @@ def test_two_streams_one_context(oracle, lphy, sf, mode):
     a_t = torch.from_numpy(iq.view(np.float32).copy()).to(dev)
     b_t = torch.from_numpy(iq2.view(np.float32).copy()).to(dev)
     per = d.syms_per_frame(fs, mode)
-    F = lphy.F_DECODE
+    F = lphy.F_DECODE | (lphy.F_UNFUSED if unfused else 0)
     # single-stream references, one after the other
     s0 = torch.cuda.current_stream()
     ra = _host(lphy, *_dev_run(lphy, d, a_t, nf, fs, mode, F, s0.cuda_stream), nf, per)
@@ -81,7 +82,8 @@ def test_two_streams_one_context(oracle, lphy, sf, mode):
             np.testing.assert_array_equal(got[2].view(np.uint8), ref[2].view(np.uint8))
 
 
-@pytest.mark.parametrize("sf,mode,unfused", [(12, 2, False), (11, 1, False), (12, 0, False),
+@pytest.mark.parametrize("sf,mode,unfused", [(12, 2, True), (11, 1, True), (12, 0, True),
+                                             (12, 2, False), (11, 2, False),
                                              (9, 2, True), (7, 0, True)])
 def test_forced_recheck_no_symbol_lost(oracle, lphy, sf, mode, unfused):
     nf = 24 if sf >= 11 else 96

@@ -46,7 +46,7 @@ def run(sf, names):
         lib = lphy._LIB
         if hasattr(lib, "lphy_hip_phase_cycles"):
             import ctypes as C
-            out = (C.c_ulonglong * 4)()
+            out = (C.c_ulonglong * 8)()
             lib.lphy_hip_phase_cycles.argtypes = [C.c_void_p, C.c_void_p]
             lib.lphy_hip_phase_cycles(wl.dem.ctx, out)  # clear
             wl._event_ms(mode, D | lphy.F_UNFUSED | lphy.F_STAGE_SYMBOLS, 1)

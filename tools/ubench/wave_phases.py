@@ -1,7 +1,8 @@
-"""k_frames tile clocks (timing aid only): mixed (estimate-bearing) tiles vs
-symbol-only tiles, and the fold/rotation-table tail of the mixed tiles.
+"""k_wave phase clocks (timing aid only): per-wave clock sums of the unit
+phases (DMA wait, staging, pass 1, exchange + DMA issue, pass 2, argmax +
+store, estimate units, other) on the bench workload of one SF.
 Needs a variant built with -DLPHY_PROFILE_PHASES (variants.py build).
-  python tools/ubench/frame_phases.py <sf> <variant> [mode]"""
+  python tools/ubench/wave_phases.py <sf> <variant> [mode]"""
 import ctypes as C
 import sys
 from pathlib import Path
@@ -25,11 +26,11 @@ lib.lphy_hip_phase_cycles.argtypes = [C.c_void_p, C.c_void_p]
 lib.lphy_hip_phase_cycles(wl.dem.ctx, out)
 wl._event_ms(mode, flags, 1, warmup=0)
 lib.lphy_hip_phase_cycles(wl.dem.ctx, out)
-mix, sym, fold, nmix = out[0], out[1], out[2], out[3]
-N = 1 << sf
-wt = 64 // max(N // 16, 1)
-nsym = wl.frames * 68 // wt - nmix  # approximate: prefix tiles ignored
-tot = mix + sym
-print(f"SF{sf} mode {mode} {name}: {ms:.3f} ms; mixed tiles {mix / tot:.3f} of wave clocks "
-      f"(fold+rtab+close tail {fold / tot:.3f}); mixed tiles {nmix}, "
-      f"cycles per mixed tile {mix / max(nmix, 1):.0f}, per symbol-only tile {sym / max(nsym, 1):.0f}", flush=True)
+names = ["dma_wait", "staging", "pass1", "exch+dma", "pass2", "argmax+out", "estimate", "other"]
+tot = sum(out) or 1
+waves = min(256, (wl.frames + 3) // 4) * 4
+units = wl.frames * (66 + 2) / (64 // max((1 << sf) // 64, 1))
+print(f"SF{sf} mode {mode} {name}: {ms:.3f} ms/launch (phase-clock build), per-wave cycles {tot / waves:.0f}, "
+      f"per unit {tot / units:.0f}", flush=True)
+for n, v in zip(names, out):
+    print(f"  {n:11s} {v / tot:6.3f}  {v / units:8.0f} cycles/unit", flush=True)
