@@ -76,7 +76,7 @@ struct DemodArgs {
     // atomic max / min), flags (1 NaN, 2 symbol left open)}; nullptr = off
     uint4* spec_big;
     int debug_recheck;       // LPHY_F_DEBUG_RECHECK: mark estimated frames kStatusRecheck before k_demod
-    int wave;                // the fused SF 11-12 launch (k_wave) ran: k_post's fix-up starts with k_wsettle
+    int wave;                // the fused SF 11-12 launch (k_wave) ran (it settles its frames itself)
     // persistent demod workers: symbol stride per step split into whole
     // frames + symbols (host-computed, so the kernel never divides)
     unsigned stride_f, stride_s;
@@ -2496,15 +2496,6 @@ int launch_frames_sf(const DemodArgs& A, hipStream_t st) {
 template <int SF>
 int launch_post_sf(int mode, const DemodArgs& A, const FinalArgs& F, bool fix, bool fin, hipStream_t st) {
     const dim3 grid((unsigned)((A.frames + kTile - 1) / kTile));
-    if constexpr (SF == 11 || SF == 12) {
-        if (fix && A.wave && A.spec && mode != LPHY_MODE_DEMODULATE) {
-            const dim3 wg((unsigned)((A.frames + WGeo<SF>::WPB - 1) / WGeo<SF>::WPB));
-            if (mode == LPHY_MODE_LORA_DEMODULATE)
-                hipLaunchKernelGGL((k_wsettle<SF, LPHY_MODE_LORA_DEMODULATE>), wg, dim3(256), 0, st, A);
-            else
-                hipLaunchKernelGGL((k_wsettle<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>), wg, dim3(256), 0, st, A);
-        }
-    }
     if (fix && A.spec_big) {
         if (mode == LPHY_MODE_LORA_DEMODULATE)
             hipLaunchKernelGGL((k_spec_settle<SF, LPHY_MODE_LORA_DEMODULATE>), dim3((unsigned)A.frames), dim3(kTile), 0,

@@ -57,6 +57,7 @@ struct WGeo {
     static constexpr int M4 = N / 1024;   // KISS M(4)
     static constexpr int R5 = (SF & 1) ? 2 : 4;  // radix of the innermost stage
     static constexpr int PPS = N / 128;   // LDS-DMA pieces (1 KiB) per symbol
+    static_assert(PPS % 4 == 0, "LDS-DMA in groups of four pieces");
     static constexpr int BUF = SPW * N;   // complex per wave buffer
     static constexpr int WPB = 4;         // waves per workgroup
     // block of pass-1 group c = i mod 64 in KISS's output order: base-4
@@ -97,6 +98,15 @@ constexpr float kWaveExtra = 64.0f;
 // LDS-DMA in flight on vmcnt).  The table is never written by a kernel.
 typedef const __attribute__((address_space(4))) cf32 ctw_t;
 __device__ __forceinline__ ctw_t* ctw(const cf32* p) { return (ctw_t*)p; }
+
+// The kernel's own argument block in the kernarg segment (constant address
+// space), for the functions k_wave calls out of line: a reference to its
+// DemodArgs would make the compiler copy the whole block to scratch, whose
+// reloads (vmcnt) then wait for the LDS-DMA in flight; through this pointer
+// every field is a scalar load (lgkmcnt).  P is k_wave's only argument, at
+// offset 0 of the segment.
+typedef const __attribute__((address_space(4))) FrameArgs* KArgs;
+__device__ __forceinline__ const DemodArgs& kargs(KArgs k) { return ((const FrameArgs*)k)->A; }
 
 // Compiler-only fence: memory operations are not moved across it, so the
 // scheduler cannot hoist a whole loop's loads (and their registers) ahead.
@@ -236,14 +246,17 @@ struct WTw {
 // per-lane table above and products with wave-uniform twiddles; exact: every
 // twiddle from the KISS table (per-lane loads, one butterfly group at a time).
 template <int SF, bool FAST>
-__device__ __forceinline__ void wpass2(cf32 (&v)[64], const WTw<SF>& T, const cf32* __restrict__ tw, int l) {
-    using W = WGeo<SF>;
+__device__ __forceinline__ void wpass2_s2(cf32 (&v)[64], const WTw<SF>& T, const cf32* __restrict__ tw, int l) {
     cf32 w2[3];
 #pragma unroll
     for (int q = 1; q <= 3; ++q) w2[q - 1] = FAST ? T.t2[q - 1] : tw[16 * l * q];
 #pragma unroll
     for (int b = 0; b < 16; ++b)
         wbfly4<FAST>(v[4 * b], v[4 * b + 1], v[4 * b + 2], v[4 * b + 3], w2[0], w2[1], w2[2], false);
+}
+template <int SF, bool FAST>
+__device__ __forceinline__ void wpass2_s10(cf32 (&v)[64], const WTw<SF>& T, const cf32* __restrict__ tw, int l) {
+    using W = WGeo<SF>;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         cfence();
@@ -270,6 +283,11 @@ __device__ __forceinline__ void wpass2(cf32 (&v)[64], const WTw<SF>& T, const cf
         }
         wbfly4<FAST>(v[r], v[r + 16], v[r + 32], v[r + 48], w[0], w[1], w[2], false);
     }
+}
+template <int SF, bool FAST>
+__device__ __forceinline__ void wpass2(cf32 (&v)[64], const WTw<SF>& T, const cf32* __restrict__ tw, int l) {
+    wpass2_s2<SF, FAST>(v, T, tw, l);
+    wpass2_s10<SF, FAST>(v, T, tw, l);
 }
 
 // The 64 x LPS transpose between the passes through the wave's buffer.
@@ -309,9 +327,55 @@ __device__ __forceinline__ void wdma(const DemodArgs& A, cf32* buf, unsigned f0,
     for (int h = 0; h < W::SPW; ++h) {
         const unsigned f = h ? f1 : f0, base = h ? base1 : base0;
         const cf32* src = A.iq + (unsigned long long)f * A.frame_samples + base + 2 * lane;
+        // four 1 KiB pieces per base: the instruction's immediate offset moves
+        // the source and the LDS destination alike (tools/ubench/glds_align)
 #pragma unroll
-        for (int r = 0; r < W::PPS; ++r)
-            __builtin_amdgcn_global_load_lds((g_void*)(src + 128 * r), (lds_void*)(buf + h * W::N + 128 * r), 16, 0, 0);
+        for (int r = 0; r < W::PPS; r += 4) {
+            g_void* g = (g_void*)(src + 128 * r);
+            lds_void* d = (lds_void*)(buf + h * W::N + 128 * r);
+            __builtin_amdgcn_global_load_lds(g, d, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(g, d, 16, 1024, 0);
+            __builtin_amdgcn_global_load_lds(g, d, 16, 2048, 0);
+            __builtin_amdgcn_global_load_lds(g, d, 16, 3072, 0);
+        }
+    }
+}
+
+// Keyed top two (see team_argmax2_keyed_first) merged over each symbol's
+// LPS lanes without LDS traffic: DPP exchanges inside every 16-lane row
+// (xor 1, xor 2, half mirror, mirror: each step pairs disjoint lane sets, so
+// every row lane ends with the row's top two), then the rows' results by
+// v_readlane as wave-uniform values.  Every lane of symbol h gets its top two.
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u32(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ void top2_add(unsigned& K1, unsigned& K2, unsigned o1, unsigned o2) {
+    K2 = med3_u32(K1, o1, K2 > o2 ? K2 : o2);
+    K1 = K1 > o1 ? K1 : o1;
+}
+template <int LPS>
+__device__ __forceinline__ void wave_top2_merge(unsigned k1, unsigned k2, int h, unsigned& K1, unsigned& K2) {
+    static_assert(LPS == 32 || LPS == 64, "one or two symbols per wave");
+    top2_add(k1, k2, dpp_u32<0xB1>(k1), dpp_u32<0xB1>(k2));    // quad_perm [1,0,3,2]
+    top2_add(k1, k2, dpp_u32<0x4E>(k1), dpp_u32<0x4E>(k2));    // quad_perm [2,3,0,1]
+    top2_add(k1, k2, dpp_u32<0x141>(k1), dpp_u32<0x141>(k2));  // row_half_mirror
+    top2_add(k1, k2, dpp_u32<0x140>(k1), dpp_u32<0x140>(k2));  // row_mirror
+    unsigned r1[4], r2[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        r1[r] = (unsigned)__builtin_amdgcn_readlane((int)k1, 16 * r);
+        r2[r] = (unsigned)__builtin_amdgcn_readlane((int)k2, 16 * r);
+    }
+    top2_add(r1[0], r2[0], r1[1], r2[1]);
+    top2_add(r1[2], r2[2], r1[3], r2[3]);
+    if constexpr (LPS == 64) {
+        top2_add(r1[0], r2[0], r1[2], r2[2]);
+        K1 = r1[0];
+        K2 = r2[0];
+    } else {
+        K1 = h ? r1[2] : r1[0];
+        K2 = h ? r2[2] : r2[0];
     }
 }
 
@@ -324,7 +388,8 @@ __device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F
 // flight at once; NaN when a sample is not finite (the frame then goes to
 // the exact re-run).  Same arithmetic as wave_maxabs.
 template <int SF, int MODE>
-__device__ __noinline__ float wscan2(const DemodArgs& A, unsigned f, const cf32* down, int lane) {
+__device__ __noinline__ float wscan2(KArgs ka, unsigned f, const cf32* down, int lane) {
+    const DemodArgs& A = kargs(ka);
     constexpr int N = 1 << SF;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     constexpr int U = 32;                 // float4 per lane per round
@@ -440,12 +505,13 @@ __device__ __forceinline__ UnitResult wunit_result(const cf32 (&v)[64], int h, i
 // KISS's exact transform and the detector outputs; .nan when a bin is NaN
 // (the frame then goes to the exact re-run, as in k_frames).
 template <int SF, int MODE>
-__device__ __noinline__ UnitResult west_unit(const DemodArgs& A, cf32* buf, const cf32* dnl, float scale,
+__device__ __noinline__ UnitResult west_unit(KArgs ka, cf32* buf, const cf32* dnl, float scale,
                                              bool live) {
     using W = WGeo<SF>;
     constexpr int N = W::N, LPS = W::LPS;
     constexpr bool M0 = (MODE & 3) == LPHY_MODE_DEMODULATE;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    const DemodArgs& A = kargs(ka);
     const int lane = threadIdx.x & 63, h = lane / LPS, l = lane % LPS;
     cf32 v[64];
     const int rb = (h * N + l) << 3;
@@ -500,31 +566,88 @@ __device__ __noinline__ WRot wrot(float rate, float scale) {
     return r;
 }
 
+// One unit's LDS-DMA: windows from samples b0 (symbol 0 of the unit) and b1
+// (symbol 1 at SF 11) of frame f; on = 0: no unit.
+struct WDma {
+    unsigned f, b0, b1;
+    int on;
+};
+
 // Frame end under the speculative normalisation (as k_frames' close): the
 // samples no symbol window covers are scanned, then the frame's true
 // max-abs confirms the two-symbol normalisation, sends the frame to the
-// exact re-run (NaN / inf), or marks it for k_wsettle.
+// exact re-run (NaN / inf), or settles it here.  Settling (the frame's
+// normalisation differs from the two-symbol prediction): the estimate
+// symbols are fetched again into the wave's buffer (once the next unit's
+// LDS-DMA `nd` has landed; it is issued again at the end) and re-run with
+// the exact scale
+// (KISS's arithmetic, as the estimate units); the symbols are kept when the
+// time shift is unchanged and every certified symbol's lead covers the
+// larger sample bound and the rate difference (settle_frames' rule, with
+// r the symbols' least certificate ratio), else the frame goes to k_post's
+// exact re-run.
 template <int SF, int MODE>
-__device__ __noinline__ void wclose(const DemodArgs& A, const cf32* dnl, unsigned f, int t_off, float mx01,
-                                    float m, float r, bool nan, bool open) {
-    constexpr int N = 1 << SF;
+__device__ __noinline__ void wclose(KArgs ka, cf32* buf, const cf32* dnl, unsigned f, float rate,
+                                    float scale, int t_off, float mx01, float m, float r, bool nan, bool open,
+                                    WDma nd) {
+    using W = WGeo<SF>;
+    constexpr int N = W::N, SPW = W::SPW;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    const DemodArgs& A = kargs(ka);
+    const int lane = threadIdx.x & 63;
     const unsigned S = (unsigned)A.total_syms;
     const unsigned cnt = DECH ? S * N : (unsigned)A.frame_samples;
     const unsigned end = covered_end(S, N, cnt, t_off);
     bool fbad = false;
     if (end < cnt) m = fmaxf(m, wave_range_maxabs<SF, MODE>(A, f, end, cnt, dnl, fbad));
-    if ((threadIdx.x & 63) == 0) {
-        const float mt = fmaxf(m, mx01);
-        const lphy_frame_meta mg = norm_meta(mx01, true, 0), me = norm_meta(mt, true, 0);
-        if (nan || fbad || !(mt <= 3.40282347e38f)) {
-            A.meta[f].status = kStatusFixup;
-        } else if (me.scale != mg.scale || me.normalised != mg.normalised) {
-            A.meta[f].cfo = mt;
-            A.meta[f].time_offset = r;
-            A.meta[f].status = open ? kStatusSettleRecheck : kStatusSettle;
+    const float mt = fmaxf(m, mx01);
+    const lphy_frame_meta mg = norm_meta(mx01, true, 0), me = norm_meta(mt, true, 0);
+    if (nan || fbad || !(mt <= 3.40282347e38f)) {
+        if (lane == 0) A.meta[f].status = kStatusFixup;
+        return;
+    }
+    if (me.scale == mg.scale && me.normalised == mg.normalised) return;
+    wait_vm0();  // the next unit's IQ has landed in the buffer
+    UnitResult ua{0, 0, 0.0f, 0.0f, 0}, ub = ua;
+#pragma unroll 1
+    for (int j = 0; j < W::NE; ++j) {
+        wdma<SF>(A, buf, f, SPW == 1 ? (unsigned)j * (unsigned)N : 0u, f, (unsigned)N, lane);
+        wait_vm0();
+        const UnitResult ur = west_unit<SF, MODE>(ka, buf, dnl, me.scale, true);
+        if constexpr (SPW == 1) {
+            if (j == 0) ua = ur;
+            else ub = ur;
+        } else {
+            ua.idx = __shfl(ur.idx, 0, 64);
+            ua.valid = __shfl(ur.valid, 0, 64);
+            ua.findex = __shfl(ur.findex, 0, 64);
+            ua.phase = __shfl(ur.phase, 0, 64);
+            ua.nan = __shfl(ur.nan, 0, 64);
+            ub.idx = __shfl(ur.idx, 32, 64);
+            ub.valid = __shfl(ur.valid, 32, 64);
+            ub.findex = __shfl(ur.findex, 32, 64);
+            ub.phase = __shfl(ur.phase, 32, 64);
+            ub.nan = __shfl(ur.nan, 32, 64);
         }
     }
+    lphy_frame_meta e = me;
+    EstFold fold;
+    if (ua.valid) fold.add(ua.idx, ua.findex, 0, ua.phase);
+    else fold.add(0, 0.0f, 0, 0.0f);
+    if (ub.valid) fold.add(ub.idx, ub.findex, 0, ub.phase);
+    else fold.add(0, 0.0f, 0, 0.0f);
+    fold.finish(e, 2, N, 1);
+    const float a = fmaxf(1.0f, mt * scale) * 1.0001f;
+    const float b1 = cert_bound<SF>(rate, rate * (float)t_off, 1.0f);
+    const float d = fabsf(e.rate - rate) * (1.0f + 4.0f * kU);
+    const float A1 = (float)N * 1.41421366f * 1.0001f;
+    const bool ok = !ua.nan && !ub.nan && e.t_off == t_off && t_off >= -N && t_off <= N &&
+                    r > 4.0f * a + 4.0f * d * (float)N * A1 * a / b1;
+    if (lane == 0) {
+        e.status = !ok ? kStatusFixup : (open ? kStatusRecheck : 0);
+        meta_put_est(&A.meta[f], e);
+    }
+    if (nd.on) wdma<SF>(A, buf, nd.f, nd.b0, nd.f, nd.b1, lane);
 }
 
 // Timing experiments only (-DLPHY_PROFILE_PHASES, tools/ubench): per-wave
@@ -598,6 +721,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     constexpr bool DN = (MODE & 3) != LPHY_MODE_LORA_DEMODULATE;  // down-chirp used
     const DemodArgs& A = P.A;
+    const KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
     __shared__ cf32 sbuf[W::WPB][W::BUF];
     __shared__ cf32 dnl[DN ? N : 1];
 
@@ -607,7 +731,9 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     }
     __syncthreads();  // the only workgroup barrier: waves are independent below
 
-    const int lane = tid & 63, wv = tid >> 6;
+    // wave index as a scalar: the schedule below is wave-uniform (SALU, no
+    // exec-mask branches) and the LDS-DMA destination needs no readfirstlane
+    const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int h = lane / LPS, l = lane % LPS;
     cf32* buf = sbuf[wv];
     const unsigned nframes = (unsigned)A.frames;
@@ -637,17 +763,27 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
         m.t_off = t;
         return sym_ctx(A, 0, s, true, N, m).base;
     };
-    auto dma_unit = [&](const WCursor& c) {
+    // the LDS-DMA of unit c: frame and window start of its symbol(s)
+    auto dma_plan = [&](const WCursor& c) {
+        WDma d{0u, 0u, 0u, 0};
         const int kd = sch.kind(c);
-        if (kd == kWDead) return;
-        const unsigned k = sch.frame(c), f = fglob(k);
+        if (kd == kWDead) return d;
+        d.f = fglob(sch.frame(c));
+        d.on = 1;
         if (kd == kWEst) {  // SF 12: symbol j; SF 11: symbols 0 and 1
-            wdma<SF>(A, buf, f, SPW == 1 ? c.j * (unsigned)N : 0u, f, (unsigned)N, lane);
+            d.b0 = SPW == 1 ? c.j * (unsigned)N : 0u;
+            d.b1 = (unsigned)N;
         } else {
-            const WFrame R = rec(k);
+            const WFrame R = rec(sch.frame(c));
             const unsigned s0 = SPW * c.j, s1 = (SPW == 2 && s0 + 1 < S) ? s0 + 1 : s0;
-            wdma<SF>(A, buf, f, wbase(s0, R.t_off), f, wbase(s1, R.t_off), lane);
+            d.b0 = wbase(s0, R.t_off);
+            d.b1 = wbase(s1, R.t_off);
         }
+        return d;
+    };
+    auto dma_unit = [&](const WCursor& c) {
+        const WDma d = dma_plan(c);
+        if (d.on) wdma<SF>(A, buf, d.f, d.b0, d.f, d.b1, lane);
     };
 
     // rotation of the frame in demodulation: Qr[b] = [scale] e^{j rate (l + LPS b)}
@@ -663,7 +799,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     WCursor cu = sch.first();
     WPH_DECL
     if constexpr (!M0) {
-        const float m = wscan2<SF, MODE>(A, fglob(0), dnl, lane);
+        const float m = wscan2<SF, MODE>(ka, fglob(0), dnl, lane);
         WFrame r = rec0;
         r.mx = m;
         rec0 = r;
@@ -700,26 +836,64 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             // staging: [exact dechirp,] certified rotation, from the LDS copy
             float amax = 0.0f;
             const int rb = (h * N + l) << 3;
+            // software-pipelined in chunks of 8 samples: chunk q + 1's LDS reads
+            // are issued before chunk q's arithmetic (sched barriers pin the
+            // order; a single wave per SIMD has no other wave to hide them)
+            cf32 xq[2][8], dq[2][8];
+            auto ld_chunk = [&](int q, cf32 (&xs)[8], cf32 (&ds)[8]) __attribute__((always_inline)) {
 #pragma unroll
-            for (int e = 0; e < 64; ++e) {
-                if ((e & 7) == 0) cfence();  // 8 samples' loads in flight at a time
-                const cf32 x = lds_ld(buf, rb + ((LPS * e) << 3));
-                cf32 p = x;
-                if constexpr (DECH) p = cmul(x, dnl[(c.base + (unsigned)(l + LPS * e)) & (N - 1)]);
-                amax = max3_abs(amax, p.x, p.y);
-                if constexpr (M0) p = cmul(p, dnl[l + LPS * e]);
-                // (a unit whose symbol is not demodulated transforms whatever
-                // its window holds; nothing of it is stored)
-                v[e] = cmul_fma(cmul_fma(p, Qr[e & 7]), Pr[e >> 3]);
+                for (int i = 0; i < 8; ++i) {
+                    const int e = 8 * q + i;
+#ifndef LPHY_ABLATE_W_STAGE  // timing experiments only
+                    xs[i] = lds_ld(buf, rb + ((LPS * e) << 3));
+#else
+                    xs[i] = cf32{(float)e, (float)l};
+#endif
+                    if constexpr (DECH) ds[i] = dnl[(c.base + (unsigned)(l + LPS * e)) & (N - 1)];
+                    if constexpr (M0) ds[i] = dnl[l + LPS * e];
+                }
+            };
+            ld_chunk(0, xq[0], dq[0]);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                if (q + 1 < 8) ld_chunk(q + 1, xq[(q + 1) & 1], dq[(q + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int e = 8 * q + i;
+                    const cf32 x = xq[q & 1][i];
+                    cf32 p = x;
+                    if constexpr (DECH) p = cmul(x, dq[q & 1][i]);
+                    amax = max3_abs(amax, p.x, p.y);
+                    if constexpr (M0) p = cmul(p, dq[q & 1][i]);
+                    // (a unit whose symbol is not demodulated transforms whatever
+                    // its window holds; nothing of it is stored)
+                    v[e] = cmul_fma(cmul_fma(p, Qr[i]), Pr[q]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
             }
             WPH(1);
             wpass1<SF, true>(v, ctw(A.tw));
             WPH(2);
+#ifndef LPHY_ABLATE_W_EXCH  // timing experiments only
             wexchange<SF>(v, buf, h, l);
+#endif
+#ifdef LPHY_W_LATE_DMA
+            // pass 2's first stage consumes the exchange reads as they land;
+            // then the buffer is free for the next unit's IQ
+            wpass2_s2<SF, true>(v, T, A.tw, l);
+            wait_lgkm0();
+            dma_unit(nx);
+            WPH(3);
+            wpass2_s10<SF, true>(v, T, A.tw, l);
+#else
             wait_lgkm0();  // the exchange reads are done: the buffer is free
+#ifndef LPHY_ABLATE_W_DMA  // timing experiments only
             dma_unit(nx);  // the next unit's IQ lands during pass 2
+#endif
             WPH(3);
             wpass2<SF, true>(v, T, A.tw, l);
+#endif
             WPH(4);
             // keyed top two over the half's bins l + LPS e (key: |X|^2 bits,
             // low 6 bits the element; see team_argmax2_keyed_first)
@@ -731,14 +905,8 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                 k2 = med3_u32(k1, k2, key);
                 k1 = k1 > key ? k1 : key;
             }
-            unsigned K1 = k1, K2 = k2;
-#pragma unroll
-            for (int off = 1; off < LPS; off <<= 1) {
-                const unsigned o1 = (unsigned)__shfl_xor((int)K1, off, 64);
-                const unsigned o2 = (unsigned)__shfl_xor((int)K2, off, 64);
-                K2 = med3_u32(K1, o1, K2 > o2 ? K2 : o2);
-                K1 = K1 > o1 ? K1 : o1;
-            }
+            unsigned K1, K2;
+            wave_top2_merge<LPS>(k1, k2, h, K1, K2);
             const unsigned long long bm = __ballot(k1 == K1);
             const unsigned long long hm = LPS == 64 ? bm : ((bm >> (32 * h)) & 0xffffffffull);
             ArgMax2 b2;
@@ -785,7 +953,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                 sp_mx = 0.0f;
                 sp_r = kBig;
                 sp_fl = 0u;
-                if (R.ok) wclose<SF, MODE>(A, dnl, f, R.t_off, R.mx, mm, rr, nan, open);
+                if (R.ok) wclose<SF, MODE>(ka, buf, dnl, f, R.rate, R.scale, R.t_off, R.mx, mm, rr, nan, open, dma_plan(nx));
             }
         } else {
             // estimate unit(s): KISS's arithmetic, bit for bit (LoRaDemod.cpp:80-136,
@@ -796,7 +964,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             nm.have_sync = 1;
             if constexpr (!M0) nm = norm_meta_hot(R0.mx, true, A.no_scratch);
             const bool live = nm.status == 0;
-            const UnitResult ur = west_unit<SF, MODE>(A, buf, dnl, nm.scale, live);
+            const UnitResult ur = west_unit<SF, MODE>(ka, buf, dnl, nm.scale, live);
             bool fold_now = true;
             UnitResult ua = ur, ub = ur;
             if constexpr (SPW == 1) {
@@ -845,7 +1013,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             if (sch.kind(nx) == kWEst && nx.j == 0 && nx.phase == 2) {
                 const unsigned kn = sch.frame(nx);
                 WFrame r = rec(kn);
-                r.mx = wscan2<SF, MODE>(A, fglob(kn), dnl, lane);
+                r.mx = wscan2<SF, MODE>(ka, fglob(kn), dnl, lane);
                 set_rec(kn, r);
             }
         }
@@ -853,81 +1021,4 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     }
     WPH(7);
     WPH_FLUSH(A)
-}
-
-// Frames k_wave closed with a normalisation its two-symbol scan did not
-// predict (status kStatusSettle[Recheck], record {cfo: the frame's max-abs,
-// time_offset: the symbols' least certificate ratio}): one wavefront per
-// frame re-runs the two estimate FFTs with the exact scale (KISS's
-// arithmetic, as the estimate units) and keeps the symbols when the time
-// shift is unchanged and every certified symbol's lead covers the larger
-// sample bound and the rate difference (settle_frames' rule); else the frame
-// goes to k_post's exact re-run.  Other frames return at once.
-template <int SF, int MODE>
-__global__ __launch_bounds__(256, 1) void k_wsettle(DemodArgs A) {
-    using W = WGeo<SF>;
-    constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
-    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
-    __shared__ cf32 sbuf[W::WPB][W::BUF];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const unsigned long long f = (unsigned long long)blockIdx.x * W::WPB + wv;
-    if (f >= A.frames) return;
-    const lphy_frame_meta sm = A.meta[f];
-    if (!(sm.status == kStatusSettle || sm.status == kStatusSettleRecheck)) return;
-    const int h = lane / LPS, l = lane % LPS;
-    const lphy_frame_meta e0 = norm_meta(sm.cfo, true, 0);
-    WTw<SF> T;
-    T.load(A.tw, l);
-    const cf32* fr = A.iq + f * A.frame_samples;
-    UnitResult ua{0, 0, 0.0f, 0.0f, 0}, ub = ua;
-#pragma unroll 1
-    for (int j = 0; j < W::NE; ++j) {
-        const unsigned sy = SPW == 1 ? (unsigned)j : (unsigned)h;
-        cf32 v[64];
-#pragma unroll
-        for (int e = 0; e < 64; ++e) {
-            if ((e & 15) == 0) cfence();
-            const int i = l + LPS * e;
-            cf32 x = fr[sy * N + i];
-            if constexpr (DECH) x = cmul(x, A.down[i]);
-            v[e] = cscale(x, e0.scale);
-        }
-        wpass1<SF, false>(v, ctw(A.tw));
-        wexchange<SF>(v, sbuf[wv], h, l);
-        wpass2<SF, false>(v, T, A.tw, l);
-        const UnitResult ur = wunit_result<SF>(v, h, l, lane);
-        if constexpr (SPW == 1) {
-            if (j == 0) ua = ur;
-            else ub = ur;
-        } else {
-            ua.idx = __shfl(ur.idx, 0, 64);
-            ua.valid = __shfl(ur.valid, 0, 64);
-            ua.findex = __shfl(ur.findex, 0, 64);
-            ua.phase = __shfl(ur.phase, 0, 64);
-            ub.idx = __shfl(ur.idx, 32, 64);
-            ub.valid = __shfl(ur.valid, 32, 64);
-            ub.findex = __shfl(ur.findex, 32, 64);
-            ub.phase = __shfl(ur.phase, 32, 64);
-        }
-    }
-    lphy_frame_meta e = e0;
-    EstFold fold;
-    if (ua.valid) fold.add(ua.idx, ua.findex, 0, ua.phase);
-    else fold.add(0, 0.0f, 0, 0.0f);
-    if (ub.valid) fold.add(ub.idx, ub.findex, 0, ub.phase);
-    else fold.add(0, 0.0f, 0, 0.0f);
-    fold.finish(e, 2, N, 1);
-    const float a = fmaxf(1.0f, sm.cfo * sm.scale) * 1.0001f;
-    const float b1 = cert_bound<SF>(sm.rate, sm.rate * (float)sm.t_off, 1.0f);
-    const float d = fabsf(e.rate - sm.rate) * (1.0f + 4.0f * kU);
-    const float A1 = (float)N * 1.41421366f * 1.0001f;
-    const bool ok = e.t_off == sm.t_off && sm.t_off >= -N && sm.t_off <= N &&
-                    sm.time_offset > 4.0f * a + 4.0f * d * (float)N * A1 * a / b1;
-    if (lane == 0) {
-        lphy_frame_meta r = e;
-        r.sw0 = sm.sw0;
-        r.sw1 = sm.sw1;
-        r.status = !ok ? kStatusFixup : (sm.status == kStatusSettleRecheck ? kStatusRecheck : 0);
-        A.meta[f] = r;
-    }
 }
