@@ -122,6 +122,14 @@ __device__ __forceinline__ cf32 cmul_fma(cf32 a, cf32 b) {
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_lo:[0,0,1]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
     return r;
 }
+// The same with a wave-uniform b (a compile-time twiddle): b is an SGPR-pair
+// operand of both instructions, no copy to a VGPR.
+__device__ __forceinline__ cf32 cmul_fma_s(cf32 a, cf32 b) {
+    const cf32 t = a.yy * b.yx;
+    cf32 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_lo:[0,0,1]" : "=v"(r) : "v"(a), "s"(b), "v"(t));
+    return r;
+}
 __device__ __forceinline__ cf32 cadd(cf32 a, cf32 b) { return a + b; }
 __device__ __forceinline__ cf32 csub(cf32 a, cf32 b) { return a - b; }
 __device__ __forceinline__ cf32 cscale(cf32 a, float s) { return a * s; }

@@ -153,21 +153,70 @@ __device__ __forceinline__ cf32 root64(int j) {
     return cf32{c.re, c.im};
 }
 
-template <bool FAST>
+// x * root64(j) on the fast path from nine base constants: root64(j) =
+// (-i)^q root64(r) (j = 16 q + r), and for r > 8 root64(r) = (-B.y, -B.x)
+// with B = root64(16 - r); so w = (sx B[cx], sy B[1 - cx]) for B = root64(r'),
+// r' <= 8, and the swap and signs go into the op_sel / neg modifiers of
+// cmul_fma's two instructions (the constants then fit the SGPR budget; the
+// roots are the same correctly rounded values).
+// (two statements: hipcc pads the dependent pair itself, and may schedule
+// other work between them)
+#define LPHY_CMR(CX, CY, NX, NY)                                                                  \
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1," #CY "] op_sel_hi:[1," #CX "] neg_lo:[0," #NY          \
+        "] neg_hi:[0," #NX "]"                                                                      \
+        : "=v"(t)                                                                                   \
+        : "v"(a), "s"(B));                                                                          \
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0," #CX ",0] op_sel_hi:[0," #CY ",1] neg_lo:[0," #NX \
+        ",1] neg_hi:[0," #NY ",0]"                                                                  \
+        : "=v"(r)                                                                                   \
+        : "v"(a), "s"(B), "v"(t))
+__device__ __forceinline__ cf32 cmul_root(cf32 a, int j) {
+    j &= 63;
+    if (j == 0) return a;
+    const int q = j >> 4, r0 = j & 15;
+    const int rb = r0 <= 8 ? r0 : 16 - r0;
+    int cx = r0 <= 8 ? 0 : 1, cy = 1 - cx;
+    int sx = r0 <= 8 ? 0 : 1, sy = sx;  // 1: negated
+    for (int k = 0; k < q; ++k) {      // w <- -i w: (x, y) -> (y, -x)
+        const int c = cx, n = sx;
+        cx = cy;
+        sx = sy;
+        cy = c;
+        sy = n ^ 1;
+    }
+    const cf32 B = root64(rb);
+    cf32 r, t;
+    const int code = cx * 4 + sx * 2 + sy;
+    switch (code) {
+        case 0: LPHY_CMR(0, 1, 0, 0); break;
+        case 1: LPHY_CMR(0, 1, 0, 1); break;
+        case 2: LPHY_CMR(0, 1, 1, 0); break;
+        case 3: LPHY_CMR(0, 1, 1, 1); break;
+        case 4: LPHY_CMR(1, 0, 0, 0); break;
+        case 5: LPHY_CMR(1, 0, 0, 1); break;
+        case 6: LPHY_CMR(1, 0, 1, 0); break;
+        default: LPHY_CMR(1, 0, 1, 1); break;
+    }
+    return r;
+}
+#undef LPHY_CMR
+
+template <bool FAST, bool UNI = false>
 __device__ __forceinline__ cf32 wmul(cf32 x, cf32 t) {
-    if constexpr (FAST) return cmul_fma(x, t);
+    if constexpr (FAST && UNI) return cmul_fma_s(x, t);
+    else if constexpr (FAST) return cmul_fma(x, t);
     else return cmul(x, t);
 }
 
 // kf_bfly4 / kf_bfly2 (kissfft.hh:155-185) on registers; `one` (constant
 // after unrolling): every twiddle is tw[0] = (1, 0), skipped on the fast
 // path (magnitudes unchanged, see pass_butterflies' TRIV).
-template <bool FAST>
+template <bool FAST, bool UNI = false>
 __device__ __forceinline__ void wbfly4(cf32& x0, cf32& x1, cf32& x2, cf32& x3, cf32 w1, cf32 w2, cf32 w3,
                                        bool one) {
-    const cf32 s0 = (FAST && one) ? x1 : wmul<FAST>(x1, w1);
-    const cf32 s1 = (FAST && one) ? x2 : wmul<FAST>(x2, w2);
-    const cf32 s2 = (FAST && one) ? x3 : wmul<FAST>(x3, w3);
+    const cf32 s0 = (FAST && one) ? x1 : wmul<FAST, UNI>(x1, w1);
+    const cf32 s1 = (FAST && one) ? x2 : wmul<FAST, UNI>(x2, w2);
+    const cf32 s2 = (FAST && one) ? x3 : wmul<FAST, UNI>(x3, w3);
     const cf32 s5 = csub(x0, s1);
     const cf32 a0 = cadd(x0, s1);
     const cf32 s3 = cadd(s0, s2);
@@ -177,9 +226,23 @@ __device__ __forceinline__ void wbfly4(cf32& x0, cf32& x1, cf32& x2, cf32& x3, c
     x1 = cadd_rot(s5, s4);
     x3 = csub_rot(s5, s4);
 }
-template <bool FAST>
+// wbfly4 on the fast path with twiddles root64(j1), root64(j2), root64(j3)
+__device__ __forceinline__ void wbfly4r(cf32& x0, cf32& x1, cf32& x2, cf32& x3, int j1, int j2, int j3) {
+    const cf32 s0 = cmul_root(x1, j1);
+    const cf32 s1 = cmul_root(x2, j2);
+    const cf32 s2 = cmul_root(x3, j3);
+    const cf32 s5 = csub(x0, s1);
+    const cf32 a0 = cadd(x0, s1);
+    const cf32 s3 = cadd(s0, s2);
+    const cf32 s4 = csub(s0, s2);
+    x2 = csub(a0, s3);
+    x0 = cadd(a0, s3);
+    x1 = cadd_rot(s5, s4);
+    x3 = csub_rot(s5, s4);
+}
+template <bool FAST, bool UNI = false>
 __device__ __forceinline__ void wbfly2(cf32& x0, cf32& x1, cf32 w, bool one) {
-    const cf32 t = (FAST && one) ? x1 : wmul<FAST>(x1, w);
+    const cf32 t = (FAST && one) ? x1 : wmul<FAST, UNI>(x1, w);
     x1 = csub(x0, t);
     x0 = cadd(x0, t);
 }
@@ -213,15 +276,28 @@ __device__ __forceinline__ void wpass1(cf32 (&v)[64], ctw_t* tab) {
 #pragma unroll
             for (int k = 0; k < W::M4; ++k) {
                 const int b0 = blk * W::M3 + k;
-                wbfly4<FAST>(v[W::reg1(g, b0)], v[W::reg1(g, b0 + W::M4)], v[W::reg1(g, b0 + 2 * W::M4)],
-                             v[W::reg1(g, b0 + 3 * W::M4)], tw(256 * k), tw(512 * k), tw(768 * k), k == 0);
+                if constexpr (FAST) {
+                    constexpr int D = W::N / 64;  // tw[k'] = root64(k' / D)
+                    wbfly4r(v[W::reg1(g, b0)], v[W::reg1(g, b0 + W::M4)], v[W::reg1(g, b0 + 2 * W::M4)],
+                            v[W::reg1(g, b0 + 3 * W::M4)], 256 * k / D, 512 * k / D, 768 * k / D);
+                } else {
+                    wbfly4<FAST>(v[W::reg1(g, b0)], v[W::reg1(g, b0 + W::M4)], v[W::reg1(g, b0 + 2 * W::M4)],
+                                 v[W::reg1(g, b0 + 3 * W::M4)], tw(256 * k), tw(512 * k), tw(768 * k), k == 0);
+                }
             }
         }
         // stage 3: radix 4, M = M3, twiddle stride 64
 #pragma unroll
-        for (int k = 0; k < W::M3; ++k)
-            wbfly4<FAST>(v[W::reg1(g, k)], v[W::reg1(g, k + W::M3)], v[W::reg1(g, k + 2 * W::M3)],
-                         v[W::reg1(g, k + 3 * W::M3)], tw(64 * k), tw(128 * k), tw(192 * k), k == 0);
+        for (int k = 0; k < W::M3; ++k) {
+            if constexpr (FAST) {
+                constexpr int D = W::N / 64;
+                wbfly4r(v[W::reg1(g, k)], v[W::reg1(g, k + W::M3)], v[W::reg1(g, k + 2 * W::M3)],
+                        v[W::reg1(g, k + 3 * W::M3)], 64 * k / D, 128 * k / D, 192 * k / D);
+            } else {
+                wbfly4<FAST>(v[W::reg1(g, k)], v[W::reg1(g, k + W::M3)], v[W::reg1(g, k + 2 * W::M3)],
+                             v[W::reg1(g, k + 3 * W::M3)], tw(64 * k), tw(128 * k), tw(192 * k), k == 0);
+            }
+        }
     }
 }
 
@@ -263,7 +339,7 @@ __device__ __forceinline__ void wpass2_s10(cf32 (&v)[64], const WTw<SF>& T, cons
         cf32 w[3];
 #pragma unroll
         for (int q = 1; q <= 3; ++q) {
-            if constexpr (FAST) w[q - 1] = r == 0 ? T.t1[q - 1] : cmul_fma(T.t1[q - 1], root64(4 * r * q));
+            if constexpr (FAST) w[q - 1] = r == 0 ? T.t1[q - 1] : cmul_root(T.t1[q - 1], 4 * r * q);
             else w[q - 1] = tw[4 * (l + W::LPS * r) * q];
         }
 #pragma unroll
@@ -278,7 +354,7 @@ __device__ __forceinline__ void wpass2_s10(cf32 (&v)[64], const WTw<SF>& T, cons
         cf32 w[3];
 #pragma unroll
         for (int q = 1; q <= 3; ++q) {
-            if constexpr (FAST) w[q - 1] = r == 0 ? T.t0[q - 1] : cmul_fma(T.t0[q - 1], root64(r * q));
+            if constexpr (FAST) w[q - 1] = r == 0 ? T.t0[q - 1] : cmul_root(T.t0[q - 1], r * q);
             else w[q - 1] = tw[(l + W::LPS * r) * q];
         }
         wbfly4<FAST>(v[r], v[r + 16], v[r + 32], v[r + 48], w[0], w[1], w[2], false);
@@ -722,8 +798,11 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     constexpr bool DN = (MODE & 3) != LPHY_MODE_LORA_DEMODULATE;  // down-chirp used
     const DemodArgs& A = P.A;
     const KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
-    __shared__ cf32 sbuf[W::WPB][W::BUF];
-    __shared__ cf32 dnl[DN ? N : 1];
+    // one LDS block: the down-chirp at offset 0 (its wrapped index is then
+    // the byte address itself), the waves' buffers after it
+    __shared__ cf32 lds_all[(DN ? N : 0) + W::WPB * W::BUF];
+    cf32* const dnl = lds_all;
+    cf32 (*const sbuf)[W::BUF] = reinterpret_cast<cf32 (*)[W::BUF]>(lds_all + (DN ? N : 0));
 
     const int tid = threadIdx.x;
     if constexpr (DN) {
@@ -840,6 +919,9 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             // are issued before chunk q's arithmetic (sched barriers pin the
             // order; a single wave per SIMD has no other wave to hide them)
             cf32 xq[2][8], dq[2][8];
+            // byte address of the down-chirp entry of element 0; element e's
+            // is (d0 + 8 LPS e) mod 8 N (mode 2: the window's own chirp indices)
+            const unsigned d0 = ((c.base + (unsigned)l) & (unsigned)(N - 1)) << 3;
             auto ld_chunk = [&](int q, cf32 (&xs)[8], cf32 (&ds)[8]) __attribute__((always_inline)) {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
@@ -849,7 +931,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
 #else
                     xs[i] = cf32{(float)e, (float)l};
 #endif
-                    if constexpr (DECH) ds[i] = dnl[(c.base + (unsigned)(l + LPS * e)) & (N - 1)];
+                    if constexpr (DECH) ds[i] = lds_ld(dnl, (int)((d0 + (unsigned)((LPS * e) << 3)) & (unsigned)(8 * N - 1)));
                     if constexpr (M0) ds[i] = dnl[l + LPS * e];
                 }
             };
@@ -900,8 +982,10 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             unsigned k1 = 0u, k2 = 0u;
 #pragma unroll
             for (int e = 0; e < 64; ++e) {
-                const cf32 sq = v[e] * v[e];
-                const unsigned key = (__float_as_uint(sq.x + sq.y) & ~63u) | (unsigned)e;
+                // |X|^2 = fma(x, x, fl(y y)): within 2 u, inside cert_gap's 8 u;
+                // scalar f32 ops (no packed-f32 dependency pad)
+                const float m2 = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
+                const unsigned key = (__float_as_uint(m2) & ~63u) | (unsigned)e;
                 k2 = med3_u32(k1, k2, key);
                 k1 = k1 > key ? k1 : key;
             }
