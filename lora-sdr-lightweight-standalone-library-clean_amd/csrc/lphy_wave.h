@@ -106,6 +106,7 @@ __device__ __forceinline__ ctw_t* ctw(const cf32* p) { return (ctw_t*)p; }
 // every field is a scalar load (lgkmcnt).  P is k_wave's only argument, at
 // offset 0 of the segment.
 typedef const __attribute__((address_space(4))) FrameArgs* KArgs;
+typedef __attribute__((address_space(3))) cf32 lds_cf32;  // LDS pointers across calls
 __device__ __forceinline__ const DemodArgs& kargs(KArgs k) { return ((const FrameArgs*)k)->A; }
 
 // Compiler-only fence: memory operations are not moved across it, so the
@@ -456,6 +457,23 @@ __device__ __forceinline__ void wave_top2_merge(unsigned k1, unsigned k2, int h,
 }
 
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }   // vmcnt(0)
+
+// LDS-DMA of the KISS twiddle table (N complex) into the wave's buffer.
+template <int SF>
+__device__ __forceinline__ void wdma_table(const cf32* tw, cf32* buf, int lane) {
+    using W = WGeo<SF>;
+    typedef __attribute__((address_space(3))) void lds_void;
+    typedef __attribute__((address_space(1))) const void g_void;
+#pragma unroll
+    for (int r = 0; r < W::PPS; r += 4) {
+        g_void* g = (g_void*)(tw + 128 * r + 2 * lane);
+        lds_void* d = (lds_void*)(buf + 128 * r);
+        __builtin_amdgcn_global_load_lds(g, d, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(g, d, 16, 1024, 0);
+        __builtin_amdgcn_global_load_lds(g, d, 16, 2048, 0);
+        __builtin_amdgcn_global_load_lds(g, d, 16, 3072, 0);
+    }
+}
 __device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); } // lgkmcnt(0)
 
 // Max-abs of the frame's two estimate symbols (samples [0, 2N)), the
@@ -581,13 +599,15 @@ __device__ __forceinline__ UnitResult wunit_result(const cf32 (&v)[64], int h, i
 // KISS's exact transform and the detector outputs; .nan when a bin is NaN
 // (the frame then goes to the exact re-run, as in k_frames).
 template <int SF, int MODE>
-__device__ __noinline__ UnitResult west_unit(KArgs ka, cf32* buf, const cf32* dnl, float scale,
+__device__ __noinline__ UnitResult west_unit(KArgs ka, lds_cf32* lbuf, const lds_cf32* ldnl, float scale,
                                              bool live) {
     using W = WGeo<SF>;
     constexpr int N = W::N, LPS = W::LPS;
     constexpr bool M0 = (MODE & 3) == LPHY_MODE_DEMODULATE;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     const DemodArgs& A = kargs(ka);
+    cf32* const buf = (cf32*)lbuf;  // LDS (the cast keeps the address space known)
+    const cf32* const dnl = (const cf32*)ldnl;
     const int lane = threadIdx.x & 63, h = lane / LPS, l = lane % LPS;
     cf32 v[64];
     const int rb = (h * N + l) << 3;
@@ -602,7 +622,12 @@ __device__ __noinline__ UnitResult west_unit(KArgs ka, cf32* buf, const cf32* dn
     const WTw<SF> T{};  // unused by the exact pass
     wpass1<SF, false>(v, ctw(A.tw));
     wexchange<SF>(v, buf, h, l);
-    wpass2<SF, false>(v, T, A.tw, l);
+    // pass 2's per-lane twiddles from an LDS copy of the KISS table: one
+    // LDS-DMA round trip instead of one global round trip per butterfly group
+    wait_lgkm0();  // the exchange reads are done: the buffer is free
+    wdma_table<SF>(A.tw, buf, lane);
+    wait_vm0();
+    wpass2<SF, false>(v, T, buf, l);
     float sumsq = 0.0f;
 #pragma unroll
     for (int e = 0; e < 64; ++e) {
@@ -663,13 +688,15 @@ struct WDma {
 // r the symbols' least certificate ratio), else the frame goes to k_post's
 // exact re-run.
 template <int SF, int MODE>
-__device__ __noinline__ void wclose(KArgs ka, cf32* buf, const cf32* dnl, unsigned f, float rate,
+__device__ __noinline__ void wclose(KArgs ka, lds_cf32* lbuf, const lds_cf32* ldnl, unsigned f, float rate,
                                     float scale, int t_off, float mx01, float m, float r, bool nan, bool open,
                                     WDma nd) {
     using W = WGeo<SF>;
     constexpr int N = W::N, SPW = W::SPW;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     const DemodArgs& A = kargs(ka);
+    cf32* const buf = (cf32*)lbuf;
+    const cf32* const dnl = (const cf32*)ldnl;
     const int lane = threadIdx.x & 63;
     const unsigned S = (unsigned)A.total_syms;
     const unsigned cnt = DECH ? S * N : (unsigned)A.frame_samples;
@@ -689,7 +716,7 @@ __device__ __noinline__ void wclose(KArgs ka, cf32* buf, const cf32* dnl, unsign
     for (int j = 0; j < W::NE; ++j) {
         wdma<SF>(A, buf, f, SPW == 1 ? (unsigned)j * (unsigned)N : 0u, f, (unsigned)N, lane);
         wait_vm0();
-        const UnitResult ur = west_unit<SF, MODE>(ka, buf, dnl, me.scale, true);
+        const UnitResult ur = west_unit<SF, MODE>(ka, lbuf, ldnl, me.scale, true);
         if constexpr (SPW == 1) {
             if (j == 0) ua = ur;
             else ub = ur;
@@ -889,7 +916,9 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
         const unsigned k = sch.frame(cu), f = fglob(k);
         cf32 v[64];
         WPH(7);
+#ifndef LPHY_ABLATE_W_VMWAIT  // timing experiments only
         wait_vm0();  // this unit's IQ has landed
+#endif
         WPH(0);
         if (sch.kind(cu) == kWSym) {
             const WFrame R = rec(k);
@@ -918,7 +947,11 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             // software-pipelined in chunks of 8 samples: chunk q + 1's LDS reads
             // are issued before chunk q's arithmetic (sched barriers pin the
             // order; a single wave per SIMD has no other wave to hide them)
-            cf32 xq[2][8], dq[2][8];
+#ifndef LPHY_W_STAGE_DEPTH
+#define LPHY_W_STAGE_DEPTH 1
+#endif
+            constexpr int SD = LPHY_W_STAGE_DEPTH, SB = SD + 1;  // chunks in flight, buffers
+            cf32 xq[SB][8], dq[SB][8];
             // byte address of the down-chirp entry of element 0; element e's
             // is (d0 + 8 LPS e) mod 8 N (mode 2: the window's own chirp indices)
             const unsigned d0 = ((c.base + (unsigned)l) & (unsigned)(N - 1)) << 3;
@@ -935,19 +968,20 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                     if constexpr (M0) ds[i] = dnl[l + LPS * e];
                 }
             };
-            ld_chunk(0, xq[0], dq[0]);
+#pragma unroll
+            for (int q = 0; q < SD; ++q) ld_chunk(q, xq[q], dq[q]);
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                if (q + 1 < 8) ld_chunk(q + 1, xq[(q + 1) & 1], dq[(q + 1) & 1]);
+                if (q + SD < 8) ld_chunk(q + SD, xq[(q + SD) % SB], dq[(q + SD) % SB]);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     const int e = 8 * q + i;
-                    const cf32 x = xq[q & 1][i];
+                    const cf32 x = xq[q % SB][i];
                     cf32 p = x;
-                    if constexpr (DECH) p = cmul(x, dq[q & 1][i]);
+                    if constexpr (DECH) p = cmul(x, dq[q % SB][i]);
                     amax = max3_abs(amax, p.x, p.y);
-                    if constexpr (M0) p = cmul(p, dq[q & 1][i]);
+                    if constexpr (M0) p = cmul(p, dq[q % SB][i]);
                     // (a unit whose symbol is not demodulated transforms whatever
                     // its window holds; nothing of it is stored)
                     v[e] = cmul_fma(cmul_fma(p, Qr[i]), Pr[q]);
@@ -1037,7 +1071,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                 sp_mx = 0.0f;
                 sp_r = kBig;
                 sp_fl = 0u;
-                if (R.ok) wclose<SF, MODE>(ka, buf, dnl, f, R.rate, R.scale, R.t_off, R.mx, mm, rr, nan, open, dma_plan(nx));
+                if (R.ok) wclose<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, f, R.rate, R.scale, R.t_off, R.mx, mm, rr, nan, open, dma_plan(nx));
             }
         } else {
             // estimate unit(s): KISS's arithmetic, bit for bit (LoRaDemod.cpp:80-136,
@@ -1048,7 +1082,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             nm.have_sync = 1;
             if constexpr (!M0) nm = norm_meta_hot(R0.mx, true, A.no_scratch);
             const bool live = nm.status == 0;
-            const UnitResult ur = west_unit<SF, MODE>(ka, buf, dnl, nm.scale, live);
+            const UnitResult ur = west_unit<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, nm.scale, live);
             bool fold_now = true;
             UnitResult ua = ur, ub = ur;
             if constexpr (SPW == 1) {
