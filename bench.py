@@ -319,8 +319,14 @@ def write_perf_csv(path: str, run_id: str, rows: list) -> None:
 
 
 def frames_fused(sf: int) -> bool:
-    """Whether the bench frame shape takes the fused k_frames launch."""
-    return sf <= 10 and os.environ.get("LPHY_FUSED", "1") != "0"
+    """Whether the bench frame shape takes a fused launch (k_frames for
+    SF <= 10, k_wave for SF 11-12)."""
+    return os.environ.get("LPHY_FUSED", "1") != "0"
+
+
+def fused_kernel(sf: int) -> str:
+    """Name of the fused launch's kernel (as the PMC summaries key it)."""
+    return f"k_frames<{sf}>" if sf <= 10 else f"k_wave<{sf}>"
 
 
 def measured_traffic(kernel: str, frames: int):
@@ -476,10 +482,11 @@ def main():
     st = wl.stage_times(mode_b)
 
     N = wl.N
-    # dominant kernel = the fused k_frames launch: algorithmic bytes = every
-    # IQ sample once + one u16 per data symbol + the 32-B frame record
-    # (its own max-abs pre-scan re-reads the frame, which the
-    # PMC traffic below shows)
+    # dominant kernel = the fused launch (k_frames up to SF 10, k_wave at
+    # SF 11-12): algorithmic bytes = every IQ sample once + one u16 per data
+    # symbol + the 32-B frame record (the two-symbol scans and the
+    # settled frames' estimate re-reads are extra traffic, which the PMC
+    # summary below shows)
     fused = frames_fused(args.sf)
     kern_bytes = frames * (wl.fs * 8 + DATA_SYMS * 2 + (32 if fused else 0))
     # the fused launch timed live in the timed region (k_frames + its fix-up
@@ -487,7 +494,7 @@ def main():
     kern_ms = live_kernel_ms if fused else st["unfused_symbols"]
     achieved = kern_bytes / (kern_ms * 1e-3) / 1e9
     step_gbps = frames * DATA_SYMS * bytes_per_data_symbol(N) / (ms * 1e-3) / 1e9
-    traffic = measured_traffic(f"k_frames<{args.sf}>" if fused else f"k_demod<{args.sf}>", frames)
+    traffic = measured_traffic(fused_kernel(args.sf) if fused else f"k_demod<{args.sf}>", frames)
 
     extra = {}
     if not args.no_mode_a:
@@ -549,7 +556,7 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic["bytes"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
-                         "kernel": f"k_frames<{args.sf}>" if fused else f"k_demod<{args.sf}>",
+                         "kernel": fused_kernel(args.sf) if fused else f"k_demod<{args.sf}>",
                          "bytes_per_launch": kern_bytes,
                          "avg_launch_ms": kern_ms,
                          "timing": "HIP events around each timed step's fused launch (+ its fix-up)"
