@@ -129,12 +129,15 @@ size_t lphy_hip_syms_per_frame(const lphy_hip_ctx* ctx, size_t frame_samples,
  * Limits: frames * (frame_samples / (N*osr)) < 2^32 symbols per call and
  * frame_samples < 2^31 (32-bit symbol bookkeeping in the kernels): larger
  * batches give -ERANGE; split them across calls.
- * Memory: the context holds only constant tables.  Per-call device scratch
- * (SF 11-12 speculation records, 16 B per frame) is taken from the
- * stream-ordered pool on `stream` and released in stream order, so calls on
- * different streams of one context never share it.  Unlike the reference
- * (API_SPEC.md:11-12, no allocation after init) a call may therefore
- * allocate; see INTEGRATION.md. */
+ * Memory: the context holds only constant tables.  The fused launches
+ * (k_frames up to SF 10, k_wave at SF 11-12: osr 1, no window, modes 1/2
+ * with the speculative normalisation or mode 0) allocate nothing.  The
+ * SF 11-12 separate launches (LPHY_F_UNFUSED, osr > 1, a window,
+ * LPHY_F_EXACT_ROTATION) take per-call speculation records (16 B per frame)
+ * from the stream-ordered pool on `stream`, released in stream order, so
+ * calls on different streams of one context never share them.  Unlike the
+ * reference (API_SPEC.md:11-12, no allocation after init) such a call may
+ * therefore allocate; see INTEGRATION.md. */
 int lphy_hip_demod_batch(lphy_hip_ctx* ctx, const float* d_iq, size_t frames,
                          size_t frame_samples, uint16_t* d_syms,
                          uint8_t* d_bytes, lphy_frame_meta* d_meta, int mode,
