@@ -230,12 +230,15 @@ class Demodulator:
 
     # --- streaming ingestion (lphy_hip_demod_stream) --------------------
     def demod_stream(self, fd: int, frame_samples: int, mode: int, flags: int = 0,
-                     chunk_frames: int = 4096, max_frames: int = 0, capacity: int = 0):
+                     chunk_frames: int = 0, max_frames: int = 0, capacity: int = 0):
         """Demodulate the float32 I/Q frames read from `fd` until EOF or
         max_frames.  The result arrays hold `capacity` frames (default:
         max_frames); at most min(max_frames, capacity) frames are read.
-        Returns (symbols, payload, meta, tail_bytes) for the whole frames
-        read."""
+        chunk_frames = 0 picks ~32 MiB chunks (three are pinned per call; in
+        tools/stream_bench.py smaller chunks streamed faster).  Returns
+        (symbols, payload, meta, tail_bytes) for the whole frames read."""
+        if chunk_frames <= 0:
+            chunk_frames = max(1, (32 << 20) // (frame_samples * 8))
         cap = capacity or max_frames
         if cap <= 0:
             raise ValueError("capacity or max_frames required")
