@@ -319,14 +319,16 @@ def write_perf_csv(path: str, run_id: str, rows: list) -> None:
 
 
 def frames_fused(sf: int) -> bool:
-    """Whether the bench frame shape takes a fused launch (k_frames for
-    SF <= 10, k_wave for SF 11-12)."""
+    """Whether the bench frame shape takes a fused launch (k_frames up to
+    SF 8, k_wave from SF 9)."""
     return os.environ.get("LPHY_FUSED", "1") != "0"
 
 
 def fused_kernel(sf: int) -> str:
-    """Name of the fused launch's kernel (as the PMC summaries key it)."""
-    return f"k_frames<{sf}>" if sf <= 10 else f"k_wave<{sf}>"
+    """Name of the fused launch's kernel (as the PMC summaries key it):
+    k_frames up to SF 8, k_wave from SF 9 (LPHY_WAVE_MIN_SF moves it)."""
+    lo = int(os.environ.get("LPHY_WAVE_MIN_SF", "9"))
+    return f"k_frames<{sf}>" if sf < max(9, min(lo, 13)) else f"k_wave<{sf}>"
 
 
 def measured_traffic(kernel: str, frames: int):
@@ -482,8 +484,8 @@ def main():
     st = wl.stage_times(mode_b)
 
     N = wl.N
-    # dominant kernel = the fused launch (k_frames up to SF 10, k_wave at
-    # SF 11-12): algorithmic bytes = every IQ sample once + one u16 per data
+    # dominant kernel = the fused launch (k_frames up to SF 8, k_wave from
+    # SF 9): algorithmic bytes = every IQ sample once + one u16 per data
     # symbol + the 32-B frame record (the two-symbol scans and the
     # settled frames' estimate re-reads are extra traffic, which the PMC
     # summary below shows)

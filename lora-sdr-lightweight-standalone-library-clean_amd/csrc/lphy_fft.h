@@ -672,8 +672,12 @@ __device__ __forceinline__ ArgMax2 team_argmax2_keyed_first(const cf32 (&v)[16],
     unsigned k1 = 0u, k2 = 0u;
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
+#ifdef LPHY_KEY_FMA  // A/B: |X|^2 = fma(x, x, fl(y y)), scalar f32 (within cert_gap's 8 u)
+        const float m2 = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
+#else
         const cf32 sq = v[e] * v[e];
         const float m2 = sq.x + sq.y;
+#endif
         const unsigned key = (__float_as_uint(m2) & ~15u) | (unsigned)e;
         k2 = med3_u32(k1, k2, key);
         k1 = k1 > key ? k1 : key;

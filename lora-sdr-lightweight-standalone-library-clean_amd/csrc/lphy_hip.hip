@@ -128,10 +128,22 @@ inline bool frames_fit(unsigned sf, unsigned osr, int est_units, size_t total) {
 // wavefront (pair at SF 11), the two-symbol estimate, no window, the
 // certified rotation, and in modes 1/2 the speculative normalisation (its
 // scan covers the two estimate symbols only).
+// Lowest SF the wave-per-symbol kernel (k_wave) takes; k_frames below it
+// (same-box A/B, DESIGN §4.5: SF 10 1.64 -> 1.21 ms, SF 9 1.32 -> 1.31 ms).
+// LPHY_WAVE_MIN_SF (9..13) moves the boundary for A/B timing.
+unsigned wave_min_sf() {
+    static const unsigned v = [] {
+        const char* e = getenv("LPHY_WAVE_MIN_SF");
+        const int x = e ? atoi(e) : 0;
+        return (x >= 9 && x <= 13) ? (unsigned)x : 9u;
+    }();
+    return v;
+}
+
 inline bool wave_fit(unsigned sf, unsigned osr, int window, int est_units, size_t total, int mode,
                      const DemodArgs& A) {
-    return (sf == 11 || sf == 12) && osr == 1 && window == LPHY_WINDOW_NONE && est_units == 2 && total >= 2 &&
-           !A.exact_rotation && (mode == LPHY_MODE_DEMODULATE || A.spec);
+    return sf >= wave_min_sf() && sf <= 12 && osr == 1 && window == LPHY_WINDOW_NONE && est_units == 2 &&
+           total >= 2 && !A.exact_rotation && (mode == LPHY_MODE_DEMODULATE || A.spec);
 }
 
 const SfOps* sf_ops(unsigned sf) {
@@ -356,10 +368,10 @@ int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t f
     // (Measured alternative: the separate kernels pipelined over chunks on
     // two streams, prologue of chunk c+1 beside the symbol kernel of chunk
     // c: the co-running kernels slowed each other ~2x, 1.1x slower overall.)
+    const bool wfit = wave_fit(c->sf, c->osr, c->window, A.est_units, total, mode, A);
     const bool fused = (all || (stages & both) == both) && !(flags & LPHY_F_UNFUSED) && fused_enabled() &&
-                       (frames_fit(c->sf, c->osr, A.est_units, total) ||
-                        wave_fit(c->sf, c->osr, c->window, A.est_units, total, mode, A));
-    A.wave = fused && c->sf >= 11 ? 1 : 0;
+                       (frames_fit(c->sf, c->osr, A.est_units, total) || wfit);
+    A.wave = fused && (c->sf >= 11 || wfit) ? 1 : 0;
     A.sentinels = fused && !A.wave ? 1 : 0;  // k_cuframe marks open symbols in the output only
     // SF 11-12 separate launches, modes 1/2: the speculative normalisation
     // of k_frames across workgroups (k_maxabs scans the two estimate

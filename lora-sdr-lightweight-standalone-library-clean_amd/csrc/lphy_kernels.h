@@ -2479,6 +2479,15 @@ int launch_frames_sf(const DemodArgs& A, hipStream_t st) {
         (void)A; (void)st;
         return -ENOTSUP;
     } else {
+        if constexpr (SF >= 9) {  // the wave-per-symbol geometry down to 8 lanes per symbol
+            if (A.wave) {
+                switch (A.mode) {
+                    case LPHY_MODE_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_DEMODULATE>(A, st);
+                    case LPHY_MODE_LORA_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_LORA_DEMODULATE>(A, st);
+                    default: return launch_wave_mode<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>(A, st);
+                }
+            }
+        }
         switch (A.mode) {
             case LPHY_MODE_DEMODULATE:
                 return A.win ? launch_frames_mode<SF, LPHY_MODE_DEMODULATE | kWinBit>(A, st)

@@ -1,6 +1,6 @@
-// lphy_wave.h — fused single launch for SF 11-12 (N = 2048 / 4096): one
-// wavefront per symbol (SF 12) or per symbol pair (SF 11), no workgroup
-// barrier in the loop.  Included by lphy_kernels.h inside its anonymous
+// lphy_wave.h — fused single launch for SF 9-12 (N = 512 .. 4096): one
+// wavefront per unit of 64 x 64 complex values, i.e. one symbol at SF 12,
+// 2 / 4 / 8 symbols at SF 11 / 10 / 9, no workgroup barrier in the loop.  Included by lphy_kernels.h inside its anonymous
 // namespace, after k_frames (it reuses SymCtx, EstFold, the certificate and
 // the speculative normalisation of the SF <= 10 path).
 //
@@ -8,16 +8,16 @@
 // (/root/reference/src/phy/LoRaDemod.cpp:142-176, phy.cpp:204-238) with
 // KISS's recursive radix-4 DIT (kissfft.hh:106-185).  Here a lane holds 64
 // complex values of one symbol (LPS = N/64 lanes per symbol: 64 at SF 12,
-// 32 at SF 11 where a wave carries two symbols):
+// 32 / 16 / 8 at SF 11 / 10 / 9 where a wave carries SPW = 64 / LPS symbols):
 //
 //   staging  the unit's IQ was copied HBM -> LDS by LDS-DMA during the
 //            previous unit (global_load_lds_dwordx4, 1 KiB per wave
 //            instruction, natural sample order); lane (h, l) reads samples
 //            i = l + LPS m of symbol h, m = 0..63, applies the [exact]
 //            dechirp and the rotation, keeps them in registers;
-//   pass 1   KISS stages 5, 4, 3 (the innermost) on the lane's registers:
+//   pass 1   KISS stages L-1 .. 3 (the innermost) on the lane's registers:
 //            the inputs with equal i mod 64 form one sub-transform of
-//            length LPS (one group per lane at SF 12, two at SF 11);
+//            length LPS (SPW groups per lane);
 //   exchange the 64 x LPS transpose through the wave's own LDS buffer (the
 //            one the IQ landed in: XOR-swizzled rows, conflict-free b64
 //            writes and reads), then the next unit's LDS-DMA is issued into
@@ -37,44 +37,67 @@
 // unfused products, the detector's exact argmax, bit-identical bins.
 //
 // Per wave, frames w, w + W, ... (W waves); per frame one blocking two-symbol
-// max-abs scan (modes 1/2), the estimate units (2 at SF 12, one pair unit at
-// SF 11), then the symbol units.  The next frame's estimate units run two
+// max-abs scan (modes 1/2), the estimate units (2 at SF 12, below one unit
+// whose halves 0 and 1 hold symbols 0 and 1), then the symbol units.  The next frame's estimate units run two
 // symbol units before the current frame's end, so its time shift is known
 // when its first symbol unit's LDS-DMA is issued:
 //   E(0) | D(0)_0..D(0)_{p-1}, E(1), D(0)_p..D(0)_{ND-1} | D(1)_0 ...
 // with ND symbol units per frame and p = max(0, ND - 2).
 //
-// LDS: 4 waves x 32 KiB buffers + the down-chirp (32 KiB at SF 12): the
-// whole 160 KiB of a CU at SF 12, one 256-thread workgroup per CU.
+// LDS: 4 waves x 32 KiB buffers (below 32 lanes per symbol each symbol's
+// rows padded by LPS entries) + the down-chirp (N entries): the whole
+// 160 KiB of a CU at SF 12, one 256-thread workgroup per CU.
 
 template <int SF>
 struct WGeo {
     static constexpr int N = 1 << SF;
-    static constexpr int LPS = N / 64;    // lanes per symbol
-    static constexpr int SPW = 64 / LPS;  // symbols per unit (1 | 2)
-    static constexpr int NE = 2 / SPW;    // estimate units per frame
-    static constexpr int M3 = N / 256;    // KISS M(3): pass-1 stage 3 butterfly span
-    static constexpr int M4 = N / 1024;   // KISS M(4)
-    static constexpr int R5 = (SF & 1) ? 2 : 4;  // radix of the innermost stage
+    static constexpr int LPS = N / 64;    // lanes per symbol = pass-1 sub-transform length
+    static constexpr int SPW = 64 / LPS;  // symbols per unit (1 | 2 | 4 | 8)
+    static constexpr int NE = SPW == 1 ? 2 : 1;  // estimate units per frame
+    static constexpr int L = (SF + 1) / 2;       // KISS stages (radix 4, a last radix 2 for odd SF)
     static constexpr int PPS = N / 128;   // LDS-DMA pieces (1 KiB) per symbol
     static_assert(PPS % 4 == 0, "LDS-DMA in groups of four pieces");
-    static constexpr int BUF = SPW * N;   // complex per wave buffer
+    // symbol stride in the wave's buffer: below 32 lanes per symbol a row of
+    // LPS entries shifts the next symbol's banks (conflict-free exchange
+    // reads and staging reads across the symbols of one lane group)
+    static constexpr int SS = LPS >= 32 ? N : N + LPS;
+    static constexpr int BUF = SPW * SS;  // complex per wave buffer
     static constexpr int WPB = 4;         // waves per workgroup
+    // radix of KISS stage l, its butterfly span M(l) (product of the inner
+    // radices) and the digit weight of stage l inside a pass-1 input index
+    __host__ __device__ static constexpr int rad(int l) { return ((SF & 1) && l == L - 1) ? 2 : 4; }
+    __host__ __device__ static constexpr int Mst(int l) {
+        int m = 1;
+        for (int k = l + 1; k < L; ++k) m *= rad(k);
+        return m;
+    }
+    __host__ __device__ static constexpr int Wst(int l) {
+        int w = 1;
+        for (int k = 3; k < l; ++k) w *= rad(k);
+        return w;
+    }
     // block of pass-1 group c = i mod 64 in KISS's output order: base-4
     // reversal of its three digits (c = d0 + 4 d1 + 16 d2 -> 16 d0 + 4 d1 + d2)
     __host__ __device__ static constexpr int rev3(int c) {
         return ((c & 3) << 4) | (((c >> 2) & 3) << 2) | ((c >> 4) & 3);
     }
-    // in-group index m (i = c + 64 m) of pass-1 position p: m = d3 + 4 d4 + 16 d5,
-    // p = d3 M3 + d4 M4 + d5
+    // in-group index m (i = c + 64 m) of pass-1 position p: the mixed-radix
+    // digit reversal of KISS's stages 3 .. L-1 (SF 12: m = d3 + 4 d4 + 16 d5,
+    // p = d3 M3 + d4 M4 + d5)
     __host__ __device__ static constexpr int minv(int p) {
-        return p / M3 + 4 * ((p % M3) / M4) + 16 * (p % M4);
+        int m = 0;
+        for (int l = 3; l < L; ++l) m += ((p / Mst(l)) % rad(l)) * Wst(l);
+        return m;
     }
     // register of pass-1 group g, position p (element m'' = SPW m + g holds
     // sample i = l + LPS m'')
     __host__ __device__ static constexpr int reg1(int g, int p) { return SPW * minv(p) + g; }
-    // exchange row swizzle (complex units) of block B
-    __host__ __device__ static constexpr int sw(int B) { return (B >> 2) & 15; }
+    // exchange row swizzle (complex units) of block B: distinct over the
+    // lanes of one symbol that write together (B's digits d0, d1 follow the
+    // lane), below LPS
+    __host__ __device__ static constexpr int sw(int B) {
+        return LPS >= 32 ? (B >> 2) & 15 : (((B >> 4) & 3) + 4 * ((B >> 2) & 3)) & (LPS - 1);
+    }
 };
 
 // u-multiples the certificate charges beyond KISS's 12 L, each
@@ -248,58 +271,50 @@ __device__ __forceinline__ void wbfly2(cf32& x0, cf32& x1, cf32 w, bool one) {
     x0 = cadd(x0, t);
 }
 
-// Pass 1: KISS stages 5, 4, 3 of every group of the lane.  Twiddle indices
-// are compile-time (wave-uniform loads from the KISS table).
-template <int SF, bool FAST>
-__device__ __forceinline__ void wpass1(cf32 (&v)[64], ctw_t* tab) {
+// Pass 1: KISS stages L-1 .. 3 (the innermost ones: sub-transforms of
+// length N/64 = LPS) of every group of the lane.  Twiddle indices are
+// compile-time: the root on the fast path, wave-uniform loads from the KISS
+// table otherwise.
+template <int SF, bool FAST, int LV>
+__device__ __forceinline__ void wpass1_stage(cf32 (&v)[64], ctw_t* tab, int g) {
     using W = WGeo<SF>;
-    // twiddle tw[k] (k a multiple of N/64): the root on the fast path, the
-    // KISS table otherwise
-    auto tw = [&](int k) __attribute__((always_inline)) {
-        if constexpr (FAST) return root64(k / (W::N / 64));
-        else return cf32(tab[k]);
-    };
-    const cf32 t0 = tw(0);
+    if constexpr (LV >= 3) {
+        constexpr int R = W::rad(LV), M = W::Mst(LV), SPAN = R * M, FS = W::N / SPAN;
+        static_assert(W::LPS % SPAN == 0 && 64 % SPAN == 0, "pass-1 stage inside a group");
 #pragma unroll
-    for (int g = 0; g < W::SPW; ++g) {
-        // stage 5: radix R5, M = 1 (k = 0)
+        for (int blk = 0; blk < W::LPS / SPAN; ++blk) {
 #pragma unroll
-        for (int b = 0; b < W::LPS / W::R5; ++b) {
-            if constexpr (W::R5 == 4)
-                wbfly4<FAST>(v[W::reg1(g, 4 * b)], v[W::reg1(g, 4 * b + 1)], v[W::reg1(g, 4 * b + 2)],
-                             v[W::reg1(g, 4 * b + 3)], t0, t0, t0, true);
-            else
-                wbfly2<FAST>(v[W::reg1(g, 2 * b)], v[W::reg1(g, 2 * b + 1)], t0, true);
-        }
-        // stage 4: radix 4, M = M4, twiddle stride 256
-#pragma unroll
-        for (int blk = 0; blk < 4; ++blk) {
-#pragma unroll
-            for (int k = 0; k < W::M4; ++k) {
-                const int b0 = blk * W::M3 + k;
-                if constexpr (FAST) {
-                    constexpr int D = W::N / 64;  // tw[k'] = root64(k' / D)
-                    wbfly4r(v[W::reg1(g, b0)], v[W::reg1(g, b0 + W::M4)], v[W::reg1(g, b0 + 2 * W::M4)],
-                            v[W::reg1(g, b0 + 3 * W::M4)], 256 * k / D, 512 * k / D, 768 * k / D);
+            for (int k = 0; k < M; ++k) {
+                const int b0 = blk * SPAN + k;
+                if constexpr (R == 4) {
+                    if constexpr (FAST) {
+                        // tw[j k FS] = root64(j k FS / (N/64)) = root64(j k 64 / SPAN)
+                        wbfly4r(v[W::reg1(g, b0)], v[W::reg1(g, b0 + M)], v[W::reg1(g, b0 + 2 * M)],
+                                v[W::reg1(g, b0 + 3 * M)], k * 64 / SPAN, 2 * k * 64 / SPAN, 3 * k * 64 / SPAN);
+                    } else {
+                        wbfly4<false>(v[W::reg1(g, b0)], v[W::reg1(g, b0 + M)], v[W::reg1(g, b0 + 2 * M)],
+                                      v[W::reg1(g, b0 + 3 * M)], cf32(tab[k * FS]), cf32(tab[2 * k * FS]),
+                                      cf32(tab[3 * k * FS]), false);
+                    }
                 } else {
-                    wbfly4<FAST>(v[W::reg1(g, b0)], v[W::reg1(g, b0 + W::M4)], v[W::reg1(g, b0 + 2 * W::M4)],
-                                 v[W::reg1(g, b0 + 3 * W::M4)], tw(256 * k), tw(512 * k), tw(768 * k), k == 0);
+                    if constexpr (FAST) {
+                        const cf32 t = cmul_root(v[W::reg1(g, b0 + M)], k * 64 / SPAN);
+                        v[W::reg1(g, b0 + M)] = csub(v[W::reg1(g, b0)], t);
+                        v[W::reg1(g, b0)] = cadd(v[W::reg1(g, b0)], t);
+                    } else {
+                        wbfly2<false>(v[W::reg1(g, b0)], v[W::reg1(g, b0 + M)], cf32(tab[k * FS]), false);
+                    }
                 }
             }
         }
-        // stage 3: radix 4, M = M3, twiddle stride 64
-#pragma unroll
-        for (int k = 0; k < W::M3; ++k) {
-            if constexpr (FAST) {
-                constexpr int D = W::N / 64;
-                wbfly4r(v[W::reg1(g, k)], v[W::reg1(g, k + W::M3)], v[W::reg1(g, k + 2 * W::M3)],
-                        v[W::reg1(g, k + 3 * W::M3)], 64 * k / D, 128 * k / D, 192 * k / D);
-            } else {
-                wbfly4<FAST>(v[W::reg1(g, k)], v[W::reg1(g, k + W::M3)], v[W::reg1(g, k + 2 * W::M3)],
-                             v[W::reg1(g, k + 3 * W::M3)], tw(64 * k), tw(128 * k), tw(192 * k), k == 0);
-            }
-        }
+        wpass1_stage<SF, FAST, LV - 1>(v, tab, g);
     }
+}
+template <int SF, bool FAST>
+__device__ __forceinline__ void wpass1(cf32 (&v)[64], ctw_t* tab) {
+    using W = WGeo<SF>;
+#pragma unroll
+    for (int g = 0; g < W::SPW; ++g) wpass1_stage<SF, FAST, W::L - 1>(v, tab, g);
 }
 
 // Per-lane twiddles of pass 2's fast form (lane l of its symbol), q = 1..3:
@@ -380,40 +395,70 @@ __device__ __forceinline__ void wexchange(cf32 (&v)[64], cf32* buf, int h, int l
 #pragma unroll
     for (int g = 0; g < W::SPW; ++g) {
         const int B = W::rev3(l + W::LPS * g);
-        const int lb = ((h * W::N + B * W::LPS) << 3) | (W::sw(B) << 3);
+        const int lb = ((h * W::SS + B * W::LPS) << 3) | (W::sw(B) << 3);
 #pragma unroll
         for (int p = 0; p < W::LPS; ++p) lds_st(buf, lb ^ (p << 3), v[W::reg1(g, p)]);
     }
     // a wave's LDS operations run in issue order: the reads see the writes
     asm volatile("" ::: "memory");
     (void)b8;
-    const int rb = (h * W::N) << 3;
+    const int rb = (h * W::SS) << 3;
 #pragma unroll
     for (int Bp = 0; Bp < 64; ++Bp) v[Bp] = lds_ld(buf, rb + ((Bp * W::LPS) << 3) + ((l ^ W::sw(Bp)) << 3));
 }
 
+// One unit's LDS-DMA: frame f, unit index j, the frame's time shift; est:
+// the estimate unit (SF 12: symbol j; below: symbols 0 and 1 in halves 0
+// and 1, the other halves load symbol 1 again); on = 0: no unit.
+struct WDma {
+    unsigned f, j;
+    int t_off;
+    int est, on;
+};
+
+// Window start of symbol s under time shift t (LoRaDemod.cpp:144-150, as
+// sym_ctx for osr 1).
+__device__ __forceinline__ unsigned wwin(const DemodArgs& A, unsigned s, int t, unsigned N) {
+    const unsigned count = (unsigned)A.frame_samples;
+    unsigned base = s * N;
+    if (t > 0) {
+        if (base + N <= count && (unsigned)t <= count - N - base) base += (unsigned)t;
+    } else if (t < 0) {
+        const unsigned off = 0u - (unsigned)t;
+        if (off <= base) base -= off;
+    }
+    return base;
+}
+
 // LDS-DMA of one unit's windows into the wave's buffer: symbol h of the
-// unit from sample `base_h` of frame `f` (dead halves load a valid window).
+// unit at h SS (dead halves load a valid window).
 template <int SF>
-__device__ __forceinline__ void wdma(const DemodArgs& A, cf32* buf, unsigned f0, unsigned base0, unsigned f1,
-                                     unsigned base1, int lane) {
+__device__ __forceinline__ void wdma(const DemodArgs& A, cf32* buf, const WDma& d, int lane) {
     using W = WGeo<SF>;
     typedef __attribute__((address_space(3))) void lds_void;
     typedef __attribute__((address_space(1))) const void g_void;
+    const unsigned S = (unsigned)A.total_syms;
 #pragma unroll
     for (int h = 0; h < W::SPW; ++h) {
-        const unsigned f = h ? f1 : f0, base = h ? base1 : base0;
-        const cf32* src = A.iq + (unsigned long long)f * A.frame_samples + base + 2 * lane;
+        unsigned base;
+        if (d.est) {
+            base = (W::SPW == 1 ? d.j : (h < 2 ? (unsigned)h : 1u)) * (unsigned)W::N;
+        } else {
+            unsigned sy = (unsigned)W::SPW * d.j + (unsigned)h;
+            if (sy >= S) sy = (unsigned)W::SPW * d.j;
+            base = wwin(A, sy, d.t_off, (unsigned)W::N);
+        }
+        const cf32* src = A.iq + (unsigned long long)d.f * A.frame_samples + base + 2 * lane;
         // four 1 KiB pieces per base: the instruction's immediate offset moves
         // the source and the LDS destination alike (tools/ubench/glds_align)
 #pragma unroll
         for (int r = 0; r < W::PPS; r += 4) {
             g_void* g = (g_void*)(src + 128 * r);
-            lds_void* d = (lds_void*)(buf + h * W::N + 128 * r);
-            __builtin_amdgcn_global_load_lds(g, d, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(g, d, 16, 1024, 0);
-            __builtin_amdgcn_global_load_lds(g, d, 16, 2048, 0);
-            __builtin_amdgcn_global_load_lds(g, d, 16, 3072, 0);
+            lds_void* ld = (lds_void*)(buf + h * W::SS + 128 * r);
+            __builtin_amdgcn_global_load_lds(g, ld, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(g, ld, 16, 1024, 0);
+            __builtin_amdgcn_global_load_lds(g, ld, 16, 2048, 0);
+            __builtin_amdgcn_global_load_lds(g, ld, 16, 3072, 0);
         }
     }
 }
@@ -421,8 +466,9 @@ __device__ __forceinline__ void wdma(const DemodArgs& A, cf32* buf, unsigned f0,
 // Keyed top two (see team_argmax2_keyed_first) merged over each symbol's
 // LPS lanes without LDS traffic: DPP exchanges inside every 16-lane row
 // (xor 1, xor 2, half mirror, mirror: each step pairs disjoint lane sets, so
-// every row lane ends with the row's top two), then the rows' results by
-// v_readlane as wave-uniform values.  Every lane of symbol h gets its top two.
+// every lane ends with its 8- or 16-lane group's top two), then, for 32 or
+// 64 lanes per symbol, the rows' results by v_readlane as wave-uniform
+// values.  Every lane of symbol h gets its top two.
 template <int CTRL>
 __device__ __forceinline__ unsigned dpp_u32(unsigned v) {
     return (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
@@ -433,11 +479,21 @@ __device__ __forceinline__ void top2_add(unsigned& K1, unsigned& K2, unsigned o1
 }
 template <int LPS>
 __device__ __forceinline__ void wave_top2_merge(unsigned k1, unsigned k2, int h, unsigned& K1, unsigned& K2) {
-    static_assert(LPS == 32 || LPS == 64, "one or two symbols per wave");
+    static_assert(LPS == 8 || LPS == 16 || LPS == 32 || LPS == 64, "8 to 64 lanes per symbol");
     top2_add(k1, k2, dpp_u32<0xB1>(k1), dpp_u32<0xB1>(k2));    // quad_perm [1,0,3,2]
     top2_add(k1, k2, dpp_u32<0x4E>(k1), dpp_u32<0x4E>(k2));    // quad_perm [2,3,0,1]
     top2_add(k1, k2, dpp_u32<0x141>(k1), dpp_u32<0x141>(k2));  // row_half_mirror
+    if constexpr (LPS == 8) {  // every lane holds its 8-lane symbol's top two
+        K1 = k1;
+        K2 = k2;
+        return;
+    }
     top2_add(k1, k2, dpp_u32<0x140>(k1), dpp_u32<0x140>(k2));  // row_mirror
+    if constexpr (LPS == 16) {
+        K1 = k1;
+        K2 = k2;
+        return;
+    }
     unsigned r1[4], r2[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -486,8 +542,8 @@ __device__ __noinline__ float wscan2(KArgs ka, unsigned f, const cf32* down, int
     const DemodArgs& A = kargs(ka);
     constexpr int N = 1 << SF;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
-    constexpr int U = 32;                 // float4 per lane per round
-    constexpr int ROUNDS = N / (64 * U);  // 2N samples = N float4
+    constexpr int U = N / 64 < 32 ? N / 64 : 32;  // float4 per lane per round
+    constexpr int ROUNDS = N / (64 * U);          // 2N samples = N float4
     static_assert((128 * U) % N == 0, "chirp index of the unrolled scan");
     const float4* f4 = reinterpret_cast<const float4*>(A.iq + (unsigned long long)f * A.frame_samples);
     float fm = 0.0f;
@@ -610,7 +666,7 @@ __device__ __noinline__ UnitResult west_unit(KArgs ka, lds_cf32* lbuf, const lds
     const cf32* const dnl = (const cf32*)ldnl;
     const int lane = threadIdx.x & 63, h = lane / LPS, l = lane % LPS;
     cf32 v[64];
-    const int rb = (h * N + l) << 3;
+    const int rb = (h * W::SS + l) << 3;
 #pragma unroll
     for (int e = 0; e < 64; ++e) {
         if ((e & 7) == 0) cfence();
@@ -636,7 +692,7 @@ __device__ __noinline__ UnitResult west_unit(KArgs ka, lds_cf32* lbuf, const lds
     }
     const unsigned long long nb = __ballot(!(sumsq == sumsq));
     UnitResult ur = wunit_result<SF>(v, h, l, lane);
-    ur.nan = (LPS == 64 ? nb : ((nb >> (32 * h)) & 0xffffffffull)) != 0 ? 1 : 0;
+    ur.nan = (LPS == 64 ? nb : ((nb >> (LPS * h)) & ((1ull << (LPS & 63)) - 1))) != 0 ? 1 : 0;
     if (!live) ur = UnitResult{0, 0, 0.0f, 0.0f, 0};
     return ur;
 }
@@ -667,13 +723,6 @@ __device__ __noinline__ WRot wrot(float rate, float scale) {
     return r;
 }
 
-// One unit's LDS-DMA: windows from samples b0 (symbol 0 of the unit) and b1
-// (symbol 1 at SF 11) of frame f; on = 0: no unit.
-struct WDma {
-    unsigned f, b0, b1;
-    int on;
-};
-
 // Frame end under the speculative normalisation (as k_frames' close): the
 // samples no symbol window covers are scanned, then the frame's true
 // max-abs confirms the two-symbol normalisation, sends the frame to the
@@ -692,7 +741,7 @@ __device__ __noinline__ void wclose(KArgs ka, lds_cf32* lbuf, const lds_cf32* ld
                                     float scale, int t_off, float mx01, float m, float r, bool nan, bool open,
                                     WDma nd) {
     using W = WGeo<SF>;
-    constexpr int N = W::N, SPW = W::SPW;
+    constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     const DemodArgs& A = kargs(ka);
     cf32* const buf = (cf32*)lbuf;
@@ -714,7 +763,7 @@ __device__ __noinline__ void wclose(KArgs ka, lds_cf32* lbuf, const lds_cf32* ld
     UnitResult ua{0, 0, 0.0f, 0.0f, 0}, ub = ua;
 #pragma unroll 1
     for (int j = 0; j < W::NE; ++j) {
-        wdma<SF>(A, buf, f, SPW == 1 ? (unsigned)j * (unsigned)N : 0u, f, (unsigned)N, lane);
+        wdma<SF>(A, buf, WDma{f, (unsigned)j, 0, 1, 1}, lane);
         wait_vm0();
         const UnitResult ur = west_unit<SF, MODE>(ka, lbuf, ldnl, me.scale, true);
         if constexpr (SPW == 1) {
@@ -726,11 +775,11 @@ __device__ __noinline__ void wclose(KArgs ka, lds_cf32* lbuf, const lds_cf32* ld
             ua.findex = __shfl(ur.findex, 0, 64);
             ua.phase = __shfl(ur.phase, 0, 64);
             ua.nan = __shfl(ur.nan, 0, 64);
-            ub.idx = __shfl(ur.idx, 32, 64);
-            ub.valid = __shfl(ur.valid, 32, 64);
-            ub.findex = __shfl(ur.findex, 32, 64);
-            ub.phase = __shfl(ur.phase, 32, 64);
-            ub.nan = __shfl(ur.nan, 32, 64);
+            ub.idx = __shfl(ur.idx, LPS, 64);
+            ub.valid = __shfl(ur.valid, LPS, 64);
+            ub.findex = __shfl(ur.findex, LPS, 64);
+            ub.phase = __shfl(ur.phase, LPS, 64);
+            ub.nan = __shfl(ur.nan, LPS, 64);
         }
     }
     lphy_frame_meta e = me;
@@ -750,7 +799,7 @@ __device__ __noinline__ void wclose(KArgs ka, lds_cf32* lbuf, const lds_cf32* ld
         e.status = !ok ? kStatusFixup : (open ? kStatusRecheck : 0);
         meta_put_est(&A.meta[f], e);
     }
-    if (nd.on) wdma<SF>(A, buf, nd.f, nd.b0, nd.f, nd.b1, lane);
+    if (nd.on) wdma<SF>(A, buf, nd, lane);
 }
 
 // Timing experiments only (-DLPHY_PROFILE_PHASES, tools/ubench): per-wave
@@ -863,33 +912,21 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
         else rec0 = r;
     };
     auto fglob = [&](unsigned k) { return w + k * Wn; };
-    // window start of symbol s under time shift t (LoRaDemod.cpp:144-150, sym_ctx)
-    auto wbase = [&](unsigned s, int t) {
-        lphy_frame_meta m{};
-        m.t_off = t;
-        return sym_ctx(A, 0, s, true, N, m).base;
-    };
-    // the LDS-DMA of unit c: frame and window start of its symbol(s)
+    // the LDS-DMA of unit c: its frame, unit index and the frame's time shift
     auto dma_plan = [&](const WCursor& c) {
-        WDma d{0u, 0u, 0u, 0};
+        WDma d{0u, 0u, 0, 0, 0};
         const int kd = sch.kind(c);
         if (kd == kWDead) return d;
         d.f = fglob(sch.frame(c));
+        d.j = c.j;
         d.on = 1;
-        if (kd == kWEst) {  // SF 12: symbol j; SF 11: symbols 0 and 1
-            d.b0 = SPW == 1 ? c.j * (unsigned)N : 0u;
-            d.b1 = (unsigned)N;
-        } else {
-            const WFrame R = rec(sch.frame(c));
-            const unsigned s0 = SPW * c.j, s1 = (SPW == 2 && s0 + 1 < S) ? s0 + 1 : s0;
-            d.b0 = wbase(s0, R.t_off);
-            d.b1 = wbase(s1, R.t_off);
-        }
+        d.est = kd == kWEst ? 1 : 0;
+        if (kd != kWEst) d.t_off = rec(sch.frame(c)).t_off;
         return d;
     };
     auto dma_unit = [&](const WCursor& c) {
         const WDma d = dma_plan(c);
-        if (d.on) wdma<SF>(A, buf, d.f, d.b0, d.f, d.b1, lane);
+        if (d.on) wdma<SF>(A, buf, d, lane);
     };
 
     // rotation of the frame in demodulation: Qr[b] = [scale] e^{j rate (l + LPS b)}
@@ -943,7 +980,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             const SymCtx c = sym_ctx(A, f, live ? s : 0u, live, N, m);
             // staging: [exact dechirp,] certified rotation, from the LDS copy
             float amax = 0.0f;
-            const int rb = (h * N + l) << 3;
+            const int rb = (h * W::SS + l) << 3;
             // software-pipelined in chunks of 8 samples: chunk q + 1's LDS reads
             // are issued before chunk q's arithmetic (sched barriers pin the
             // order; a single wave per SIMD has no other wave to hide them)
@@ -1026,7 +1063,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             unsigned K1, K2;
             wave_top2_merge<LPS>(k1, k2, h, K1, K2);
             const unsigned long long bm = __ballot(k1 == K1);
-            const unsigned long long hm = LPS == 64 ? bm : ((bm >> (32 * h)) & 0xffffffffull);
+            const unsigned long long hm = LPS == 64 ? bm : ((bm >> (LPS * h)) & ((1ull << (LPS & 63)) - 1));
             ArgMax2 b2;
             b2.v = __uint_as_float(K1 & ~63u);
             b2.v2 = __uint_as_float(K2 | 63u);
@@ -1093,11 +1130,11 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                     ua = ur0;
                 }
             } else {  // the pair's second estimate unit from the upper half
-                ub.idx = __shfl(ur.idx, 32, 64);
-                ub.valid = __shfl(ur.valid, 32, 64);
-                ub.findex = __shfl(ur.findex, 32, 64);
-                ub.phase = __shfl(ur.phase, 32, 64);
-                ub.nan = __shfl(ur.nan, 32, 64);
+                ub.idx = __shfl(ur.idx, LPS, 64);
+                ub.valid = __shfl(ur.valid, LPS, 64);
+                ub.findex = __shfl(ur.findex, LPS, 64);
+                ub.phase = __shfl(ur.phase, LPS, 64);
+                ub.nan = __shfl(ur.nan, LPS, 64);
                 ua.idx = __shfl(ur.idx, 0, 64);
                 ua.valid = __shfl(ur.valid, 0, 64);
                 ua.findex = __shfl(ur.findex, 0, 64);
