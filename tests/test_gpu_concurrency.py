@@ -1,4 +1,4 @@
-"""Concurrency and ordering at SF 11-12 (the fused wave kernel and the
+"""Concurrency and ordering at SF 9-12 (the fused wave kernel and the
 separate launches) and SF <= 10 with LPHY_F_UNFUSED:
 
 * two lphy_hip_demod_batch calls on ONE context issued on two streams at
@@ -51,7 +51,7 @@ def _host(lphy, syms, pay, meta, nf, per):
             meta.cpu().numpy().view(lphy.META_DTYPE))
 
 
-@pytest.mark.parametrize("sf,mode", [(12, 2), (11, 2), (12, 1), (11, 0)])
+@pytest.mark.parametrize("sf,mode", [(12, 2), (11, 2), (12, 1), (11, 0), (10, 2), (9, 1)])
 @pytest.mark.parametrize("unfused", [False, True])
 def test_two_streams_one_context(oracle, lphy, sf, mode, unfused):
     nf = 40
@@ -83,7 +83,7 @@ def test_two_streams_one_context(oracle, lphy, sf, mode, unfused):
 
 
 @pytest.mark.parametrize("sf,mode,unfused", [(12, 2, True), (11, 1, True), (12, 0, True),
-                                             (12, 2, False), (11, 2, False),
+                                             (12, 2, False), (11, 2, False), (10, 2, False), (9, 1, False),
                                              (9, 2, True), (7, 0, True)])
 def test_forced_recheck_no_symbol_lost(oracle, lphy, sf, mode, unfused):
     nf = 24 if sf >= 11 else 96

@@ -55,7 +55,7 @@ def _all_recovered(lphy, wl):
     assert (meta["sync_word"] == 0x12).all()
 
 
-@pytest.mark.parametrize("sf,frames", [(7, 65536), (12, 4096)])
+@pytest.mark.parametrize("sf,frames", [(7, 65536), (10, 8192), (12, 4096)])
 def test_full_size_config(oracle, lphy, sf, frames):
     """C1 / C2 at full size: mode 2 (the bench's) and mode 0 (lora_phy::
     demodulate) over the whole resident batch."""
