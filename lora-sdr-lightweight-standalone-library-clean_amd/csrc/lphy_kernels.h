@@ -649,9 +649,19 @@ __device__ __forceinline__ float cert_bound(float rate, float start, float amax,
     const float P = fabsf(start) + ar;
     return kU * A * ((24.0f + 12.0f * L + extra) + 2.0f * ar + P) * 1.001f;
 }
-// winner's lead over the runner-up, less the |X|^2 roundings
+// winner's lead over the runner-up, less the |X|^2 roundings.  The square
+// roots are the hardware v_sqrt_f32 (within 1 ulp, i.e. 2u relative, for the
+// normal inputs the certificate admits: b.v >= 1e-30, runner-up clamped to
+// 1e-30), charged as 2 ulp = 4u on each side on top of the 8u: the
+// correctly rounded sqrtf's Newton fix-up cost ~20 VALU per symbol tile.
+// A NaN winner stays NaN and fails the comparison.
 __device__ __forceinline__ float cert_gap(const ArgMax2& b) {
+#ifdef LPHY_AB_SQRT_EXACT  // A/B timing only: the correctly rounded sqrtf
     return sqrtf(b.v) * (1.0f - 8.0f * kU) - sqrtf(fmaxf(b.v2, 1e-30f)) * (1.0f + 8.0f * kU);
+#else
+    return __builtin_amdgcn_sqrtf(b.v) * (1.0f - 12.0f * kU) -
+           __builtin_amdgcn_sqrtf(fmaxf(b.v2, 1e-30f)) * (1.0f + 12.0f * kU);
+#endif
 }
 template <int SF>
 __device__ __forceinline__ bool fast_certified(const ArgMax2& b, const SymCtx& c, float amax,

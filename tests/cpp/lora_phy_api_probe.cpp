@@ -110,7 +110,7 @@ void chain(const char* tag, unsigned sf, bandwidth bw, const std::vector<uint8_t
     const ssize_t ns = encode(&s.ws, payload.data(), payload.size(), syms.data(), syms.size());
     std::vector<cf> iq((ns + 2) * N + 64);
     const ssize_t nm = modulate(&s.ws, syms.data(), (size_t)ns, iq.data(), iq.size());
-    iq.resize((size_t)nm);
+    iq.resize(nm > 0 ? (size_t)nm : 0);  // (a failed call: no samples)
     if (cfo != 0.0f || delay || sigma > 0.0f) impair(iq, (unsigned)N, cfo, delay, sigma, sf * 131 + delay);
     std::vector<uint16_t> got(ns + 8);
     const ssize_t nd = demodulate(&s.ws, iq.data(), iq.size(), got.data(), got.size());
@@ -211,7 +211,7 @@ void no_alloc() {
     const ssize_t nd = demodulate(&s.ws, iq.data(), (size_t)nm, got, 8);
     char buf[64];
     std::snprintf(buf, sizeof buf, "mod=%zd dem=%zd sync=%02x samples=%016llx ", nm, nd, s.ws.sync_word,
-                  (unsigned long long)fnv(iq.data(), (size_t)nm * sizeof(cf)));
+                  (unsigned long long)(nm > 0 ? fnv(iq.data(), (size_t)nm * sizeof(cf)) : 0));
     line("no_alloc", buf + syms_str(got, nd));
 }
 
@@ -306,7 +306,7 @@ void offsets() {
     const ssize_t ns = encode(&s.ws, p.data(), p.size(), sy.data(), sy.size());
     std::vector<cf> iq((ns + 2) * 256);
     const ssize_t nm = modulate(&s.ws, sy.data(), (size_t)ns, iq.data(), iq.size());
-    iq.resize((size_t)nm);
+    iq.resize(nm > 0 ? (size_t)nm : 0);  // (a failed call: no samples)
     impair(iq, 256, 0.37f, 5, 0.1f, 4242);
     estimate_offsets(&s.ws, iq.data(), iq.size());
     const lora_metrics m = *get_last_metrics(&s.ws);
