@@ -1346,8 +1346,17 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     // chunk per tile through a per-wave LDS buffer by LDS-DMA, issued after
     // staging and folded a tile later.)
     unsigned m_seq = 0xffffffffu;  // group whose frames are scanned
+    // Under speculation (modes 1/2 with scratch) the EB tile takes its
+    // frames' two-symbol max-abs from its own staged samples instead
+    // (EST_MAX below), so the scans run only for the pre-scan schedule.
+#ifdef LPHY_AB_EB_SCAN  // A/B timing only: the round-2 scans under speculation too
+    constexpr bool kEbMax = false;
+#else
+    constexpr bool kEbMax = true;
+#endif
     auto scan_ahead = [&](unsigned nkind_, unsigned nfk_) {
         if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) {
+            if (kEbMax && spec) return;
             const unsigned long long nem = __ballot(nkind_ == kUnitEst);
             if (nem) {
                 const unsigned grp = (unsigned)__shfl((int)nfk_, __ffsll((long long)nem) - 1, 64) / F;
@@ -1430,7 +1439,54 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         // unit's frame max-abs, scanned ahead, first
         const unsigned long long emask = __ballot(kind == kUnitEst);
         float amax;
-        if (emask) {
+        if (kEbMax && spec && emask) {
+            // EST_MAX: an EB tile holds both estimate units of each of its
+            // frames, in teams 2j and 2j + 1 (2 LPS lanes).  The samples are
+            // staged [dechirped], the frame's max(|I|,|Q|) over them folded
+            // (v_max3, and NaN when one is non-finite, like wave_maxabs: such
+            // a frame goes to k_post's exact re-run), then the normalisation
+            // applied: the same operations on the same operands as staging
+            // with the scanned maximum, without reading the two symbols
+            // twice or blocking on a scan.
+            const cf32* dl = down + (c.base & (N - 1)) + fl;
+            float fm = 0.0f;
+            cf32 sum = czero();
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) {
+                const int ce = first_pass_index<SF>(e, 0);
+                cf32 p = raw[e];
+                if constexpr (DECH) p = cmul(p, dl[ce]);
+                fm = max3_abs(fm, p.x, p.y);
+                sum = sum + p;
+                v[e] = p;
+            }
+            bool bad = !(sum.x == sum.x && sum.y == sum.y) || !(fm <= 3.40282347e38f);
+#pragma unroll
+            for (int off = G::LPS; off >= 1; off >>= 1) {
+                const float o = __shfl_xor(fm, off, 64);
+                fm = o > fm ? o : fm;
+            }
+            const unsigned long long bm = __ballot(bad);
+            const unsigned pair = (unsigned)(lane / (2 * G::LPS));
+            constexpr unsigned long long PM = 2 * G::LPS >= 64 ? ~0ull : ((1ull << (2 * G::LPS)) - 1ull);
+            bad = ((bm >> (pair * 2 * G::LPS)) & PM) != 0;
+            const float mx = bad ? __builtin_nanf("") : fm;
+            if (kind == kUnitEst) {
+                const lphy_frame_meta nm = norm_meta_hot(mx, true, A.no_scratch);
+                c.scale = nm.scale;
+                c.live = nm.status == 0;
+                if (su == 0 && lam == 0) ringmx[wv][slot_of(fk)] = mx;
+            }
+            c.ok = kind == kUnitEst && c.live;
+            const float* wl = win + fl;
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) {
+                cf32 y = c.ok ? cscale(v[e], c.scale) : czero();
+                if constexpr ((MODE & kWinBit) != 0) y = cscale(y, wl[first_pass_index<SF>(e, 0)]);
+                v[e] = y;
+            }
+            amax = 0.0f;
+        } else if (emask) {
             if (kind == kUnitEst) {
                 if ((MODE & 3) != LPHY_MODE_DEMODULATE) {
                     const lphy_frame_meta nm = norm_meta_hot(ringmx[wv][slot_of(fk)], true, A.no_scratch);
