@@ -1743,18 +1743,22 @@ __device__ __forceinline__ uint8_t hamming84_decode(uint8_t b) {
     return (uint8_t)((x ^ (unsigned)(kFlip >> (4 * syn))) & 0xfu);
 }
 
+// LoRaCodes.hpp:69-105
+// The reference shifts the register 8 times through poly 0x1021 with a
+// zero input bit per byte; that equals the byte-wise CCITT step with a
+// zero input byte below (all 65,536 registers checked on the host), and
+// the whitening register's feedback is the parity of v & 0xB8.
+__device__ __forceinline__ unsigned sx_shift8(unsigned c) {
+    unsigned x = c >> 8;
+    x ^= x >> 4;
+    return ((c << 8) ^ (x << 12) ^ (x << 5) ^ x) & 0xffffu;
+}
+__device__ __forceinline__ unsigned sx_lfsr(unsigned v) {
+    return ((__builtin_popcount(v & 0xB8u) & 1u) | (v << 1)) & 0xffu;
+}
 __device__ __forceinline__ uint16_t sx1272_checksum(const uint8_t* data, int len) {
-    // LoRaCodes.hpp:69-105
-    // The reference shifts the register 8 times through poly 0x1021 with a
-    // zero input bit per byte; that equals the byte-wise CCITT step with a
-    // zero input byte below (all 65,536 registers checked on the host), and
-    // the whitening register's feedback is the parity of v & 0xB8.
-    auto shift8 = [](unsigned c) -> unsigned {
-        unsigned x = c >> 8;
-        x ^= x >> 4;
-        return ((c << 8) ^ (x << 12) ^ (x << 5) ^ x) & 0xffffu;
-    };
-    auto lfsr = [](unsigned v) -> unsigned { return ((__builtin_popcount(v & 0xB8u) & 1u) | (v << 1)) & 0xffu; };
+    auto shift8 = [](unsigned c) -> unsigned { return sx_shift8(c); };
+    auto lfsr = [](unsigned v) -> unsigned { return sx_lfsr(v); };
     unsigned res = 0, v = 0xff;
     for (int i = 0; i < len; ++i) {
         const unsigned crc = shift8(res);
@@ -1769,7 +1773,71 @@ __device__ __forceinline__ uint16_t sx1272_checksum(const uint8_t* data, int len
 
 
 
+// Register form of the finalisation for rows of up to 64 symbols (32
+// bytes) that are 16-byte aligned with 4-aligned output: the record and all
+// the symbols are loaded before the status test (one memory round trip, not
+// two), and the checksum runs over the decoded words held in registers
+// instead of re-reading the bytes just stored (a third round trip and 28
+// byte loads per frame).  Same bytes, same checksum steps as below.
+__device__ __forceinline__ bool finalize_frame_regs(const FinalArgs& A, unsigned long long f) {
+    const unsigned long long nb = A.nsyms / 2;
+    const uint16_t* s = A.syms + f * A.sym_stride;
+    uint8_t* out = A.bytes + f * nb;
+    if (!A.decode || (A.nsyms & 1) || nb > 32 || (nb & 3) || (reinterpret_cast<uintptr_t>(s) & 15) ||
+        (reinterpret_cast<uintptr_t>(out) & 3))
+        return false;
+    const unsigned nw = (unsigned)(nb / 4);  // wave-uniform
+    const uint4* s4 = reinterpret_cast<const uint4*>(s);
+    uint4 q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if ((unsigned)j < nw) q[j] = s4[j];
+    lphy_frame_meta m = A.meta[f];
+    if (m.status != 0) return true;
+    if (A.set_sync && m.have_sync)
+        m.sync_word = (uint8_t)((((m.sw0 >> A.shift) & 0x0f) << 4) | ((m.sw1 >> A.shift) & 0x0f));
+    unsigned wd[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        wd[j] = 0u;
+        if ((unsigned)j < nw) {
+            const unsigned qs[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const unsigned hi = hamming84_decode((uint8_t)qs[b]) & 0x0fu;
+                const unsigned lo = hamming84_decode((uint8_t)(qs[b] >> 16)) & 0x0fu;
+                wd[j] |= ((hi << 4) | lo) << (8 * b);
+            }
+            *reinterpret_cast<unsigned*>(out + 4 * j) = wd[j];
+        }
+    }
+    if (nb >= 4) {  // phy.cpp:252-259, over bytes 2 .. nb-3
+        const int len = (int)nb - 4;
+        unsigned res = 0, v = 0xff;
+#pragma unroll
+        for (int i = 0; i < 28; ++i) {
+            if (i >= len) break;  // wave-uniform
+            const unsigned byte = (wd[(i + 2) >> 2] >> (8 * ((i + 2) & 3))) & 0xffu;
+            const unsigned crc = sx_shift8(res);
+            v = sx_lfsr(v);
+            res = crc ^ byte;
+        }
+        res ^= v;
+        v = sx_lfsr(v);
+        res ^= v << 8;
+        const unsigned pw = wd[(nb - 2) >> 2] >> (8 * ((nb - 2) & 3));  // bytes nb-2, nb-1 (same word)
+        m.crc_ok = (uint16_t)(pw & 0xffffu) == (uint16_t)res;
+    } else {
+        m.crc_ok = 0;
+    }
+    A.meta[f] = m;
+    return true;
+}
+
 __device__ __forceinline__ void finalize_frame(const FinalArgs& A, unsigned long long f) {
+#ifndef LPHY_AB_FINAL_MEM  // A/B timing only: the memory form for every row
+    if (finalize_frame_regs(A, f)) return;
+#endif
     lphy_frame_meta m = A.meta[f];
     if (m.status != 0) return;
     if (A.set_sync && m.have_sync)

@@ -43,6 +43,7 @@ def run(sf, names):
         full = wl._event_ms(mode, D, 10)
         fused = wl._event_ms(mode, D | both, 10)
         sym = wl._event_ms(mode, D | lphy.F_UNFUSED | lphy.F_STAGE_SYMBOLS, 10)
+        fin = wl._event_ms(mode, D | lphy.F_STAGE_FINAL, 10)
         extra = ""
         lib = lphy._LIB
         if hasattr(lib, "lphy_hip_phase_cycles"):
@@ -56,7 +57,7 @@ def run(sf, names):
             extra = " phases stage/fft/tail = " + "/".join(f"{out[i] / tot:.2f}" for i in range(3))
         wl.run(mode)
         chk = wl.check(mode)
-        print(f"{name:14s} SF{sf}: full {full:.3f} ms  fused {fused:.3f} ms  k_demod {sym:.3f} ms  "
+        print(f"{name:14s} SF{sf}: full {full:.3f} ms  fused {fused:.3f} ms  k_demod {sym:.3f} ms  final {fin * 1e3:.1f} us  "
               f"ok={chk['payloads_recovered']}/{chk['frames']} oracle={chk['oracle_frames_bit_exact']}{extra}",
               flush=True)
         del wl
