@@ -1447,7 +1447,10 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             // a frame goes to k_post's exact re-run), then the normalisation
             // applied: the same operations on the same operands as staging
             // with the scanned maximum, without reading the two symbols
-            // twice or blocking on a scan.
+            // twice or blocking on a scan.  (Modes 1/2 only, so never with
+            // EARLY, the mode-0 in-staging reload of `raw`, which this
+            // staging does not do.)
+            static_assert(!EARLY || (MODE & 3) == LPHY_MODE_DEMODULATE, "EST_MAX staging has no EARLY reload");
             const cf32* dl = down + (c.base & (N - 1)) + fl;
             float fm = 0.0f;
             cf32 sum = czero();
