@@ -11,8 +11,11 @@ resident in HBM; the timed step is one pass of the hot path over the batch:
     per-symbol rotate + KISS-identical FFT + argmax) -> lora_decode + CRC
 
 (LPHY_MODE_DECHIRP_LORA_DEMODULATE + LPHY_F_DECODE through the C ABI), plus,
-for N > 1 ranks, an all_gather of the decoded payloads (RCCL over xGMI).
-`value` = data symbols demodulated by all ranks / max-over-ranks time.
+for N > 1 ranks, the gather of every rank's results (symbols, payloads,
+32-byte frame records) to rank 0 (RCCL over xGMI, overlapped with the next
+step).  `value` = data symbols demodulated by all ranks / max-over-ranks time.
+`--gpus N` without WORLD_SIZE starts the N ranks itself (one process per
+GPU); under torch.distributed.run it checks WORLD_SIZE == N.
 
 Also reported: the high-level lora_phy::demodulate path (mode A), the
 dominant kernel's roofline fraction (HIP events on the launch stream), and
@@ -40,6 +43,10 @@ sys.path.insert(0, str(ROOT / "tests"))
 import lphy  # noqa: E402
 import shard  # noqa: E402
 
+# LPHY_BENCH_REHEARSE=1 rehearses the N > 1 path on a one-GPU box: every
+# rank on cuda:0, gloo instead of RCCL, the slabs staged through host memory
+# for the gather.  Its lines say "rehearsal" and are never a scaling result.
+REHEARSE = os.environ.get("LPHY_BENCH_REHEARSE") == "1"
 HBM_PEAK_GBPS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 PAYLOAD = 32                  # bytes per frame (performance_test.cpp:67)
 DATA_SYMS = 2 * PAYLOAD       # 64 data symbols
@@ -54,7 +61,8 @@ def bytes_per_data_symbol(N: int) -> float:
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); > 1 without WORLD_SIZE spawns the ranks itself")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--sf", type=int, default=7)
@@ -79,7 +87,8 @@ def parse():
 class Workload:
     """One SF configuration resident on this rank's GPU."""
 
-    def __init__(self, sf: int, bw: int, frames: int, rank: int, dev: torch.device, payloads=None):
+    def __init__(self, sf: int, bw: int, frames: int, rank: int, dev: torch.device, payloads=None,
+                 outs=None):
         self.sf, self.N, self.bw, self.frames = sf, 1 << sf, bw, frames
         self.fs = TOTAL_SYMS * self.N
         self.dem = lphy.Demodulator(sf, bw, 1, lphy.WINDOW_NONE, device=dev.index)
@@ -92,14 +101,19 @@ class Workload:
         self.iq = torch.empty(frames * self.fs * 2, dtype=torch.float32, device=dev)
         self.dem.modulate_batch(t_in, frames, DATA_SYMS, self.iq, 1.0, 0x12, stream)
         del t_in
-        self.syms = torch.zeros(frames * DATA_SYMS, dtype=torch.int16, device=dev)
-        self.pay = torch.zeros(frames * PAYLOAD, dtype=torch.uint8, device=dev)
-        self.meta = torch.zeros(frames * 32, dtype=torch.uint8, device=dev)
+        # output sets (symbols, payloads, frame records): one of its own, or
+        # views into the rank's result slabs (N > 1: two, double-buffered
+        # against the gather of the previous step)
+        self.outs = outs or [(torch.zeros(frames * DATA_SYMS, dtype=torch.int16, device=dev),
+                              torch.zeros(frames * PAYLOAD, dtype=torch.uint8, device=dev),
+                              torch.zeros(frames * 32, dtype=torch.uint8, device=dev))]
+        self.syms, self.pay, self.meta = self.outs[0]
         torch.cuda.synchronize()
 
-    def run(self, mode: int, flags: int = lphy.F_DECODE):
-        self.dem.demod_batch(self.iq, self.frames, self.fs, self.syms, self.meta, mode,
-                             flags, payload=self.pay,
+    def run(self, mode: int, flags: int = lphy.F_DECODE, slot: int = 0):
+        syms, pay, meta = self.outs[slot]
+        self.dem.demod_batch(self.iq, self.frames, self.fs, syms, meta, mode,
+                             flags, payload=pay,
                              stream=torch.cuda.current_stream().cuda_stream)
 
     def _event_ms(self, mode: int, flags: int, reps: int, warmup: int = 20) -> float:
@@ -162,29 +176,69 @@ class Workload:
 SETTLE_S = 0.15  # untimed settle before the warmup steps (see timed)
 
 
+class Gatherer:
+    """The §8e exchange of an N > 1 step: the rank's result slab (symbols,
+    payloads, frame records of all its frames) gathered to rank 0 in one
+    RCCL collective.  Two slabs alternate: step k's gather is issued async
+    right after its launch, so it runs while step k+1 demodulates into the
+    other slab; before step k+2 reuses slab k % 2 the stream waits for that
+    gather.  `finish` drains both and returns rank 0's last gathered slabs."""
+
+    def __init__(self, slabs):
+        self.slabs = slabs
+        self.work = [None] * len(slabs)
+        self.out = [None] * len(slabs)
+        self.last = 0
+
+    def before(self, k: int) -> int:
+        slot = k % len(self.slabs)
+        if self.work[slot] is not None:
+            self.work[slot].wait()  # the stream waits for the gather that reads this slab
+            self.work[slot] = None
+        return slot
+
+    def after(self, slot: int) -> None:
+        if REHEARSE:  # gloo: host copies, synchronous
+            self.out[slot], _ = shard.gather_slab(self.slabs[slot].buf.cpu())
+        else:
+            self.out[slot], self.work[slot] = shard.gather_slab(self.slabs[slot].buf, async_op=True)
+        self.last = slot
+
+    def finish(self):
+        for i, w in enumerate(self.work):
+            if w is not None:
+                w.wait()
+                self.work[i] = None
+        return self.out[self.last]
+
+
 def timed(wl: Workload, mode: int, steps: int, warmup: int, world: int, events: list | None = None,
-          settle_s: float = 0.0):
+          settle_s: float = 0.0, gat: Gatherer | None = None):
     """Wall time of `steps` steps between barriers.  With `events`, each
     step issues the demodulation as two calls on the same stream - prologue
     + symbols (the fused k_frames launch and its fix-up), then the per-frame
     finalisation - and HIP events bracket the first, so the dominant
     kernel's duration is measured inside the timed region; the per-step
-    (start, end) event pairs are appended to `events`."""
+    (start, end) event pairs are appended to `events`.  With `gat` (N > 1)
+    each step also gathers its results to rank 0 (Gatherer)."""
     both = lphy.F_DECODE | lphy.F_STAGE_PROLOGUE | lphy.F_STAGE_SYMBOLS
+    k_step = [0]
 
     def step(ev=None):
+        slot = gat.before(k_step[0]) if gat else 0
+        k_step[0] += 1
         if ev is None:
-            wl.run(mode)
+            wl.run(mode, slot=slot)
         else:
             a = torch.cuda.Event(enable_timing=True)
             b = torch.cuda.Event(enable_timing=True)
             a.record()
-            wl.run(mode, both)
+            wl.run(mode, both, slot=slot)
             b.record()
-            wl.run(mode, lphy.F_DECODE | lphy.F_STAGE_FINAL)
+            wl.run(mode, lphy.F_DECODE | lphy.F_STAGE_FINAL, slot=slot)
             ev.append((a, b))
-        if world > 1:  # the only exchange: decoded payloads (RCCL all_gather)
-            shard.gather_payloads(wl.pay, wl.frames, PAYLOAD, world * wl.frames)
+        if gat:
+            gat.after(slot)
 
     # The card's clocks dip for the first ~20 ms of a new sustained load
     # (after an idle gap: one fast launch, then launches up to 40 % slower
@@ -200,6 +254,8 @@ def timed(wl: Workload, mode: int, steps: int, warmup: int, world: int, events: 
         torch.cuda.synchronize()
     for _ in range(warmup):
         step()
+    if gat:
+        gat.finish()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -207,15 +263,42 @@ def timed(wl: Workload, mode: int, steps: int, warmup: int, world: int, events: 
     t0 = time.perf_counter()
     for _ in range(steps):
         step(events)
+    if gat:
+        gat.finish()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=wl.iq.device)
+        t = torch.tensor([dt], dtype=torch.float64, device="cpu" if REHEARSE else wl.iq.device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
     return dt
+
+
+def rank_payloads(sf: int, frames: int, rank: int) -> np.ndarray:
+    """The payloads Workload draws for `rank` (so rank 0 can check every
+    rank's gathered results)."""
+    rng = np.random.default_rng(0x5EED + 7919 * rank + sf)
+    return rng.integers(0, 256, (frames, PAYLOAD), dtype=np.uint8)
+
+
+def check_gathered(parts, sf: int, frames: int, world: int) -> dict:
+    """Rank 0's view of the whole job after the gather: every rank's
+    symbols, payloads and frame records (sync word, status) against what
+    that rank transmitted."""
+    meta_dt = lphy.META_DTYPE
+    ok_pay = ok_sym = ok_rec = 0
+    for r in range(world):
+        (syms, pay, rec), = shard.unpack_slab(parts[r], [frames], DATA_SYMS, PAYLOAD)
+        want = rank_payloads(sf, frames, r)
+        m = rec.reshape(-1).view(meta_dt)
+        ok_pay += int((pay == want).all(axis=1).sum())
+        ok_sym += int((syms == lphy.encode_payloads(want)).all(axis=1).sum())
+        ok_rec += int(((m["status"] == 0) & (m["sync_word"] == 0x12) & (m["have_sync"] == 1)).sum())
+    total = world * frames
+    return {"frames": total, "payloads_recovered": ok_pay, "symbols_exact": ok_sym,
+            "records_ok": ok_rec, "all_ok": ok_pay == ok_sym == ok_rec == total}
 
 
 def usable_cpus() -> dict:
@@ -238,15 +321,29 @@ def usable_cpus() -> dict:
     return out
 
 
+def effective_cpus(c: dict | None = None) -> int:
+    """CPUs this process can actually use: min(affinity mask, cgroup CPU
+    quota rounded up).  A GPU box reports the whole host in os.cpu_count()
+    (256) but grants a 16-CPU quota."""
+    import math
+    c = c or usable_cpus()
+    n = c["affinity_cpus"]
+    if c.get("cgroup_cpu_quota"):
+        n = min(n, max(1, math.ceil(c["cgroup_cpu_quota"])))
+    return max(1, n)
+
+
 def cpu_baseline(wl: Workload, seconds: float, runs: int = 5) -> dict:
     """The reference CPU path on this host:
-    nproc threads, one workspace per thread, on a bounded sample of the same
-    resident frames; each of `runs` runs repeats the sample until
-    seconds / (2 runs) have passed, and the median rate is reported for
-    mode B (dechirp + lora_demodulate + lora_decode, the bench's path) and
-    mode A (demodulate + decode, phy.cpp)."""
+    one thread per effective CPU (effective_cpus), one workspace per thread,
+    on a bounded sample of the same resident frames; each of `runs` runs
+    repeats the sample until seconds / (2 runs) have passed, and the median
+    rate is reported for mode B (dechirp + lora_demodulate + lora_decode,
+    the bench's path) and mode A (demodulate + decode, phy.cpp).  A shorter
+    mode-B run with os.cpu_count() threads is kept as an extra field."""
     import checkers
-    threads = os.cpu_count() or 1
+    cpus = usable_cpus()
+    threads = effective_cpus(cpus)
     if checkers.reference_available():
         ck, kind = checkers.Reference(), "reference"
     else:
@@ -269,10 +366,20 @@ def cpu_baseline(wl: Workload, seconds: float, runs: int = 5) -> dict:
         res[name] = {"value": float(np.median(rates)), "runs": [float(r) for r in rates],
                      "frames": total, "payloads_ok": ok}
     b = res["mode_B"]
+    host = cpus["host_cpus"]
+    if host != threads:  # oversubscribed: os.cpu_count() threads on the quota
+        rates = []
+        for _ in range(3):
+            t, _ = ck.bench(1, wl.sf, x, nf, wl.fs, host, wl.bw)
+            rates.append(nf * DATA_SYMS / t)
+        res["mode_B_os_cpu_count_threads"] = {"value": float(np.median(rates)), "threads": host,
+                                              "runs": [float(r) for r in rates]}
     return {"value": b["value"], "unit": "data symbols/s", "cores": threads, "kind": kind,
-            "runs": len(b["runs"]), "modes": res, "cpus": usable_cpus(),
+            "runs": len(b["runs"]), "modes": res, "cpus": cpus,
             "sample": f"SF{wl.sf} BW{wl.bw // 1000}: {nf}-frame batches of the bench's resident frames, "
-                      f"{threads} threads (os.cpu_count()), median of {runs} runs of ~{per_run:.1f} s per "
+                      f"{threads} threads (effective CPUs: min(affinity {cpus['affinity_cpus']}, cgroup quota "
+                      f"{cpus['cgroup_cpu_quota']}); os.cpu_count() = {host}), median of {runs} runs of "
+                      f"~{per_run:.1f} s per "
                       "mode; value = mode B (dechirp+lora_demodulate+lora_decode, payloads ok="
                       f"{b['payloads_ok']}); mode A = demodulate+decode (phy.cpp, does not round-trip, "
                       "SURVEY §0.3)"}
@@ -349,21 +456,25 @@ def measured_traffic(kernel: str, frames: int):
     return best
 
 
-def _sync_time(fn, steps, warmup, world, dev):
+def _sync_time(fn, steps, warmup, world, dev, gat=None):
     for _ in range(warmup):
         fn()
+    if gat:
+        gat.finish()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
+    if gat:
+        gat.finish()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device="cpu" if REHEARSE else dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
     return dt
@@ -376,21 +487,53 @@ def run_c3(args, baseline, world, rank, dev) -> dict:
     (one resident batch and one launch per SF); payloads gathered."""
     total = args.total_frames or (1 << 17) * world  # weak scaling: 1 M frames at 8 ranks
     first, count, mine, payloads, plan = shard.mixed_plan(total, world, rank, payload=PAYLOAD)
-    buckets = [Workload(sf, args.bw, int(idx.size), rank, dev, payloads=payloads[idx])
-               for sf, idx in sorted(plan.items())]
+    order = sorted(plan)
+    slabs = None
+    if world > 1:
+        # one slab per rank holds all its buckets; every rank's layout is
+        # known from the seeded plan, so the slabs are padded to the largest
+        plans = [shard.mixed_plan(total, world, r, payload=PAYLOAD)[4] for r in range(world)]
+        cap = max(shard.slab_layout([p[sf].size for sf in sorted(p)], DATA_SYMS, PAYLOAD)[1]
+                  for p in plans)
+        slabs = [shard.ResultSlab([plan[sf].size for sf in order], DATA_SYMS, PAYLOAD, dev, cap)
+                 for _ in range(2)]
+    buckets = [Workload(sf, args.bw, int(plan[sf].size), rank, dev, payloads=payloads[plan[sf]],
+                        outs=[sl.views(i) for sl in slabs] if slabs else None)
+               for i, sf in enumerate(order)]
     mode_b = lphy.MODE_DECHIRP_LORA_DEMODULATE
 
+    gat = Gatherer(slabs) if world > 1 else None
+    k_step = [0]
+
     def step():
+        slot = gat.before(k_step[0]) if gat else 0
+        k_step[0] += 1
         for wl in buckets:
-            wl.run(mode_b)
-        if world > 1:
-            for wl in buckets:  # the only exchange: decoded payloads
-                shard.gather_varlen(wl.pay)
+            wl.run(mode_b, slot=slot)
+        if gat:  # the only exchange: every bucket's results in one gather
+            gat.after(slot)
     steps = max(2, args.steps // 4)
-    dt = _sync_time(step, steps, 1, world, dev)
-    syms = torch.tensor([sum(w.frames for w in buckets) * DATA_SYMS], dtype=torch.float64, device=dev)
+    dt = _sync_time(step, steps, 1, world, dev, gat)
+    syms = torch.tensor([sum(w.frames for w in buckets) * DATA_SYMS], dtype=torch.float64,
+                        device="cpu" if REHEARSE else dev)
     if world > 1:
         torch.distributed.all_reduce(syms)
+    gathered = None
+    if world > 1:
+        parts = gat.finish()
+        if rank == 0:
+            # the whole stream, every rank's buckets put back in frame order
+            allp = shard.mixed_plan(total, 1, 0, payload=PAYLOAD)[3]
+            got = []
+            for r in range(world):
+                f_r, c_r, _, _, p_r = shard.mixed_plan(total, world, r, payload=PAYLOAD)
+                srt = sorted(p_r)
+                unp = shard.unpack_slab(parts[r], [p_r[sf].size for sf in srt], DATA_SYMS, PAYLOAD)
+                got.append(shard.reassemble(p_r, {sf: u[1] for sf, u in zip(srt, unp)}, c_r, PAYLOAD))
+            got = np.concatenate(got)
+            gathered = {"frames": int(total), "stream_in_order": bool(np.array_equal(got, allp))}
+        for wl in buckets:
+            wl.run(mode_b)  # slot 0 again for the local checks below
     ok = sum(w.check(mode_b)["payloads_recovered"] for w in buckets)
     # the buckets' payloads put back in frame order = this rank's stream
     ordered = shard.reassemble(plan, {w.sf: w.pay for w in buckets}, count, PAYLOAD)
@@ -406,7 +549,8 @@ def run_c3(args, baseline, world, rank, dev) -> dict:
                                    "cost-balanced shards, one launch per SF bucket",
                        "frames_this_rank": int(count), "frames_per_sf_rank0": per_sf,
                        "iq_gb_rank0": iq_gb, "parallelism": f"frames sharded x{world}"},
-            "check": {"payloads_recovered": ok, "frames": int(count), "reassembled_in_order": in_order}}
+            "check": {"payloads_recovered": ok, "frames": int(count), "reassembled_in_order": in_order,
+                      "gathered_rank0": gathered}}
 
 
 def run_c4(args, baseline, world, rank, dev) -> dict:
@@ -419,26 +563,50 @@ def run_c4(args, baseline, world, rank, dev) -> dict:
     out = {}
     value = None
     for snr in (-10.0, -15.0):
-        wl = Workload(sf, args.bw, frames, rank, dev)
+        slabs = ([shard.ResultSlab([frames], DATA_SYMS, PAYLOAD, dev) for _ in range(2)]
+                 if world > 1 else None)
+        wl = Workload(sf, args.bw, frames, rank, dev, outs=[sl.views(0) for sl in slabs] if slabs else None)
         g = torch.Generator(device=dev)
         g.manual_seed(0xC4 + int(-snr) + 7919 * rank)
         sig = float(np.sqrt(10 ** (-snr / 10) / 2))
         wl.iq.add_(torch.randn(wl.iq.shape, generator=g, device=dev) * sig)
         mode_b = lphy.MODE_DECHIRP_LORA_DEMODULATE
         steps = max(3, args.steps // 4)
-        dt = _sync_time(lambda: wl.run(mode_b), steps, 1, world, dev)
+        gat = Gatherer(slabs) if slabs else None
+        k_step = [0]
+
+        def step():
+            slot = gat.before(k_step[0]) if gat else 0
+            k_step[0] += 1
+            wl.run(mode_b, slot=slot)
+            if gat:
+                gat.after(slot)
+        dt = _sync_time(step, steps, 1, world, dev, gat)
         if value is None:
             value = world * frames * DATA_SYMS * steps / dt
         torch.cuda.synchronize()
-        sent = lphy.encode_payloads(wl.payloads)
-        got = wl.syms.cpu().numpy().view(np.uint16).reshape(frames, DATA_SYMS)
-        pay = wl.pay.cpu().numpy().reshape(frames, PAYLOAD)
-        ser = float((got != sent).mean())
-        ber = float(np.unpackbits(pay ^ wl.payloads).mean())
+        # error rates over the whole job: rank 0 holds every rank's gathered
+        # symbols and payloads (N > 1), and regenerates what each rank sent
+        if gat:
+            parts = gat.finish()
+            res = [shard.unpack_slab(parts[r], [frames], DATA_SYMS, PAYLOAD)[0] for r in range(world)] \
+                if rank == 0 else []
+            sent_pay = [rank_payloads(sf, frames, r) for r in range(world)] if rank == 0 else []
+        else:
+            res = [(wl.syms.cpu().numpy().view(np.uint16).reshape(frames, DATA_SYMS),
+                    wl.pay.cpu().numpy().reshape(frames, PAYLOAD), None)]
+            sent_pay = [wl.payloads]
+        wl.run(mode_b)  # slot 0 for the local oracle sample
         chk = wl.check(mode_b)
-        out[f"snr_{int(snr)}dB"] = {"ser": ser, "ber": ber, "frames": frames,
-                                    "frame_error_rate": float((pay != wl.payloads).any(axis=1).mean()),
-                                    "oracle_frames_bit_exact": chk["oracle_frames_bit_exact"]}
+        if rank == 0:
+            got = np.concatenate([r[0] for r in res])
+            pay = np.concatenate([r[1] for r in res])
+            sp = np.concatenate(sent_pay)
+            ser = float((got != lphy.encode_payloads(sp)).mean())
+            ber = float(np.unpackbits(pay ^ sp).mean())
+            out[f"snr_{int(snr)}dB"] = {"ser": ser, "ber": ber, "frames": int(sp.shape[0]),
+                                        "frame_error_rate": float((pay != sp).any(axis=1).mean()),
+                                        "oracle_frames_bit_exact": chk["oracle_frames_bit_exact"]}
         del wl
         torch.cuda.empty_cache()
     return {"metric": baseline["metric"], "value": value, "unit": "data symbols/s",
@@ -450,15 +618,81 @@ def run_c4(args, baseline, world, rank, dev) -> dict:
             "awgn": out}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_env(rank: int, world: int, port: int) -> dict:
+    """The torch.distributed environment of one rank on this node (what
+    torch.distributed.run sets): one process per GPU, rank r on GPU r."""
+    return {"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+            "LOCAL_WORLD_SIZE": str(world), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+            "MASTER_PORT": str(port)}
+
+
+def launch_ranks(cmd: list, world: int, devices: int | None = None) -> int:
+    """Run `cmd` as `world` ranks, one child process per GPU, and return
+    the first failing rank's exit code (0 when all succeed).  Called before
+    anything touches the GPU (torch.cuda.device_count() does not initialise
+    it on ROCm); refuses when the node has fewer devices than ranks.  A
+    rank that fails ends the others (their own PIDs)."""
+    import subprocess
+    if devices is None:
+        devices = world if REHEARSE else torch.cuda.device_count()
+    if devices < world:
+        print(f"bench.py: --gpus {world} needs {world} GPUs, this node has {devices}", file=sys.stderr)
+        return 3
+    port = _free_port()
+    procs = [subprocess.Popen(cmd, env={**os.environ, **rank_env(r, world, port)}) for r in range(world)]
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    for q in live:
+                        q.terminate()
+            time.sleep(0.1)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ:
+        n = args.gpus or 1
+        if n > 1:  # spawn the ranks ourselves (driver-style `bench.py --gpus N`)
+            sys.exit(launch_ranks([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], n))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(3)
+    if torch.cuda.device_count() < world and not REHEARSE:
+        print(f"bench.py: {world} ranks, {torch.cuda.device_count()} GPUs", file=sys.stderr)
+        sys.exit(3)
+    if REHEARSE:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=dev)
+        if REHEARSE:
+            torch.distributed.init_process_group("gloo")
+        else:
+            torch.distributed.init_process_group("nccl", device_id=dev)
     baseline = json.loads((ROOT / "BASELINE.json").read_text())
     if args.config == "c2":
         args.sf = 12
@@ -466,16 +700,27 @@ def main():
     elif args.config in ("c3", "c4"):
         line = (run_c3 if args.config == "c3" else run_c4)(args, baseline, world, rank, dev)
         if rank == 0:
+            if REHEARSE:
+                line["rehearsal"] = "all ranks on cuda:0 over gloo (LPHY_BENCH_REHEARSE): not a scaling result"
             print(json.dumps(line))
         if world > 1:
             torch.distributed.destroy_process_group()
         return
 
     frames = args.frames or DEFAULT_FRAMES.get(args.sf, 4096)
-    wl = Workload(args.sf, args.bw, frames, rank, dev)
+    slabs = ([shard.ResultSlab([frames], DATA_SYMS, PAYLOAD, dev) for _ in range(2)]
+             if world > 1 else None)
+    wl = Workload(args.sf, args.bw, frames, rank, dev, outs=[sl.views(0) for sl in slabs] if slabs else None)
+    gat = Gatherer(slabs) if slabs else None
     mode_b = lphy.MODE_DECHIRP_LORA_DEMODULATE
     live_ev: list = []
-    dt = timed(wl, mode_b, args.steps, args.warmup, world, events=live_ev, settle_s=SETTLE_S)
+    dt = timed(wl, mode_b, args.steps, args.warmup, world, events=live_ev, settle_s=SETTLE_S, gat=gat)
+    gathered = None
+    if gat:
+        parts = gat.finish()
+        if rank == 0:
+            gathered = check_gathered(parts, args.sf, frames, world)
+        wl.run(mode_b)  # slot 0 holds the results the local checks read
     ms = dt / args.steps * 1e3
     live_kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in live_ev]))
     data_syms = world * frames * DATA_SYMS
@@ -549,7 +794,7 @@ def main():
                 "workload": f"SF{args.sf} BW{args.bw // 1000} CR4/5, {frames} frames/GPU x "
                             f"{PAYLOAD} B payload ({TOTAL_SYMS} symbols), fused dechirp -> "
                             "lora_demodulate -> lora_decode+CRC" +
-                            (", all_gather of payloads" if world > 1 else ""),
+                            (", gather of symbols + payloads + frame records to rank 0" if world > 1 else ""),
                 "sf": args.sf, "bw_hz": args.bw, "frames_per_gpu": frames,
                 "symbols_per_frame": TOTAL_SYMS, "parallelism": f"frames sharded x{world}",
             },
@@ -565,9 +810,12 @@ def main():
                                    if fused else "HIP events, separate symbol-stage launches"},
             "stage_ms": st,
             "check": check_b,
+            "gathered_rank0": gathered,
             "cpu_baseline": cpu,
         }
         line.update(extra)
+        if REHEARSE:
+            line["rehearsal"] = "all ranks on cuda:0 over gloo (LPHY_BENCH_REHEARSE): not a scaling result"
         print(json.dumps(line))
     if world > 1:
         torch.distributed.destroy_process_group()

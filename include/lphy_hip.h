@@ -83,27 +83,13 @@ enum lphy_flags {
     LPHY_F_STAGE_PROLOGUE = 4u,  /* per-frame max-abs + offset estimate   */
     LPHY_F_STAGE_SYMBOLS = 8u,   /* per-symbol rotate + FFT + argmax      */
     LPHY_F_STAGE_FINAL = 16u,    /* per-frame sync word, decode, CRC      */
-    LPHY_F_UNFUSED = 32u,        /* separate prologue / symbol launches
+    LPHY_F_UNFUSED = 32u         /* separate prologue / symbol launches
                                     instead of the fused single launch
-                                    (same results; for comparison)       */
-    LPHY_F_EXACT_ROTATION = 64u, /* fused launch: rotate every symbol with
-                                    the per-sample sincos of the reference
-                                    instead of the certified per-frame
-                                    table (same results; for comparison) */
-    LPHY_F_RESIDENT = 128u,      /* fused launch: where it applies (SF 7,
-                                    56..70 whole symbols per frame), the
-                                    single-read kernel that keeps each frame
-                                    on the CU (same results; experimental) */
-    LPHY_F_SCAN_FIRST = 256u,    /* fused launch, modes 1/2: scan each whole
-                                    frame's max-abs before its estimate (a
-                                    second read of the frame) instead of the
-                                    speculative normalisation checked at the
-                                    frame's end (same results; comparison) */
-    LPHY_F_DEBUG_RECHECK = 512u  /* testing: separate launches mark every
-                                    estimated frame "has open symbols"
-                                    before the symbol kernel runs, so the
-                                    path a concurrent re-check takes is
-                                    exercised on every frame (same results) */
+                                    (same results; the shapes the fused
+                                    kernels do not take run them anyway) */
+    /* Bits 64..512 are comparison / test paths of the test-only build
+     * (lib/test/, csrc/lphy_testing.h); this library rejects them with
+     * -EINVAL. */
 };
 
 enum lphy_window { LPHY_WINDOW_NONE = 0, LPHY_WINDOW_HANN = 1 };
@@ -117,6 +103,21 @@ int lphy_hip_ctx_create(lphy_hip_ctx** out, int device, unsigned sf,
                         unsigned bw_hz, unsigned osr, int window);
 void lphy_hip_ctx_destroy(lphy_hip_ctx* ctx);
 
+/* A context of its own over `base`'s constant tables (shared, read-only;
+ * they are freed with the last context holding them), with `osr` (0: the
+ * base's).  Each context has its own stream and staging for the *_host
+ * entry points, so contexts made this way - one per workspace or thread, as
+ * the C++ shim does (lora_demod_init, init) - never wait for each other.
+ * Returns 0, -EINVAL, -ENOMEM or -EIO. */
+int lphy_hip_ctx_share(lphy_hip_ctx** out, const lphy_hip_ctx* base, unsigned osr);
+
+/* Size the context's host-call staging for calls of up to `frames` frames
+ * of `frame_samples` samples (the *_host entry points below), so that those
+ * calls allocate nothing: the reference allocates nothing after init
+ * (API_SPEC.md:9-14; lora_demod_init's max_samples, LoRaDemod.cpp:11-33).
+ * A larger call later grows the staging once.  Returns 0 or -ENOMEM/-EIO. */
+int lphy_hip_ctx_reserve(lphy_hip_ctx* ctx, size_t frames, size_t frame_samples);
+
 /* Symbols written per frame for a frame of `frame_samples` samples. */
 size_t lphy_hip_syms_per_frame(const lphy_hip_ctx* ctx, size_t frame_samples,
                                int mode);
@@ -129,15 +130,13 @@ size_t lphy_hip_syms_per_frame(const lphy_hip_ctx* ctx, size_t frame_samples,
  * Limits: frames * (frame_samples / (N*osr)) < 2^32 symbols per call and
  * frame_samples < 2^31 (32-bit symbol bookkeeping in the kernels): larger
  * batches give -ERANGE; split them across calls.
- * Memory: the context holds only constant tables.  The fused launches
- * (k_frames up to SF 10, k_wave at SF 11-12: osr 1, no window, modes 1/2
- * with the speculative normalisation or mode 0) allocate nothing.  The
- * SF 11-12 separate launches (LPHY_F_UNFUSED, osr > 1, a window,
- * LPHY_F_EXACT_ROTATION) take per-call speculation records (16 B per frame)
- * from the stream-ordered pool on `stream`, released in stream order, so
- * calls on different streams of one context never share them.  Unlike the
- * reference (API_SPEC.md:11-12, no allocation after init) such a call may
- * therefore allocate; see INTEGRATION.md. */
+ * Memory: the fused launches (k_frames up to SF 8 and for windowed SF 9-10,
+ * k_wave at SF 9-12: osr 1, no window, modes 1/2 with the speculative
+ * normalisation or mode 0) allocate nothing.  The SF 11-12 separate launches
+ * (LPHY_F_UNFUSED, osr > 1, a window) take per-call speculation records
+ * (16 B per frame) from the stream-ordered pool on `stream`, released in
+ * stream order, so calls on different streams of one context never share
+ * them; the *_host forms lend them from the reserved staging instead. */
 int lphy_hip_demod_batch(lphy_hip_ctx* ctx, const float* d_iq, size_t frames,
                          size_t frame_samples, uint16_t* d_syms,
                          uint8_t* d_bytes, lphy_frame_meta* d_meta, int mode,
@@ -171,7 +170,10 @@ int lphy_hip_modulate_batch(lphy_hip_ctx* ctx, const uint16_t* d_syms,
                             float amplitude, uint8_t sync, void* stream);
 
 /* Host-buffer convenience used by the C++ shim: uploads, runs
- * lphy_hip_demod_batch, downloads; synchronous. */
+ * lphy_hip_demod_batch, downloads, on the context's own stream and staging
+ * (lphy_hip_ctx_reserve); returns when that stream is done, without waiting
+ * for other work on the device.  Calls on one context are serialised; use
+ * one context per thread (lphy_hip_ctx_share) for concurrent calls. */
 int lphy_hip_demod_host(lphy_hip_ctx* ctx, const float* h_iq, size_t frames,
                         size_t frame_samples, uint16_t* h_syms,
                         uint8_t* h_bytes, lphy_frame_meta* h_meta, int mode,
@@ -221,6 +223,12 @@ const char* lphy_hip_version(void);
  * over launches on `ctx`'s device since the last reset.  Diagnostic only:
  * synchronises the device.  Returns 0 or -EIO. */
 int lphy_hip_recheck_count(lphy_hip_ctx* ctx, unsigned long long* out, int reset);
+
+/* Device index checks that failed (an LDS or global index outside its
+ * array) since the last reset, summed over the kernels of every SF.  Only
+ * the test build (lib/test/, -DLPHY_DEBUG_BOUNDS) counts them; this library
+ * returns -ENOTSUP.  Synchronises the device. */
+int lphy_hip_bounds_violations(lphy_hip_ctx* ctx, unsigned long long* out, int reset);
 
 /* ------------------------------------------------------------------------
  * Batch forms of the codec helpers of the reference's LoRaCodes.hpp (SURVEY

@@ -135,6 +135,25 @@ __device__ __forceinline__ cf32 csub(cf32 a, cf32 b) { return a - b; }
 __device__ __forceinline__ cf32 cscale(cf32 a, float s) { return a * s; }
 __device__ __forceinline__ cf32 czero() { return cf32{0.0f, 0.0f}; }
 
+// Debug index checks (the test build, -DLPHY_DEBUG_BOUNDS): a computed LDS /
+// global index outside its array counts in this translation unit's device
+// counter (read back through SfOps::violations, lphy_hip_bounds_violations)
+// instead of trapping, so a bad index fails a test rather than faulting the
+// GPU.  Compiled out of the product library.
+#ifdef LPHY_DEBUG_BOUNDS
+namespace {
+__device__ unsigned long long g_bound_violations;
+}
+#endif
+__host__ __device__ constexpr void bound_check(long long i, long long lim) {
+#if defined(LPHY_DEBUG_BOUNDS) && defined(__HIP_DEVICE_COMPILE__)
+    if (!__builtin_is_constant_evaluated() && !(i >= 0 && i < lim)) atomicAdd(&g_bound_violations, 1ull);
+#else
+    (void)i;
+    (void)lim;
+#endif
+}
+
 template <int SF>
 struct Geo {
     static constexpr int N = 1 << SF;
@@ -163,7 +182,10 @@ struct Geo {
     __host__ __device__ static constexpr int sx(int slot) { return XS ? (slot * SKX) & (N - 1) : 0; }
     // general address of position p of the symbol in `slot`
     __host__ __device__ static constexpr int addr(int slot, int p) {
-        return slot * SSTRIDE + (swz(p) ^ sx(slot));
+        bound_check(p, N);
+        const int a = slot * SSTRIDE + (swz(p) ^ sx(slot));
+        bound_check(a, T * SSTRIDE);
+        return a;
     }
     // split form: per-lane base for the lane-dependent position bits ...
     __host__ __device__ static constexpr int lbase(int slot, int lanepart) {
@@ -173,7 +195,11 @@ struct Geo {
     __host__ __device__ static constexpr int cpart(int constpart) { return XS ? swz(constpart) : constpart; }
     __host__ __device__ static constexpr int at(int lb, int cp) { return XS ? (lb ^ cp) : (lb + cp); }
     // the same in bytes (complex = 8 B): lb8 = lbase << 3, cp8 = cpart << 3
-    __host__ __device__ static constexpr int at8(int lb8, int cp8) { return XS ? (lb8 ^ cp8) : (lb8 + cp8); }
+    __host__ __device__ static constexpr int at8(int lb8, int cp8) {
+        const int a = XS ? (lb8 ^ cp8) : (lb8 + cp8);
+        bound_check(a, 8 * T * SSTRIDE);
+        return a;
+    }
     __host__ __device__ static constexpr int R(int l) { return ((SF & 1) && l == L - 1) ? 2 : 4; }
     __host__ __device__ static constexpr int M(int l) {
         int p = 1;

@@ -23,7 +23,9 @@
 // operand order so that symbol indices, sync words and decoded bytes are
 // bit-identical to the reference's CPU path.
 #include "lphy_kernels.h"
+#include "lphy_testing.h"
 
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -48,23 +50,45 @@ __attribute__((weak)) extern const SfOps sf_ops_11 = {};
 __attribute__((weak)) extern const SfOps sf_ops_12 = {};
 }  // namespace lphy
 #endif
+// Constant device tables of one (sf, bw, window): KISS twiddles, down-chirp,
+// Hann window.  Read-only after creation, so contexts made by
+// lphy_hip_ctx_share hold the same tables.
+struct lphy_tables {
+    int device = 0;
+    cf32* d_tw = nullptr;
+    cf32* d_down = nullptr;
+    float* d_win = nullptr;
+    ~lphy_tables() {
+        (void)hipSetDevice(device);
+        if (d_tw) (void)hipFree(d_tw);
+        if (d_down) (void)hipFree(d_down);
+        if (d_win) (void)hipFree(d_win);
+    }
+};
+
 struct lphy_hip_ctx {
     int device = 0;
     unsigned sf = 0, N = 0, bw_hz = 0, osr = 1;
     int window = 0;
     float power_scale = 0.0f;
-    cf32* d_tw = nullptr;
+    std::shared_ptr<lphy_tables> tab;
+    cf32* d_tw = nullptr;   // tab's
     cf32* d_down = nullptr;
     float* d_win = nullptr;
-    // staging for the host convenience entry points
+    // the host convenience entry points (*_host): their own stream, so a
+    // call waits for its own work only (hipStreamSynchronize), and staging
+    // sized by lphy_hip_ctx_reserve up front; the mutex only orders calls
+    // that share this context (one context per workspace / thread: never
+    // contended)
     std::mutex mu;
+    hipStream_t stream = nullptr;
     void* d_stage = nullptr;
     unsigned long long* d_counters = nullptr;  // [0] rechecks, [1..8] phase clocks (experiments)
     size_t stage_bytes = 0;
-    // (per-call scratch - the SF 11-12 speculation records, the producer's
-    // phases, the compensation's shift buffer - comes from the stream-ordered
-    // allocator on the caller's stream, so concurrent calls on different
-    // streams or threads of one context never share it)
+    // (per-call scratch of the device entry points - the SF 11-12 speculation
+    // records, the producer's phases, the compensation's shift buffer - comes
+    // from the stream-ordered allocator on the caller's stream, so concurrent
+    // calls on different streams or threads of one context never share it)
 };
 
 
@@ -233,11 +257,30 @@ struct StreamScratch {
 
 extern "C" {
 
-const char* lphy_hip_version(void) { return "lphy_hip 0.1 gfx950"; }
+const char* lphy_hip_version(void) {
+#if defined(LPHY_TEST_PATHS) && defined(LPHY_DEBUG_BOUNDS)
+    return "lphy_hip 0.2 gfx950 test+bounds";
+#elif defined(LPHY_TEST_PATHS)
+    return "lphy_hip 0.2 gfx950 test";
+#else
+    return "lphy_hip 0.2 gfx950";
+#endif
+}
 
 // Internal (not in include/lphy_hip.h): the context's HIP device, for the
 // streaming ingestion in lphy_stream.hip.
 int lphy_hip_ctx_device(const lphy_hip_ctx* c) { return c ? c->device : -1; }
+
+namespace {
+// A context's own state: the host entry points' stream and the counters
+// (the tables are set by the caller).
+int ctx_own_state(lphy_hip_ctx* c) {
+    if (hipMalloc(&c->d_counters, 9 * sizeof(unsigned long long)) != hipSuccess) return -ENOMEM;
+    HIP_OK(hipMemset(c->d_counters, 0, 9 * sizeof(unsigned long long)));
+    HIP_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    return 0;
+}
+}  // namespace
 
 int lphy_hip_ctx_create(lphy_hip_ctx** out, int device, unsigned sf, unsigned bw_hz,
                         unsigned osr, int window) {
@@ -259,39 +302,83 @@ int lphy_hip_ctx_create(lphy_hip_ctx** out, int device, unsigned sf, unsigned bw
     c->osr = osr;
     c->window = window;
     c->power_scale = (float)(20.0 * std::log10((double)c->N));  // LoRaDetector.hpp:29
+    c->tab = std::make_shared<lphy_tables>();
+    lphy_tables& t = *c->tab;
+    t.device = device;
     std::vector<std::complex<float>> tw, down;
     make_twiddles(tw, (int)c->N);
     make_downchirp(down, (int)c->N, (float)bw_hz / 125000.0f);
-    if (hipMalloc(&c->d_tw, c->N * sizeof(cf32)) != hipSuccess ||
-        hipMalloc(&c->d_down, c->N * sizeof(cf32)) != hipSuccess ||
-        hipMalloc(&c->d_counters, 9 * sizeof(unsigned long long)) != hipSuccess) {
+    if (hipMalloc(&t.d_tw, c->N * sizeof(cf32)) != hipSuccess ||
+        hipMalloc(&t.d_down, c->N * sizeof(cf32)) != hipSuccess ||
+        (window == LPHY_WINDOW_HANN && hipMalloc(&t.d_win, c->N * sizeof(float)) != hipSuccess)) {
         lphy_hip_ctx_destroy(c);
         return -ENOMEM;
     }
-    HIP_OK(hipMemcpy(c->d_tw, tw.data(), c->N * sizeof(cf32), hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(c->d_down, down.data(), c->N * sizeof(cf32), hipMemcpyHostToDevice));
-    HIP_OK(hipMemset(c->d_counters, 0, 9 * sizeof(unsigned long long)));
+    c->d_tw = t.d_tw;
+    c->d_down = t.d_down;
+    c->d_win = t.d_win;
+    if (int rc = ctx_own_state(c)) {
+        lphy_hip_ctx_destroy(c);
+        return rc;
+    }
+    HIP_OK(hipMemcpy(t.d_tw, tw.data(), c->N * sizeof(cf32), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(t.d_down, down.data(), c->N * sizeof(cf32), hipMemcpyHostToDevice));
     if (window == LPHY_WINDOW_HANN) {
         std::vector<float> w;
         make_hann(w, (int)c->N);
-        if (hipMalloc(&c->d_win, c->N * sizeof(float)) != hipSuccess) {
-            lphy_hip_ctx_destroy(c);
-            return -ENOMEM;
-        }
-        HIP_OK(hipMemcpy(c->d_win, w.data(), c->N * sizeof(float), hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(t.d_win, w.data(), c->N * sizeof(float), hipMemcpyHostToDevice));
     }
     *out = c;
+    return 0;
+}
+
+int lphy_hip_ctx_share(lphy_hip_ctx** out, const lphy_hip_ctx* base, unsigned osr) {
+    if (!out || !base) return -EINVAL;
+    *out = nullptr;
+    if (osr == 0) osr = base->osr;
+    if (osr > 64) return -EINVAL;
+    HIP_OK(hipSetDevice(base->device));
+    auto* c = new lphy_hip_ctx;
+    c->device = base->device;
+    c->sf = base->sf;
+    c->N = base->N;
+    c->bw_hz = base->bw_hz;
+    c->osr = osr;  // the tables depend on N only
+    c->window = base->window;
+    c->power_scale = base->power_scale;
+    c->tab = base->tab;
+    c->d_tw = base->d_tw;
+    c->d_down = base->d_down;
+    c->d_win = base->d_win;
+    if (int rc = ctx_own_state(c)) {
+        lphy_hip_ctx_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return 0;
+}
+
+// Internal (not in include/lphy_hip.h): the oversampling ratio of a context
+// the caller owns alone (the C++ shim's per-workspace contexts; the
+// reference's lora_demodulate takes osr per call).  The tables depend on N
+// only.
+int lphy_hip_ctx_set_osr(lphy_hip_ctx* c, unsigned osr) {
+    if (!c || osr == 0 || osr > 64) return -EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->osr = osr;
     return 0;
 }
 
 void lphy_hip_ctx_destroy(lphy_hip_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->d_tw) (void)hipFree(c->d_tw);
-    if (c->d_down) (void)hipFree(c->d_down);
-    if (c->d_win) (void)hipFree(c->d_win);
+    if (c->stream) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamDestroy(c->stream);
+    }
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->d_counters) (void)hipFree(c->d_counters);
+    c->tab.reset();  // the tables go with the last context holding them
     delete c;
 }
 
@@ -323,6 +410,9 @@ int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t f
                      unsigned flags, hipStream_t st, void* lent_spec) {
     if (!c || !d_iq || !d_meta || !d_syms) return -EINVAL;
     if (mode < 0 || mode > 2) return -EINVAL;
+#ifndef LPHY_TEST_PATHS
+    if (flags & kTestFlags) return -EINVAL;  // comparison paths: test build only
+#endif
     if ((flags & LPHY_F_DECODE) && !d_bytes) return -EINVAL;
     if (frames == 0) return 0;
     const size_t step = (size_t)c->N * c->osr;
@@ -351,7 +441,6 @@ int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t f
     A.no_scratch = (flags & LPHY_F_NO_SCRATCH) ? 1 : 0;
     A.exact_rotation = (flags & LPHY_F_EXACT_ROTATION) ? 1 : 0;
     A.counters = c->d_counters;
-    A.resident = (flags & LPHY_F_RESIDENT) ? 1 : 0;
     A.spec = (mode != LPHY_MODE_DEMODULATE && !A.no_scratch && !(flags & LPHY_F_SCAN_FIRST)) ? 1 : 0;
     A.debug_recheck = (flags & LPHY_F_DEBUG_RECHECK) ? 1 : 0;
     const size_t est_syms = mode == LPHY_MODE_DEMODULATE ? 2 : (total < 2 ? total : 2);
@@ -372,7 +461,6 @@ int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t f
     const bool fused = (all || (stages & both) == both) && !(flags & LPHY_F_UNFUSED) && fused_enabled() &&
                        (frames_fit(c->sf, c->osr, A.est_units, total) || wfit);
     A.wave = fused && (c->sf >= 11 || wfit) ? 1 : 0;
-    A.sentinels = fused && !A.wave ? 1 : 0;  // k_cuframe marks open symbols in the output only
     // SF 11-12 separate launches, modes 1/2: the speculative normalisation
     // of k_frames across workgroups (k_maxabs scans the two estimate
     // symbols, k_demod folds the rest, k_post closes each frame); needs the
@@ -555,7 +643,80 @@ int lphy_hip_recheck_count(lphy_hip_ctx* c, unsigned long long* out, int reset) 
     return 0;
 }
 
+int lphy_hip_bounds_violations(lphy_hip_ctx* c, unsigned long long* out, int reset) {
+    if (!c || !out) return -EINVAL;
+#ifdef LPHY_DEBUG_BOUNDS
+    HIP_OK(hipSetDevice(c->device));
+    HIP_OK(hipDeviceSynchronize());
+    unsigned long long total = 0;
+    for (unsigned sf = 1; sf <= 12; ++sf) {
+        const SfOps* o = sf_ops(sf);
+        unsigned long long n = 0;
+        if (o && o->violations) {
+            if (int rc = o->violations(&n, reset)) return rc;
+        }
+        total += n;
+    }
+    *out = total;
+    return 0;
+#else
+    *out = 0;
+    return -ENOTSUP;
+#endif
+}
+
 // ---- host-buffer convenience (synchronous) --------------------------------
+// Each call runs on the context's own stream and waits for that stream only:
+// host copies in (async, ordered on the stream), the kernels, host copies
+// out, hipStreamSynchronize.  Staging comes from lphy_hip_ctx_reserve; a
+// call larger than the reservation grows it (the only allocation after it).
+namespace {
+struct HostLayout {  // byte offsets in the staging buffer of one *_host call
+    size_t iq = 0, syms = 0, bytes = 0, meta = 0, spec = 0, end = 0;
+};
+
+HostLayout demod_layout(const lphy_hip_ctx* c, size_t frames, size_t frame_samples, int mode) {
+    const size_t per = lphy_hip_syms_per_frame(c, frame_samples, mode);
+    HostLayout L;
+    L.syms = align_up(frames * frame_samples * sizeof(cf32));
+    L.bytes = L.syms + align_up(std::max<size_t>(1, frames * per) * sizeof(uint16_t));
+    L.meta = L.bytes + align_up(std::max<size_t>(1, frames * (per / 2)));
+    L.spec = L.meta + align_up(frames * sizeof(lphy_frame_meta));
+    L.end = L.spec + align_up(frames * sizeof(uint4));
+    return L;
+}
+
+// staging every *_host entry point needs for calls of up to `frames`
+// frames of `frame_samples` samples (or one buffer of frames * frame_samples)
+size_t host_stage_bytes(const lphy_hip_ctx* c, size_t frames, size_t frame_samples) {
+    const size_t n = frames * frame_samples;
+    const size_t syms = frame_samples / ((size_t)c->N * c->osr) + 2;
+    size_t b = std::max(demod_layout(c, frames, frame_samples, LPHY_MODE_LORA_DEMODULATE).end,
+                        demod_layout(c, frames, frame_samples, LPHY_MODE_DEMODULATE).end);
+    b = std::max(b, 2 * align_up(n * sizeof(cf32)));                                      // compensate
+    b = std::max(b, align_up(syms * sizeof(uint16_t)) + align_up(n * sizeof(cf32)) +
+                        align_up(syms * sizeof(float)));                                  // modulate
+    b = std::max(b, 3 * align_up(std::max<size_t>(1, frames * syms) * sizeof(uint16_t)));  // decode
+    return b;
+}
+
+int ensure_host_stage(lphy_hip_ctx* c, size_t bytes) {
+    if (c->stage_bytes >= bytes) return 0;
+    if (c->d_stage) {
+        HIP_OK(hipStreamSynchronize(c->stream));
+        (void)hipFree(c->d_stage);
+    }
+    return ensure_stage(c, bytes);
+}
+}  // namespace
+
+int lphy_hip_ctx_reserve(lphy_hip_ctx* c, size_t frames, size_t frame_samples) {
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    return ensure_host_stage(c, host_stage_bytes(c, std::max<size_t>(frames, 1), frame_samples));
+}
+
 int lphy_hip_demod_host(lphy_hip_ctx* c, const float* h_iq, size_t frames,
                         size_t frame_samples, uint16_t* h_syms, uint8_t* h_bytes,
                         lphy_frame_meta* h_meta, int mode, unsigned flags) {
@@ -563,30 +724,30 @@ int lphy_hip_demod_host(lphy_hip_ctx* c, const float* h_iq, size_t frames,
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_OK(hipSetDevice(c->device));
     const size_t per = lphy_hip_syms_per_frame(c, frame_samples, mode);
-    const size_t iq_b = align_up(frames * frame_samples * sizeof(cf32));
-    const size_t sym_b = align_up(std::max<size_t>(1, frames * per) * sizeof(uint16_t));
-    const size_t byte_b = align_up(std::max<size_t>(1, frames * (per / 2)));
-    const size_t meta_b = align_up(frames * sizeof(lphy_frame_meta));
-    const size_t spec_b = align_up(frames * sizeof(uint4));
-    int rc = ensure_stage(c, iq_b + sym_b + byte_b + meta_b + spec_b);
+    const HostLayout L = demod_layout(c, frames, frame_samples, mode);
+    int rc = ensure_host_stage(c, L.end);
     if (rc) return rc;
     char* base = (char*)c->d_stage;
-    float* d_iq = (float*)base;
-    uint16_t* d_syms = (uint16_t*)(base + iq_b);
-    uint8_t* d_bytes = (uint8_t*)(base + iq_b + sym_b);
-    lphy_frame_meta* d_meta = (lphy_frame_meta*)(base + iq_b + sym_b + byte_b);
-    HIP_OK(hipMemcpy(d_iq, h_iq, frames * frame_samples * sizeof(cf32), hipMemcpyHostToDevice));
-    HIP_OK(hipMemset(d_meta, 0, frames * sizeof(lphy_frame_meta)));
+    float* d_iq = (float*)(base + L.iq);
+    uint16_t* d_syms = (uint16_t*)(base + L.syms);
+    uint8_t* d_bytes = (uint8_t*)(base + L.bytes);
+    lphy_frame_meta* d_meta = (lphy_frame_meta*)(base + L.meta);
+    hipStream_t st = c->stream;
+    HIP_OK(hipMemcpyAsync(d_iq, h_iq, frames * frame_samples * sizeof(cf32), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetAsync(d_meta, 0, frames * sizeof(lphy_frame_meta), st));
     rc = demod_batch_impl(c, d_iq, frames, frame_samples, d_syms,
-                          (flags & LPHY_F_DECODE) ? d_bytes : nullptr, d_meta, mode, flags, nullptr,
-                          base + iq_b + sym_b + byte_b + meta_b);
-    if (rc) return rc;
-    HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(h_meta, d_meta, frames * sizeof(lphy_frame_meta), hipMemcpyDeviceToHost));
+                          (flags & LPHY_F_DECODE) ? d_bytes : nullptr, d_meta, mode, flags, st,
+                          base + L.spec);
+    if (rc) {
+        (void)hipStreamSynchronize(st);
+        return rc;
+    }
+    HIP_OK(hipMemcpyAsync(h_meta, d_meta, frames * sizeof(lphy_frame_meta), hipMemcpyDeviceToHost, st));
     if (h_syms && per)
-        HIP_OK(hipMemcpy(h_syms, d_syms, frames * per * sizeof(uint16_t), hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpyAsync(h_syms, d_syms, frames * per * sizeof(uint16_t), hipMemcpyDeviceToHost, st));
     if (h_bytes && (flags & LPHY_F_DECODE) && per / 2)
-        HIP_OK(hipMemcpy(h_bytes, d_bytes, frames * (per / 2), hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpyAsync(h_bytes, d_bytes, frames * (per / 2), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
     return 0;
 }
 
@@ -599,19 +760,23 @@ int lphy_hip_decode_host(lphy_hip_ctx* c, const uint16_t* h_syms, size_t count,
     const size_t sym_b = align_up(std::max<size_t>(1, count) * sizeof(uint16_t));
     const size_t byte_b = align_up(std::max<size_t>(1, count / 2));
     const size_t meta_b = align_up(sizeof(lphy_frame_meta));
-    int rc = ensure_stage(c, sym_b + byte_b + meta_b);
+    int rc = ensure_host_stage(c, sym_b + byte_b + meta_b);
     if (rc) return rc;
     char* base = (char*)c->d_stage;
     uint16_t* d_syms = (uint16_t*)base;
     uint8_t* d_bytes = (uint8_t*)(base + sym_b);
     lphy_frame_meta* d_meta = (lphy_frame_meta*)(base + sym_b + byte_b);
-    if (count) HIP_OK(hipMemcpy(d_syms, h_syms, count * sizeof(uint16_t), hipMemcpyHostToDevice));
-    HIP_OK(hipMemset(d_meta, 0, sizeof(lphy_frame_meta)));
-    rc = lphy_hip_decode_batch(c, d_syms, 1, count, d_bytes, d_meta, nullptr);
-    if (rc) return rc;
-    HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(h_meta, d_meta, sizeof(lphy_frame_meta), hipMemcpyDeviceToHost));
-    if (count / 2) HIP_OK(hipMemcpy(h_bytes, d_bytes, count / 2, hipMemcpyDeviceToHost));
+    hipStream_t st = c->stream;
+    if (count) HIP_OK(hipMemcpyAsync(d_syms, h_syms, count * sizeof(uint16_t), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetAsync(d_meta, 0, sizeof(lphy_frame_meta), st));
+    rc = lphy_hip_decode_batch(c, d_syms, 1, count, d_bytes, d_meta, st);
+    if (rc) {
+        (void)hipStreamSynchronize(st);
+        return rc;
+    }
+    HIP_OK(hipMemcpyAsync(h_meta, d_meta, sizeof(lphy_frame_meta), hipMemcpyDeviceToHost, st));
+    if (count / 2) HIP_OK(hipMemcpyAsync(h_bytes, d_bytes, count / 2, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
     return 0;
 }
 
@@ -622,17 +787,21 @@ int lphy_hip_estimate_host(lphy_hip_ctx* c, const float* h_iq, size_t count,
     HIP_OK(hipSetDevice(c->device));
     const size_t iq_b = align_up(std::max<size_t>(1, count) * sizeof(cf32));
     const size_t meta_b = align_up(sizeof(lphy_frame_meta));
-    int rc = ensure_stage(c, iq_b + meta_b);
+    int rc = ensure_host_stage(c, iq_b + meta_b);
     if (rc) return rc;
     char* base = (char*)c->d_stage;
     float* d_iq = (float*)base;
     lphy_frame_meta* d_meta = (lphy_frame_meta*)(base + iq_b);
-    HIP_OK(hipMemcpy(d_iq, h_iq, count * sizeof(cf32), hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(d_meta, h_meta, sizeof(lphy_frame_meta), hipMemcpyHostToDevice));
-    rc = lphy_hip_estimate_batch(c, d_iq, 1, count, count, d_meta, nullptr);
-    if (rc) return rc;
-    HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(h_meta, d_meta, sizeof(lphy_frame_meta), hipMemcpyDeviceToHost));
+    hipStream_t st = c->stream;
+    HIP_OK(hipMemcpyAsync(d_iq, h_iq, count * sizeof(cf32), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(d_meta, h_meta, sizeof(lphy_frame_meta), hipMemcpyHostToDevice, st));
+    rc = lphy_hip_estimate_batch(c, d_iq, 1, count, count, d_meta, st);
+    if (rc) {
+        (void)hipStreamSynchronize(st);
+        return rc;
+    }
+    HIP_OK(hipMemcpyAsync(h_meta, d_meta, sizeof(lphy_frame_meta), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
     return 0;
 }
 
@@ -643,14 +812,18 @@ int lphy_hip_compensate_host(lphy_hip_ctx* c, float* h_iq, size_t count, float c
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_OK(hipSetDevice(c->device));
     const size_t iq_b = align_up(count * sizeof(cf32));
-    int rc = ensure_stage(c, 2 * iq_b);
+    int rc = ensure_host_stage(c, 2 * iq_b);
     if (rc) return rc;
     float* d = (float*)c->d_stage;
-    HIP_OK(hipMemcpy(d, h_iq, count * sizeof(cf32), hipMemcpyHostToDevice));
-    rc = compensate_impl(c, d, count, cfo, time_offset, nullptr, (char*)c->d_stage + iq_b);
-    if (rc) return rc;
-    HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(h_iq, d, count * sizeof(cf32), hipMemcpyDeviceToHost));
+    hipStream_t st = c->stream;
+    HIP_OK(hipMemcpyAsync(d, h_iq, count * sizeof(cf32), hipMemcpyHostToDevice, st));
+    rc = compensate_impl(c, d, count, cfo, time_offset, st, (char*)c->d_stage + iq_b);
+    if (rc) {
+        (void)hipStreamSynchronize(st);
+        return rc;
+    }
+    HIP_OK(hipMemcpyAsync(h_iq, d, count * sizeof(cf32), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
     return 0;
 }
 
@@ -662,16 +835,20 @@ int lphy_hip_modulate_host(lphy_hip_ctx* c, const uint16_t* h_syms, size_t nsyms
     const size_t samples = (nsyms + 2) * (size_t)c->N * c->osr;
     const size_t sym_b = align_up(std::max<size_t>(1, nsyms) * sizeof(uint16_t));
     const size_t iq_b = align_up(samples * sizeof(cf32));
-    int rc = ensure_stage(c, sym_b + iq_b + align_up((nsyms + 2) * sizeof(float)));
+    int rc = ensure_host_stage(c, sym_b + iq_b + align_up((nsyms + 2) * sizeof(float)));
     if (rc) return rc;
     char* base = (char*)c->d_stage;
     uint16_t* d_syms = (uint16_t*)base;
     float* d_iq = (float*)(base + sym_b);
-    if (nsyms) HIP_OK(hipMemcpy(d_syms, h_syms, nsyms * sizeof(uint16_t), hipMemcpyHostToDevice));
-    rc = modulate_impl(c, d_syms, 1, nsyms, d_iq, amplitude, sync, nullptr, base + sym_b + iq_b);
-    if (rc) return rc;
-    HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(h_iq, d_iq, samples * sizeof(cf32), hipMemcpyDeviceToHost));
+    hipStream_t st = c->stream;
+    if (nsyms) HIP_OK(hipMemcpyAsync(d_syms, h_syms, nsyms * sizeof(uint16_t), hipMemcpyHostToDevice, st));
+    rc = modulate_impl(c, d_syms, 1, nsyms, d_iq, amplitude, sync, st, base + sym_b + iq_b);
+    if (rc) {
+        (void)hipStreamSynchronize(st);
+        return rc;
+    }
+    HIP_OK(hipMemcpyAsync(h_iq, d_iq, samples * sizeof(cf32), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
     return 0;
 }
 

@@ -67,8 +67,6 @@ struct DemodArgs {
     int exact_rotation;      // LPHY_F_EXACT_ROTATION: no certified fast path
     float power_scale;       // LoRaDetector.hpp:29, (float)(20*log10((double)N))
     unsigned long long* counters;  // ctx counters: [0] rechecks, [1..4] phase clocks
-    int sentinels;           // k_post: look for kSymRecheck in frames with status 0 (k_cuframe)
-    int resident;            // LPHY_F_RESIDENT: k_cuframe where it applies
     int spec;                // k_frames modes 1/2: speculative normalisation (no whole-frame pre-scan)
     // separate launches, SF 11-12 fast path, modes 1/2: the same speculation
     // across workgroups, per frame {max-abs of the two estimate symbols,
@@ -100,6 +98,8 @@ struct SfOps {
     int (*frames)(const DemodArgs&, hipStream_t);
     int (*post)(int mode, const DemodArgs&, const FinalArgs&, bool fix, bool fin, hipStream_t);
     int (*estimate)(const DemodArgs&, hipStream_t);
+    // debug build: read (and reset) this SF's failed index checks (else null)
+    int (*violations)(unsigned long long* out, int reset);
 };
 extern const SfOps sf_ops_1, sf_ops_2, sf_ops_3, sf_ops_4, sf_ops_5, sf_ops_6,
     sf_ops_7, sf_ops_8, sf_ops_9, sf_ops_10, sf_ops_11, sf_ops_12;
@@ -586,7 +586,15 @@ __device__ __forceinline__ void stage_symbol(cf32* lds, const Stage<SF>& stg, co
     }
 }
 
+// debug build: sample `off` of frame `f` lies inside the batch (bound_check)
+__device__ __forceinline__ void iq_check(const DemodArgs& A, unsigned long long f, long long off) {
+    bound_check((long long)f, (long long)A.frames);
+    bound_check(off, (long long)A.frame_samples);
+}
+
 __device__ __forceinline__ void store_symbol(const DemodArgs& A, const SymCtx& c, uint16_t idx) {
+    bound_check(c.f, (long long)A.frames);
+    bound_check(c.have_sync ? (long long)c.s - 2 : (long long)c.s, (long long)A.out_per_frame);
     if (c.have_sync && c.s < 2) {
         if (c.s == 0) A.meta[c.f].sw0 = idx;
         else A.meta[c.f].sw1 = idx;
@@ -986,6 +994,7 @@ __device__ __forceinline__ float wave_maxabs(const DemodArgs& A, unsigned f, con
     const cf32* fr = A.iq + (unsigned long long)f * A.frame_samples;
     // limit: the first `limit` samples only (speculative normalisation)
     const unsigned count = limit ? limit : (DECH ? (unsigned)A.total_syms * N : (unsigned)A.frame_samples);
+    iq_check(A, f, (long long)count - 1);
     float mx = 0.0f;
     bool bad = false;  // non-finite [dechirped] sample
     auto acc = [&](cf32 x, unsigned i) {
@@ -1071,6 +1080,7 @@ __device__ float wave_range_maxabs(const DemodArgs& A, unsigned f, unsigned lo, 
     const cf32* fr = A.iq + (unsigned long long)f * A.frame_samples;
     float mx = 0.0f;
     bool b = false;
+    if (hi > lo) iq_check(A, f, (long long)hi - 1);
     for (unsigned i = lo + (unsigned)lane; i < hi; i += 64) {
         cf32 x = fr[i];
         if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) x = cmul(x, down[i & (N - 1)]);
@@ -1171,6 +1181,7 @@ __device__ __forceinline__ float stage_fast(cf32 (&v)[16], cf32 (&raw)[16], cons
 #pragma unroll
         for (int e = 0; e < G::E; ++e) {
             const int ce = first_pass_index<SF>(e, 0);
+            bound_check((c.base & (N - 1)) + fl + ce, 2 * N);
             cf32 p = raw[e];
             if constexpr (EARLY) raw[e] = nsrc[ce];  // the next tile's sample, as this one is consumed
             if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) {
@@ -1185,6 +1196,8 @@ __device__ __forceinline__ float stage_fast(cf32 (&v)[16], cf32 (&raw)[16], cons
 #pragma unroll
         for (int e = 0; e < G::E; ++e) {
             const int ce = first_pass_index<SF>(e, 0);
+            bound_check((c.base & (N - 1)) + fl + ce, 2 * N);
+            bound_check(fl + ce, N);
             cf32 p = raw[e];
             if constexpr (EARLY) raw[e] = nsrc[ce];
             if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) p = cmul(p, dl[ce]);
@@ -1273,8 +1286,14 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     const unsigned ng = (nk + F - 1) / F;
     const unsigned dt_last = ((nk - (ng - 1) * F) * S + WT - 1) / WT;  // live D tiles of the last group
     const unsigned ntiles = PT + (ng - 1) * GT + (dt_last <= PB ? dt_last : dt_last + EBT);
-    auto slot_of = [](unsigned kf) -> unsigned { return ((kf / F) & 1u) * F + kf % F; };
-    const bool exact_only = A.exact_rotation != 0;
+    auto slot_of = [](unsigned kf) -> unsigned {
+        const unsigned sl = ((kf / F) & 1u) * F + kf % F;
+        bound_check(sl, NSLOT);
+        return sl;
+    };
+    // no certified outputs: LPHY_F_EXACT_ROTATION, or LPHY_F_DEBUG_RECHECK
+    // (tests: every symbol left to k_post's exact re-run)
+    const bool exact_only = A.exact_rotation != 0 || A.debug_recheck != 0;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     // Speculative normalisation (modes 1/2).  The reference scales the whole
     // frame by 1 / max(|I|,|Q|) before it estimates (LoRaDemod.cpp:60-78), so
@@ -1349,10 +1368,13 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     // Under speculation (modes 1/2 with scratch) the EB tile takes its
     // frames' two-symbol max-abs from its own staged samples instead
     // (EST_MAX below), so the scans run only for the pre-scan schedule.
+    // That needs both estimate units of a frame in one tile (teams 2j and
+    // 2j + 1): 2 LPS <= 64 lanes, i.e. SF <= 9.  At SF 10 a team is the
+    // whole wave (EBT = 2 tiles per frame), so the scans stay.
 #ifdef LPHY_AB_EB_SCAN  // A/B timing only: the round-2 scans under speculation too
     constexpr bool kEbMax = false;
 #else
-    constexpr bool kEbMax = true;
+    constexpr bool kEbMax = 2 * G::LPS <= 64;
 #endif
     auto scan_ahead = [&](unsigned nkind_, unsigned nfk_) {
         if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) {
@@ -1380,7 +1402,10 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     {
         const cf32* src = A.iq + (unsigned long long)c.f * A.frame_samples + c.base + fl;
 #pragma unroll
-        for (int e = 0; e < G::E; ++e) raw[e] = src[first_pass_index<SF>(e, 0)];
+        for (int e = 0; e < G::E; ++e) {
+            iq_check(A, c.f, (long long)c.base + fl + first_pass_index<SF>(e, 0));
+            raw[e] = src[first_pass_index<SF>(e, 0)];
+        }
     }
     // speculative normalisation: the lane's running state for the two frames
     // whose symbols can be in flight (by parity of the frame): max-abs of the
@@ -1434,6 +1459,8 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         if (early) {
             next_ctx();
             nsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base + fl;
+            iq_check(A, nc.f, (long long)nc.base);
+            iq_check(A, nc.f, (long long)nc.base + N - 1);
         }
         // an EB tile (estimate units of one group, and dead units): each
         // unit's frame max-abs, scanned ahead, first
@@ -1530,7 +1557,10 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             if (t + 1 < ntiles) {
                 const cf32* lsrc = A.iq + (unsigned long long)nc.f * A.frame_samples + nc.base + fl;
 #pragma unroll
-                for (int e = 0; e < G::E; ++e) raw[e] = lsrc[first_pass_index<SF>(e, 0)];
+                for (int e = 0; e < G::E; ++e) {
+                    iq_check(A, nc.f, (long long)nc.base + fl + first_pass_index<SF>(e, 0));
+                    raw[e] = lsrc[first_pass_index<SF>(e, 0)];
+                }
             }
         }
 
@@ -1654,6 +1684,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
             }
             ring[wv][sl] = float4{m.rate, m.scale, __int_as_float(m.t_off),
                                   __uint_as_float((m.status == 0 ? 1u : 0u) | 2u)};
+            bound_check(w + fk * W, (long long)A.frames);
             meta_put_est(&A.meta[w + fk * W], m);
         }
         team_sync<SF>();
@@ -1700,6 +1731,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
                 const float4 rr = ring[wv][slot_of(kf)];
                 if (__float_as_uint(rr.w) & 1u) {
                     const unsigned f = w + kf * W;
+                    bound_check(f, (long long)A.frames);
                     const unsigned cnt = DECH ? S * N : (unsigned)A.frame_samples;
                     const unsigned end = covered_end(S, N, cnt, __float_as_int(rr.z));
                     bool fbad = false;
@@ -2177,16 +2209,6 @@ __device__ void settle_frames(const DemodArgs& A, unsigned long long fb, bool mi
     __syncthreads();
 }
 
-// Whether frame f holds a symbol left open by k_cuframe, which marks them in
-// the output only (kSymRecheck): its symbols and the sync symbols' record.
-__device__ __forceinline__ bool has_sentinel(const DemodArgs& A, unsigned long long f) {
-    const lphy_frame_meta m = A.meta[f];
-    bool any = m.have_sync && (m.sw0 == kSymRecheck || m.sw1 == kSymRecheck);
-    const uint16_t* o = A.syms + f * A.out_per_frame;
-    for (unsigned long long i = 0; i < A.out_per_frame; ++i) any |= o[i] == kSymRecheck;
-    return any;
-}
-
 // Separate launches with spec_big (SF 11-12, modes 1/2): the frame-end
 // check k_frames makes in-kernel, one workgroup per frame (so the exact
 // estimates of settled frames run in parallel).  The samples no symbol
@@ -2303,7 +2325,7 @@ __global__ __launch_bounds__(kTile) void k_post(DemodArgs A, FinalArgs F, int fi
             if (f < A.frames) st = A.meta[f].status;
         }
         const bool fixup = st == kStatusFixup;
-        const bool recheck = st == kStatusRecheck || (A.sentinels && f < A.frames && st == 0 && has_sentinel(A, f));
+        const bool recheck = st == kStatusRecheck;
         if (__syncthreads_or(fixup)) {
             if (threadIdx.x == 0) fcount = 0;
             __syncthreads();
@@ -2321,7 +2343,6 @@ __global__ __launch_bounds__(kTile) void k_post(DemodArgs A, FinalArgs F, int fi
     if (fin && f < A.frames) finalize_frame(F, f);
 }
 
-#include "lphy_cuframe.h"
 #include "lphy_wave.h"
 
 // ---------------------------------------------------------------------------
@@ -2519,45 +2540,10 @@ int launch_frames_occ(const DemodArgs& A, hipStream_t st) {
 #ifndef LPHY_FRAMES_OCC  // experiments: -DLPHY_FRAMES_OCC=3
 #define LPHY_FRAMES_OCC 2
 #endif
-// Single-read CU-resident kernel (lphy_cuframe.h) for the frames it takes:
-// SF 7, whole symbols only, 56..70 symbols, 16-byte aligned IQ.  Opt-in
-// (LPHY_F_RESIDENT, or LPHY_CUFRAME=1 for experiments): it is bit-exact
-// (tests/test_gpu_cuframe.py) but its barrier-locked rounds leave the waves
-// waiting, so it is slower than k_frames today.
-inline bool cuframe_enabled(const DemodArgs& A) {
-    static int env = -1;
-    if (env < 0) {
-        const char* e = getenv("LPHY_CUFRAME");
-        env = (e && e[0] == '1') ? 1 : 0;
-    }
-    return A.resident || env == 1;
-}
-template <int SF>
-bool cuframe_fit(const DemodArgs& A) {
-    using C = CuCfg<SF>;
-    const unsigned long long S = A.total_syms;
-    return cuframe_enabled(A) && S >= (unsigned long long)C::SMIN && S <= (unsigned long long)C::SMAX &&
-           A.frame_samples == S * (unsigned long long)C::N && A.est_units == 2 &&
-           (reinterpret_cast<uintptr_t>(A.iq) & 15) == 0;
-}
-template <int SF, int MODE>
-int launch_cuframe(const DemodArgs& A, hipStream_t st) {
-    unsigned long long blocks = (unsigned long long)cu_count();
-    if (blocks > A.frames) blocks = A.frames;
-    hipLaunchKernelGGL((k_cuframe<SF, MODE>), dim3((unsigned)blocks), dim3(CuCfg<SF>::THREADS), 0, st, A);
-    HIP_OK(hipGetLastError());
-    return 0;
-}
-
 template <int SF, int MODE>
 int launch_frames_mode(const DemodArgs& A, hipStream_t st) {
-    if constexpr (SF == 7) {
-        if (cuframe_fit<SF>(A)) return launch_cuframe<SF, MODE>(A, st);
-    }
     return launch_frames_occ<SF, MODE, LPHY_FRAMES_OCC>(A, st);
 }
-
-
 
 template <int SF, int MODE>
 void launch_symbols_w(const DemodArgs& A, unsigned long long tiles, hipStream_t st, int per_cu) {

@@ -17,6 +17,20 @@ template int launch_post_sf<LPHY_SF>(int, const DemodArgs&, const FinalArgs&, bo
 template int launch_estimate_sf<LPHY_SF>(const DemodArgs&, hipStream_t);
 }  // namespace
 
+#ifdef LPHY_DEBUG_BOUNDS
+// this translation unit's failed index checks (lphy_fft.h bound_check)
+namespace {
+int read_violations(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bound_violations), sizeof(*out)) != hipSuccess) return -EIO;
+    if (reset) {
+        const unsigned long long z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_bound_violations), &z, sizeof(z)) != hipSuccess) return -EIO;
+    }
+    return 0;
+}
+}  // namespace
+#endif
+
 // host-side table (the device pass would otherwise emit it as a constant
 // referencing host functions)
 #ifndef __HIP_DEVICE_COMPILE__
@@ -26,6 +40,11 @@ const SfOps LPHY_CAT(sf_ops_, LPHY_SF) = {
     &launch_frames_sf<LPHY_SF>,
     &launch_post_sf<LPHY_SF>,
     &launch_estimate_sf<LPHY_SF>,
+#ifdef LPHY_DEBUG_BOUNDS
+    &read_violations,
+#else
+    nullptr,
+#endif
 };
 }  // namespace lphy
 #endif

@@ -73,11 +73,12 @@ long long read_chunk(int fd, bool seekable, char* buf, size_t want) {
     const size_t part = (want + kReaders - 1) / kReaders;
     std::vector<long long> got(kReaders, 0);
     std::vector<std::thread> th;
+    int parts = 0;
     for (int k = 0; k < kReaders; ++k) {
         const size_t o = (size_t)k * part;
         if (o >= want) break;
         const size_t n = want - o < part ? want - o : part;
-        th.emplace_back([&, k, o, n] {
+        auto part_read = [&, k, o, n] {
             size_t g = 0;
             while (g < n) {
                 const ssize_t r = ::pread(fd, buf + o + g, n - g, base + (off_t)(o + g));
@@ -90,12 +91,20 @@ long long read_chunk(int fd, bool seekable, char* buf, size_t want) {
                 g += (size_t)r;
             }
             got[k] = (long long)g;
-        });
+        };
+        // no exception may cross the C ABI: when a thread cannot be started
+        // (std::system_error under a thread limit) this thread reads the part
+        try {
+            th.emplace_back(part_read);
+        } catch (...) {
+            part_read();
+        }
+        ++parts;
     }
     for (auto& t : th) t.join();
     // the bytes read are the contiguous prefix up to the first short part (EOF)
     size_t total = 0;
-    for (int k = 0; k < (int)th.size(); ++k) {
+    for (int k = 0; k < parts; ++k) {
         if (got[k] < 0) return got[k];
         total += (size_t)got[k];
         const size_t o = (size_t)k * part;

@@ -1,0 +1,21 @@
+// lphy_testing.h — comparison / test paths of lphy_hip_demod_batch, not part
+// of the public C ABI (include/lphy_hip.h).  The flag bits are accepted only
+// by the test-only build (Makefile `test`: lib/test/liblphy_hip.so, compiled
+// with -DLPHY_TEST_PATHS and -DLPHY_DEBUG_BOUNDS); the product library
+// rejects them with -EINVAL.  The kernels are the same code: the flags only
+// select schedules the tests use as references.
+#pragma once
+
+enum lphy_test_flags {
+    LPHY_F_EXACT_ROTATION = 64u,  // every symbol with the reference's per-sample
+                                  // sincos rotation instead of the certified
+                                  // per-frame table (tests/test_gpu_fast_rotation.py)
+    LPHY_F_SCAN_FIRST = 256u,     // modes 1/2: whole-frame max-abs pre-scan
+                                  // instead of the speculative normalisation
+                                  // (tests/test_gpu_spec.py)
+    LPHY_F_DEBUG_RECHECK = 512u,  // separate launches: every estimated frame
+                                  // marked "has open symbols" first; fused
+                                  // kernels: every symbol left to k_post's
+                                  // exact re-run (tests/test_gpu_concurrency.py)
+};
+constexpr unsigned kTestFlags = LPHY_F_EXACT_ROTATION | 128u | LPHY_F_SCAN_FIRST | LPHY_F_DEBUG_RECHECK;

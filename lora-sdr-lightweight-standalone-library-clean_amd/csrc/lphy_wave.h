@@ -1078,7 +1078,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             const float cgap = cert_gap(b2);
             const bool cert = cgap > 4.0f * (cb1 * am) && (float)N * 1.41421366f * am * 1.0001f < 1e18f &&
                               am >= 1e-20f && b2.v >= 1e-30f;
-            const bool redo = c.ok && !cert;
+            const bool redo = c.ok && (!cert || A.debug_recheck);  // (DEBUG_RECHECK: tests)
             if (live && l == 0) {
                 const uint16_t out = redo ? kSymRecheck : (uint16_t)b2.i;
                 if (c.have_sync && c.s < 2) store_symbol(A, c, c.ok ? out : (uint16_t)0);

@@ -5,19 +5,31 @@
 // on the GPU.  There is no CPU fallback: if no HIP device is usable the
 // demodulation entry points fail with -ENODEV.
 //
-// GPU contexts (constant tables for one sf/bw/osr/window) are cached
-// process-wide, keyed by configuration; the reference keeps no global state,
-// so the cache is the one deliberate difference in that respect.
+// GPU state follows the reference's ownership (API_SPEC.md:9-14,136-140):
+//   * every workspace gets a context of its own at init() / lora_demod_init()
+//     - its own stream and host-call staging, sized there, over constant
+//     tables (twiddles, down-chirp, window) shared per sf/bw/window - so
+//     workspaces used from different threads never wait for each other and
+//     a call allocates nothing (unless it exceeds what init reserved);
+//   * the reference's stateless free functions (lora_decode, lora_modulate)
+//     use a context per calling thread, created by that thread's first
+//     init() / lora_demod_init() (or its first call);
+//   * the shared tables are the one process-wide cache (read-only).
 #include <lora_phy/phy.hpp>
 #include <lphy_hip.h>
 
 #include <cerrno>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
+#include <shared_mutex>
 #include <tuple>
+#include <unordered_map>
 #include <vector>
+
+extern "C" int lphy_hip_ctx_set_osr(lphy_hip_ctx* c, unsigned osr);  // internal (lphy_hip.hip)
 
 namespace lora_phy {
 namespace {
@@ -29,21 +41,100 @@ int device_index() {
     return e ? std::atoi(e) : 0;
 }
 
-// Cached context per (sf, bw, osr, window).
-lphy_hip_ctx* get_ctx(unsigned sf, unsigned bw_hz, unsigned osr, int window, int* err) {
+// Symbols per call the high-level API's staging is sized for at init()
+// (a 127-byte payload and its 2 sync symbols); larger calls grow it once.
+constexpr size_t kReserveSymbols = 256 + 2;
+
+// The shared constant tables: one base context per (sf, bw, window), never
+// used for calls itself.
+lphy_hip_ctx* base_ctx(unsigned sf, unsigned bw_hz, int window, int* err) {
     static std::mutex mu;
-    static std::map<std::tuple<unsigned, unsigned, unsigned, int>, lphy_hip_ctx*> cache;
+    static std::map<std::tuple<unsigned, unsigned, int>, lphy_hip_ctx*> cache;
     std::lock_guard<std::mutex> lk(mu);
-    auto key = std::make_tuple(sf, bw_hz, osr, window);
+    auto key = std::make_tuple(sf, bw_hz, window);
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
     lphy_hip_ctx* c = nullptr;
-    int rc = lphy_hip_ctx_create(&c, device_index(), sf, bw_hz, osr, window);
+    int rc = lphy_hip_ctx_create(&c, device_index(), sf, bw_hz, 1, window);
     if (rc) {
         if (err) *err = rc;
         return nullptr;
     }
     cache[key] = c;
+    return c;
+}
+
+// A context of one's own over the shared tables, staging reserved for
+// `samples` samples per call.
+lphy_hip_ctx* own_ctx(unsigned sf, unsigned bw_hz, unsigned osr, int window, size_t samples, int* err) {
+    lphy_hip_ctx* b = base_ctx(sf, bw_hz, window, err);
+    if (!b) return nullptr;
+    lphy_hip_ctx* c = nullptr;
+    int rc = lphy_hip_ctx_share(&c, b, osr ? osr : 1u);
+    if (!rc) rc = lphy_hip_ctx_reserve(c, 1, samples);
+    if (rc) {
+        lphy_hip_ctx_destroy(c);
+        if (err) *err = rc;
+        return nullptr;
+    }
+    return c;
+}
+
+// Per-thread contexts of the stateless free functions, keyed by
+// (sf, bw, osr); freed when the thread ends.
+struct ThreadCtx {
+    std::map<std::tuple<unsigned, unsigned, unsigned>, lphy_hip_ctx*> m;
+    ~ThreadCtx() {
+        for (auto& kv : m) lphy_hip_ctx_destroy(kv.second);
+    }
+};
+thread_local ThreadCtx t_ctx;
+
+lphy_hip_ctx* thread_ctx(unsigned sf, unsigned bw_hz, unsigned osr, int* err) {
+    auto key = std::make_tuple(sf, bw_hz, osr);
+    auto it = t_ctx.m.find(key);
+    if (it != t_ctx.m.end()) return it->second;
+    lphy_hip_ctx* c = own_ctx(sf, bw_hz, osr, LPHY_WINDOW_NONE, kReserveSymbols * (size_t(1) << sf) * osr, err);
+    if (c) t_ctx.m[key] = c;
+    return c;
+}
+
+// the decoder's context (any SF: decode only reads symbols)
+lphy_hip_ctx* decode_ctx(int* err) { return thread_ctx(7, 125000, 1, err); }
+
+// lora_workspace -> its context (the reference struct has no room for it).
+// Lookups take a shared lock only; init() replaces the entry.
+std::shared_mutex ws_mu;
+std::unordered_map<const lora_workspace*, lphy_hip_ctx*> ws_map;
+
+int window_flag(window_type k, const void* buf);
+
+lphy_hip_ctx* ws_ctx(const lora_workspace* ws, unsigned sf, unsigned osr, int* err) {
+    {
+        std::shared_lock<std::shared_mutex> lk(ws_mu);
+        auto it = ws_map.find(ws);
+        if (it != ws_map.end()) return it->second;
+    }
+    // a workspace init() did not set up here (e.g. a copy): make its context now
+    lphy_hip_ctx* c = own_ctx(sf, static_cast<unsigned>(ws->bw), osr, window_flag(ws->window_kind, ws->window),
+                              kReserveSymbols * (size_t(1) << sf) * osr, err);
+    if (!c) return nullptr;
+    std::unique_lock<std::shared_mutex> lk(ws_mu);
+    auto r = ws_map.emplace(ws, c);
+    if (!r.second) {  // another thread got there first
+        lphy_hip_ctx_destroy(c);
+        return r.first->second;
+    }
+    return c;
+}
+
+// lora_demod_workspace keeps its context pointer in the reference layout's
+// fft_buf (8 bytes, the storage the reference placement-constructs its FFT
+// object into); ws->fft == ws->fft_buf marks it valid.
+lphy_hip_ctx* demod_ws_ctx(const lora_demod_workspace* ws) {
+    if (ws->fft != static_cast<const void*>(ws->fft_buf)) return nullptr;
+    lphy_hip_ctx* c = nullptr;
+    std::memcpy(&c, ws->fft_buf, sizeof c);
     return c;
 }
 
@@ -107,6 +198,23 @@ int init(lora_workspace* ws, const lora_params* cfg) {  // phy.cpp:27-52
     ws->window_kind = cfg->window;
     if (ws->window_kind != window_type::window_none && !ws->window) return -ENOMEM;
     if (ws->window) fill_window(ws->window, (size_t)N, ws->window_kind);
+    // the workspace's GPU context and staging, so later calls allocate
+    // nothing (the reference allocates nothing after init, API_SPEC.md:9-14)
+    int err = 0;
+    lphy_hip_ctx* c = own_ctx(cfg->sf, static_cast<unsigned>(ws->bw), ws->osr,
+                              window_flag(ws->window_kind, ws->window),
+                              kReserveSymbols * size_t(N) * ws->osr, &err);
+    if (c) {
+        std::unique_lock<std::shared_mutex> lk(ws_mu);
+        auto it = ws_map.find(ws);
+        if (it != ws_map.end()) {
+            lphy_hip_ctx_destroy(it->second);  // re-init: the new configuration wins
+            it->second = c;
+        } else {
+            ws_map.emplace(ws, c);
+        }
+    }
+    (void)decode_ctx(&err);  // this thread's decoder context
     return 0;
 }
 
@@ -127,7 +235,7 @@ ssize_t decode(lora_workspace* ws, const uint16_t* symbols, size_t symbol_count,
     if (symbol_count % 2) return -EINVAL;  // LoRaDecoder.cpp:10
     if (symbol_count / 2 > payload_cap) return -ERANGE;  // checked before writing
     int err = -ENODEV;
-    lphy_hip_ctx* c = get_ctx(7, 125000, 1, 0, &err);
+    lphy_hip_ctx* c = ws_ctx(ws, deduce_sf(ws), get_osr(ws), &err);
     if (!c) return err;
     lphy_frame_meta m{};
     int rc = lphy_hip_decode_host(c, symbols, symbol_count, payload, &m);
@@ -152,8 +260,7 @@ void estimate_offsets(lora_workspace* ws, const std::complex<float>* samples,
     const unsigned sf = deduce_sf(ws), osr = get_osr(ws);
     const size_t step = (size_t(1) << sf) * osr;
     if (sample_count / step == 0) return;
-    lphy_hip_ctx* c = get_ctx(sf, static_cast<unsigned>(ws->bw), osr,
-                              window_flag(ws->window_kind, ws->window), nullptr);
+    lphy_hip_ctx* c = ws_ctx(ws, sf, osr, nullptr);
     if (!c) return;
     lphy_frame_meta m{};
     if (lphy_hip_estimate_host(c, reinterpret_cast<const float*>(samples), sample_count, &m)) return;
@@ -165,7 +272,7 @@ void compensate_offsets(const lora_workspace* ws, std::complex<float>* samples,
                         size_t sample_count) {  // phy.cpp:150-180
     if (!ws || !samples || sample_count == 0) return;
     const unsigned sf = deduce_sf(ws), osr = get_osr(ws);
-    lphy_hip_ctx* c = get_ctx(sf, static_cast<unsigned>(ws->bw), osr, LPHY_WINDOW_NONE, nullptr);
+    lphy_hip_ctx* c = ws_ctx(ws, sf, osr, nullptr);
     if (!c) return;
     (void)lphy_hip_compensate_host(c, reinterpret_cast<float*>(samples), sample_count,
                                    ws->metrics.cfo, ws->metrics.time_offset);
@@ -182,8 +289,7 @@ ssize_t demodulate(lora_workspace* ws, const std::complex<float>* iq, size_t sam
     const size_t num = total - 2;
     if (num > symbol_cap) return -ERANGE;
     int err = -ENODEV;
-    lphy_hip_ctx* c = get_ctx(sf, static_cast<unsigned>(ws->bw), osr,
-                              window_flag(ws->window_kind, ws->window), &err);
+    lphy_hip_ctx* c = ws_ctx(ws, sf, osr, &err);
     if (!c) return err;
     lphy_frame_meta m{};
     int rc = lphy_hip_demod_host(c, reinterpret_cast<const float*>(iq), 1, sample_count,
@@ -206,8 +312,7 @@ int demodulate_batch(const lora_workspace* ws, const std::complex<float>* iq, si
     if (!ws || !iq || !symbols) return -EINVAL;
     const unsigned sf = deduce_sf(ws), osr = get_osr(ws);
     int err = -ENODEV;
-    lphy_hip_ctx* c = get_ctx(sf, static_cast<unsigned>(ws->bw), osr,
-                              window_flag(ws->window_kind, ws->window), &err);
+    lphy_hip_ctx* c = ws_ctx(ws, sf, osr, &err);
     if (!c) return err;
     std::vector<lphy_frame_meta> m(frames);
     int rc = lphy_hip_demod_host(c, reinterpret_cast<const float*>(iq), frames, frame_samples,
@@ -226,17 +331,33 @@ int demodulate_batch(const lora_workspace* ws, const std::complex<float>* iq, si
 // ---------------------------------------------------------------------------
 void lora_demod_init(lora_demod_workspace* ws, unsigned sf, window_type win,
                      std::complex<float>* scratch, size_t max_samples) {  // LoRaDemod.cpp:11-33
+    if (lphy_hip_ctx* old = demod_ws_ctx(ws)) lphy_hip_ctx_destroy(old);  // re-init without free
     ws->N = size_t(1) << sf;
     ws->window_kind = win;
     fill_window(ws->window, ws->N, win);
     fill_plan(ws->fft_plan, (int)ws->N, false);
+    // the workspace's GPU context, its staging sized for max_samples (the
+    // scratch length the reference is given for the calls to come; without
+    // one, kReserveSymbols symbols), kept where the reference constructs its
+    // FFT object; no context (no device) leaves nullptr there and the calls
+    // return -ENODEV
+    int err = 0;
+    lphy_hip_ctx* c = sf >= 1 && sf <= 12
+                          ? own_ctx(sf, 125000, 1,
+                                    win != window_type::window_none ? LPHY_WINDOW_HANN : LPHY_WINDOW_NONE,
+                                    max_samples ? max_samples : kReserveSymbols * ws->N, &err)
+                          : nullptr;
+    std::memcpy(ws->fft_buf, &c, sizeof c);
     ws->fft = ws->fft_buf;          // non-null "constructed" markers
     ws->detector = ws->detector_buf;
     ws->scratch = scratch;
     ws->scratch_len = max_samples;
+    (void)decode_ctx(&err);  // this thread's lora_decode context
 }
 
 void lora_demod_free(lora_demod_workspace* ws) {  // LoRaDemod.cpp:35-48
+    if (lphy_hip_ctx* c = demod_ws_ctx(ws)) lphy_hip_ctx_destroy(c);
+    std::memset(ws->fft_buf, 0, sizeof ws->fft_buf);
     ws->detector = nullptr;
     ws->fft = nullptr;
     ws->N = 0;
@@ -248,8 +369,9 @@ size_t lora_modulate(const uint16_t* symbols, size_t symbol_count, std::complex<
                      unsigned sf, unsigned osr, bandwidth bw, float amplitude,
                      uint8_t sync) {  // LoRaMod.cpp:8-43
     const size_t produced = (symbol_count + 2) * (size_t(1) << sf) * osr;
-    lphy_hip_ctx* c = get_ctx(sf, static_cast<unsigned>(bw), osr ? osr : 1, 0, nullptr);
-    if (!c || osr == 0) return 0;
+    if (osr == 0 || sf < 1 || sf > 12) return 0;
+    lphy_hip_ctx* c = thread_ctx(sf, static_cast<unsigned>(bw), osr, nullptr);
+    if (!c) return 0;
     if (lphy_hip_modulate_host(c, symbols, symbol_count, reinterpret_cast<float*>(out),
                                amplitude, sync))
         return 0;
@@ -260,14 +382,9 @@ ssize_t lora_demodulate(lora_demod_workspace* ws, const std::complex<float>* sam
                         size_t sample_count, uint16_t* out_symbols, unsigned osr,
                         uint8_t* out_sync) {  // LoRaDemod.cpp:50-197
     if (!ws || ws->N == 0 || osr == 0) return -EINVAL;
-    unsigned sf = 0;
-    while ((size_t(1) << sf) < ws->N) ++sf;
-    int err = -ENODEV;
-    lphy_hip_ctx* c = get_ctx(sf, 125000, osr,
-                              ws->window_kind != window_type::window_none ? LPHY_WINDOW_HANN
-                                                                          : LPHY_WINDOW_NONE,
-                              &err);
-    if (!c) return err;
+    lphy_hip_ctx* c = demod_ws_ctx(ws);
+    if (!c) return -ENODEV;
+    if (int rc = lphy_hip_ctx_set_osr(c, osr)) return rc;  // the workspace's own context
     const bool scratch_ok = ws->scratch && ws->scratch_len >= sample_count;
     const size_t total = sample_count / (ws->N * osr);
     lphy_frame_meta m{};
@@ -302,7 +419,7 @@ ssize_t lora_decode(const uint16_t* symbols, size_t symbol_count,
     if (symbol_count % 2 != 0) return -EINVAL;
     if (symbol_count == 0) return 0;
     int err = -ENODEV;
-    lphy_hip_ctx* c = get_ctx(7, 125000, 1, 0, &err);
+    lphy_hip_ctx* c = decode_ctx(&err);
     if (!c) return err;
     lphy_frame_meta m{};
     int rc = lphy_hip_decode_host(c, symbols, symbol_count, out_bytes, &m);

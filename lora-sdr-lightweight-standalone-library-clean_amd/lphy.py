@@ -5,6 +5,13 @@ lib/liblphy_hip.so (built in-tree by the package Makefile) and exposes the
 batch entry points on device pointers (torch tensors) plus the host-buffer
 conveniences.  There is no fallback: when the library or a HIP device is
 missing, calls raise.
+
+lib/test/liblphy_hip.so is the test-only build (Makefile `test`): the same
+kernels with device index checks (-DLPHY_DEBUG_BOUNDS, counted in
+bounds_violations()) and the comparison flags F_EXACT_ROTATION /
+F_SCAN_FIRST / F_DEBUG_RECHECK (csrc/lphy_testing.h), which the product
+library rejects.  Demodulator(..., test_build=True) uses it; LPHY_LIB=test
+makes it the default (a whole test run under the index checks).
 """
 from __future__ import annotations
 
@@ -18,6 +25,8 @@ import numpy as np
 PKG = Path(__file__).resolve().parent
 LIB_DIR = PKG / "lib"
 HIP_SO = LIB_DIR / "liblphy_hip.so"
+TEST_SO = LIB_DIR / "test" / "liblphy_hip.so"
+DEFAULT_SO = TEST_SO if os.environ.get("LPHY_LIB") == "test" else HIP_SO
 SHIM_SO = LIB_DIR / "liblora_phy_amd.so"
 
 MODE_DEMODULATE = 0
@@ -29,10 +38,10 @@ F_STAGE_PROLOGUE = 4
 F_STAGE_SYMBOLS = 8
 F_STAGE_FINAL = 16
 F_UNFUSED = 32  # separate prologue / symbol launches (lphy_hip.h)
-F_EXACT_ROTATION = 64  # fused launch without the certified per-frame rotation table
-F_RESIDENT = 128  # fused launch: single-read CU-resident kernel where it applies (SF 7)
-F_SCAN_FIRST = 256  # fused launch, modes 1/2: whole-frame max-abs pre-scan (no speculation)
-F_DEBUG_RECHECK = 512  # separate launches: every estimated frame marked "open symbols" first (tests)
+# test-only build (csrc/lphy_testing.h; the product library returns -EINVAL):
+F_EXACT_ROTATION = 64  # every symbol with the reference's per-sample rotation
+F_SCAN_FIRST = 256  # modes 1/2: whole-frame max-abs pre-scan (no speculation)
+F_DEBUG_RECHECK = 512  # every symbol / estimated frame left to the exact re-run
 WINDOW_NONE = 0
 WINDOW_HANN = 1
 
@@ -59,7 +68,8 @@ _vp = C.c_void_p
 _sz = C.c_size_t
 
 EXPORTS = (
-    "lphy_hip_ctx_create", "lphy_hip_ctx_destroy", "lphy_hip_syms_per_frame",
+    "lphy_hip_ctx_create", "lphy_hip_ctx_destroy", "lphy_hip_ctx_share", "lphy_hip_ctx_reserve",
+    "lphy_hip_syms_per_frame", "lphy_hip_recheck_count", "lphy_hip_bounds_violations",
     "lphy_hip_demod_batch", "lphy_hip_decode_batch", "lphy_hip_estimate_batch",
     "lphy_hip_compensate", "lphy_hip_modulate_batch", "lphy_hip_demod_host",
     "lphy_hip_decode_host", "lphy_hip_estimate_host", "lphy_hip_compensate_host",
@@ -75,7 +85,7 @@ CODE_ENC84, CODE_DEC84, CODE_ENC74, CODE_DEC74 = 0, 1, 2, 3
 CODE_ENCP54, CODE_CHKP54, CODE_ENCP64, CODE_CHKP64 = 4, 5, 6, 7
 SUM_SX1272_CRC, SUM_HEADER, SUM_CHECKSUM8 = 0, 1, 2
 
-_LIB = None
+_LIBS: dict = {}
 
 
 class LphyError(RuntimeError):
@@ -85,11 +95,20 @@ class LphyError(RuntimeError):
         self.rc = rc
 
 
-def load(path: Path = HIP_SO) -> C.CDLL:
-    """Load liblphy_hip.so (raises if it was not built)."""
-    global _LIB
-    if _LIB is not None:
-        return _LIB
+def use(path) -> C.CDLL:
+    """Make the library at `path` the default of later load() / Demodulator
+    calls (experiment builds: tools/ubench) and load it."""
+    global DEFAULT_SO
+    DEFAULT_SO = Path(path)
+    return load(DEFAULT_SO)
+
+
+def load(path: Path | None = None) -> C.CDLL:
+    """Load liblphy_hip.so (raises if it was not built); `path` picks another
+    build (TEST_SO), default DEFAULT_SO."""
+    path = Path(path or DEFAULT_SO)
+    if str(path) in _LIBS:
+        return _LIBS[str(path)]
     if not path.exists():
         raise FileNotFoundError(f"{path} missing: build with __graft_entry__.build()")
     # One HIP runtime per process: torch ships its own libamdhip64 (SONAME
@@ -105,6 +124,9 @@ def load(path: Path = HIP_SO) -> C.CDLL:
     L.lphy_hip_ctx_create.argtypes = [C.POINTER(_vp), C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_int]
     L.lphy_hip_ctx_destroy.argtypes = [_vp]
     L.lphy_hip_ctx_destroy.restype = None
+    L.lphy_hip_ctx_share.argtypes = [C.POINTER(_vp), _vp, C.c_uint]
+    L.lphy_hip_ctx_reserve.argtypes = [_vp, _sz, _sz]
+    L.lphy_hip_bounds_violations.argtypes = [_vp, C.POINTER(C.c_ulonglong), C.c_int]
     L.lphy_hip_syms_per_frame.argtypes = [_vp, _sz, C.c_int]
     L.lphy_hip_syms_per_frame.restype = _sz
     L.lphy_hip_demod_batch.argtypes = [_vp, _vp, _sz, _sz, _vp, _vp, _vp, C.c_int, C.c_uint, _vp]
@@ -133,7 +155,7 @@ def load(path: Path = HIP_SO) -> C.CDLL:
     L.lphy_hip_lorawan_parse_batch.argtypes = [_vp, _sz, _sz, _vp, _sz, _vp, _sz, _vp, _vp, _vp]
     L.lphy_hip_lorawan_mic_host.argtypes = [C.c_int, _vp, C.c_int, C.c_uint32, C.c_uint32, _vp, _sz,
                                             C.POINTER(C.c_uint32)]
-    _LIB = L
+    _LIBS[str(path)] = L
     return L
 
 
@@ -173,10 +195,11 @@ class Demodulator:
     """One (sf, bw, osr, window) configuration on one HIP device."""
 
     def __init__(self, sf: int, bw_hz: int = 125000, osr: int = 1,
-                 window: int = WINDOW_NONE, device: int = 0):
-        self.lib = load()
+                 window: int = WINDOW_NONE, device: int = 0, test_build: bool = False,
+                 lib_path=None):
+        self.lib = load(lib_path or (TEST_SO if test_build else None))
         self.sf, self.N, self.bw_hz, self.osr = sf, 1 << sf, bw_hz, osr
-        self.device = device
+        self.window, self.device = window, device
         h = _vp()
         _chk(self.lib.lphy_hip_ctx_create(C.byref(h), device, sf, bw_hz, osr, window),
              "lphy_hip_ctx_create")
@@ -300,6 +323,17 @@ class Demodulator:
                                              out.ctypes.data, amplitude, sync),
              "lphy_hip_modulate_host")
         return out
+
+    def bounds_violations(self, reset: bool = True) -> int:
+        """Device index checks that failed since the last reset (test build
+        only: the product library returns -ENOTSUP).  Synchronises."""
+        n = C.c_ulonglong(0)
+        _chk(self.lib.lphy_hip_bounds_violations(self.ctx, C.byref(n), int(reset)),
+             "lphy_hip_bounds_violations")
+        return int(n.value)
+
+    def reserve(self, frames: int, frame_samples: int) -> None:
+        _chk(self.lib.lphy_hip_ctx_reserve(self.ctx, frames, frame_samples), "lphy_hip_ctx_reserve")
 
     def recheck_count(self, reset: bool = True) -> int:
         """Symbols the fused kernel re-ran with the exact rotation (device sync)."""

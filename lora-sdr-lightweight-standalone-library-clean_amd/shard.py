@@ -1,8 +1,9 @@
 """Multi-GPU layout of a demodulation batch: one process per GPU, frames
 sharded by index, no collective on the data path; the only exchange is the
-gather of decoded payloads (RCCL all_gather over xGMI; gloo on CPU in the
-tests).  Frames are independent, so scaling is weak: each rank owns its
-frames' IQ in its own HBM."""
+gather of each rank's results - symbols, decoded payloads and frame records,
+one contiguous slab per rank - to rank 0 (RCCL over xGMI, gloo
+on CPU in the tests).  Frames are independent, so scaling is weak: each rank
+owns its frames' IQ in its own HBM."""
 from __future__ import annotations
 
 import torch
@@ -37,50 +38,75 @@ def balanced_ranges(costs, world: int) -> list[tuple[int, int]]:
     return [(cuts[r], cuts[r + 1] - cuts[r]) for r in range(world)]
 
 
-def gather_payloads(local: torch.Tensor, frames: int, payload: int, total: int,
-                    group=None) -> torch.Tensor:
-    """All ranks' decoded payloads (uint8, frames*payload each, frame_range
-    order) concatenated on every rank.  Uneven shards are padded to the
-    largest shard for the collective and trimmed after."""
-    world = dist.get_world_size(group)
-    counts = [frame_range(total, world, r)[1] for r in range(world)]
-    assert frames == counts[dist.get_rank(group)]
-    cap = max(counts) * payload
-    buf = local.reshape(-1)
-    if buf.numel() != cap:
-        pad = torch.zeros(cap, dtype=torch.uint8, device=local.device)
-        pad[: buf.numel()] = buf
-        buf = pad
-    if dist.get_backend(group) == "gloo":
-        parts = [torch.empty_like(buf) for _ in range(world)]
-        dist.all_gather(parts, buf, group=group)
-        out = torch.cat(parts)
-    else:
-        out = torch.empty(world * cap, dtype=torch.uint8, device=local.device)
-        dist.all_gather_into_tensor(out, buf, group=group)
-    if all(c * payload == cap for c in counts):
-        return out
-    return torch.cat([out[r * cap: r * cap + counts[r] * payload] for r in range(world)])
+META_BYTES = 32  # lphy_frame_meta (include/lphy_hip.h)
 
 
-def gather_varlen(local: torch.Tensor, group=None) -> list[torch.Tensor]:
-    """All ranks' uint8 buffers of possibly different lengths (e.g. the
-    payloads of one SF bucket of a mixed-SF batch), in rank order, on every
-    rank: sizes first, then one padded all_gather."""
+def _al(n: int, a: int = 256) -> int:
+    return (n + a - 1) // a * a
+
+
+def slab_layout(counts, syms_per_frame: int, payload: int):
+    """Byte layout of one rank's results in a single buffer (the
+    u16 symbols, the decoded payload bytes and the 32-byte frame record per
+    frame): one part per entry of `counts` (a single-SF batch has one part,
+    a mixed-SF rank one per SF bucket), each [symbols | payloads | records],
+    every section 256-byte aligned.  Returns ([(frames, off_syms, off_pay,
+    off_meta)], bytes used)."""
+    parts, off = [], 0
+    for n in counts:
+        n = int(n)
+        s = off
+        off += _al(n * syms_per_frame * 2)
+        p = off
+        off += _al(n * payload)
+        m = off
+        off += _al(n * META_BYTES)
+        parts.append((n, s, p, m))
+    return parts, off
+
+
+class ResultSlab:
+    """A rank's demodulation outputs in one contiguous uint8 device buffer
+    (slab_layout), so the gather to rank 0 is a single collective per step.
+    `nbytes` pads the buffer to the largest rank's layout: every rank's
+    buffer then has the same size, as the collective needs."""
+
+    def __init__(self, counts, syms_per_frame: int, payload: int, device, nbytes: int = 0):
+        self.spf, self.payload = syms_per_frame, payload
+        self.parts, self.used = slab_layout(counts, syms_per_frame, payload)
+        self.nbytes = max(self.used, int(nbytes))
+        self.buf = torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
+
+    def views(self, i: int = 0):
+        """(int16 symbols, uint8 payloads, uint8 frame records) of part i."""
+        n, s, p, m = self.parts[i]
+        b = self.buf
+        return (b[s:s + n * self.spf * 2].view(torch.int16), b[p:p + n * self.payload],
+                b[m:m + n * META_BYTES])
+
+
+def unpack_slab(buf, counts, syms_per_frame: int, payload: int):
+    """Host view of a gathered slab: per part (uint16 symbols [n, spf],
+    uint8 payloads [n, payload], uint8 records [n, 32])."""
+    import numpy as np
+    a = buf.cpu().numpy() if hasattr(buf, "cpu") else np.asarray(buf, np.uint8)
+    out = []
+    for n, s, p, m in slab_layout(counts, syms_per_frame, payload)[0]:
+        out.append((a[s:s + n * syms_per_frame * 2].view(np.uint16).reshape(n, syms_per_frame),
+                    a[p:p + n * payload].reshape(n, payload),
+                    a[m:m + n * META_BYTES].reshape(n, META_BYTES)))
+    return out
+
+
+def gather_slab(buf: torch.Tensor, dst: int = 0, group=None, async_op: bool = False):
+    """Every rank's slab (equal sizes) to rank `dst`: RCCL gather over xGMI
+    (ncclSend/ncclRecv in one group; gloo on CPU).  Returns (list of world
+    buffers on dst, None elsewhere; the work handle when async_op)."""
     world = dist.get_world_size(group)
-    buf = local.reshape(-1)
-    n = torch.tensor([buf.numel()], dtype=torch.int64, device=local.device)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n, group=group)
-    sizes = [int(x.item()) for x in sizes]
-    cap = max(sizes) if sizes else 0
-    if buf.numel() != cap:
-        pad = torch.zeros(cap, dtype=torch.uint8, device=local.device)
-        pad[: buf.numel()] = buf
-        buf = pad
-    parts = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(parts, buf, group=group)
-    return [p[:k] for p, k in zip(parts, sizes)]
+    out = ([torch.empty_like(buf) for _ in range(world)]
+           if dist.get_rank(group) == dst else None)
+    work = dist.gather(buf, out, dst=dst, group=group, async_op=async_op)
+    return out, work
 
 
 def mixed_plan(total: int, world: int, rank: int, seed: int = 0xC3, payload: int = 32,

@@ -16,6 +16,25 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
+def pytest_sessionfinish(session, exitstatus):
+    """Under LPHY_LIB=test (the whole suite on the test build), any failed
+    device index check fails the session (tests/test_gpu_bounds.py)."""
+    if os.environ.get("LPHY_LIB") != "test":
+        return
+    try:
+        import torch
+        if not torch.cuda.is_available():
+            return
+        import lphy
+        n = lphy.Demodulator(7).bounds_violations()
+    except Exception as e:  # the library or device is missing: nothing ran on it
+        print(f"\nbounds check skipped: {e}")
+        return
+    print(f"\ndevice index checks failed over the session: {n}")
+    if n:
+        session.exitstatus = 1
+
+
 @pytest.fixture(scope="session")
 def oracle():
     from checkers import Oracle

@@ -4,13 +4,15 @@ separate launches) and SF <= 10 with LPHY_F_UNFUSED:
 * two lphy_hip_demod_batch calls on ONE context issued on two streams at
   once give the single-stream results bit for bit (the SF 11-12
   speculation records are per-call scratch, not context state);
-* LPHY_F_DEBUG_RECHECK marks every estimated frame "has open symbols"
-  (kStatusRecheck) before the symbol kernel runs - the state a symbol may
-  observe when another workgroup's certificate failed first - so the
-  round-2 race (such a symbol skipped and never written) is exercised on
-  every frame deterministically; the output buffer is poisoned first and no
-  poison may survive in any frame.  Every frame is compared with the
-  oracle."""
+* LPHY_F_DEBUG_RECHECK, separate launches: marks every estimated frame
+  "has open symbols" (kStatusRecheck) before the symbol kernel runs - the
+  state a symbol may observe when another workgroup's certificate failed
+  first - so the round-2 race (such a symbol skipped and never written) is
+  exercised on every frame deterministically; fused kernels (k_frames,
+  k_wave): every symbol is left uncertified, so k_post's exact re-run
+  produces all of them (lphy_hip_recheck_count must cover every data
+  symbol).  The output buffer is poisoned first and no poison may survive in
+  any frame.  Every frame is compared with the oracle."""
 import numpy as np
 import pytest
 import torch
@@ -95,9 +97,17 @@ def test_forced_recheck_no_symbol_lost(oracle, lphy, sf, mode, unfused):
     base = lphy.F_DECODE | (lphy.F_UNFUSED if unfused else 0)
     st = torch.cuda.current_stream().cuda_stream
     plain = _host(lphy, *_dev_run(lphy, d, x_t, nf, fs, mode, base, st, poison=False), nf, per)
-    forced = _host(lphy, *_dev_run(lphy, d, x_t, nf, fs, mode, base | lphy.F_DEBUG_RECHECK, st), nf, per)
+    dt = lphy.Demodulator(sf, test_build=True)  # LPHY_F_DEBUG_RECHECK: test build only
+    dt.recheck_count(reset=True)
+    forced = _host(lphy, *_dev_run(lphy, dt, x_t, nf, fs, mode, base | lphy.F_DEBUG_RECHECK, st), nf, per)
+    assert dt.bounds_violations() == 0
     live = forced[2]["status"] == 0
     assert live.all()
+    if not unfused:
+        # the fused kernels leave every symbol uncertified under the flag:
+        # k_post's exact re-run must have produced each one
+        n = dt.recheck_count()
+        assert n >= nf * per, f"{n} exact re-runs for {nf * per} data symbols"
     assert not (forced[0] == POISON).any(), "a symbol was never written"
     np.testing.assert_array_equal(forced[0], plain[0])
     np.testing.assert_array_equal(forced[1], plain[1])

@@ -57,3 +57,29 @@ def test_lorawan_api_transcript_matches_reference(tmp_path):
     assert b[0] == "mic kat 82b5c3d6"
     bad = [(x, y) for x, y in zip(a, b) if x != y]
     assert not bad, "\n".join(f"ours: {x[:300]}\nref:  {y[:300]}" for x, y in bad[:5])
+
+
+T_REF_PROBE = ROOT / "oracle" / "_ref" / "lora_phy_threads_probe_ref"
+
+
+@pytest.mark.parametrize("threads,sf,frames", [(2, 9, 10), (4, 7, 8), (2, 12, 3)])
+def test_cxx_api_threads_match_reference(tmp_path, threads, sf, frames):
+    """Separate workspaces on separate threads at the same SF, concurrently
+    (tests/cpp/lora_phy_threads_probe.cpp): the drop-in gives each workspace
+    its own context (stream + staging) at init, so the threads run side by
+    side, and each thread's transcript equals the reference's."""
+    if not T_REF_PROBE.exists():
+        pytest.skip("reference threads probe not built (oracle/Makefile tprobe)")
+    exe = tmp_path / "tprobe_amd"
+    subprocess.run(["g++", "-O2", "-std=gnu++17", "-ffp-contract=off", f"-I{ROOT / 'include'}",
+                    "-o", str(exe), str(ROOT / "tests" / "cpp" / "lora_phy_threads_probe.cpp"),
+                    f"-L{PKG / 'lib'}", "-llora_phy_amd", f"-Wl,-rpath,{PKG / 'lib'}", "-lpthread"], check=True)
+    args = [str(threads), str(sf), str(frames)]
+    ours = subprocess.run([str(exe)] + args, capture_output=True, text=True, timeout=300)
+    assert ours.returncode == 0, ours.stderr
+    ref = subprocess.run([str(T_REF_PROBE)] + args, capture_output=True, text=True, timeout=300)
+    assert ref.returncode == 0, ref.stderr
+    a, b = ours.stdout.splitlines(), ref.stdout.splitlines()
+    assert len(b) == threads * frames * 2 and len(a) == len(b)
+    bad = [(x, y) for x, y in zip(a, b) if x != y]
+    assert not bad, "\n".join(f"ours: {x[:300]}\nref:  {y[:300]}" for x, y in bad[:5])

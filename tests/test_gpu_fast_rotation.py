@@ -35,11 +35,15 @@ def _impaired(oracle, sf, nf, seed, plen=32, snr_db=None, cfo_bins=0.4, gain=(1.
 
 
 def _both(lphy, d, iq, mode):
+    """The product library's run and the exact rotation's (test build:
+    LPHY_F_EXACT_ROTATION is not in the product library)."""
     nf, fs = iq.shape
     a = d.demod_host(iq, nf, fs, mode, lphy.F_DECODE)
     n_fast = d.recheck_count(reset=True)
-    b = d.demod_host(iq, nf, fs, mode, lphy.F_DECODE | lphy.F_EXACT_ROTATION)
-    n_exact = d.recheck_count(reset=True)
+    dt = lphy.Demodulator(d.sf, d.bw_hz, d.osr, d.window, test_build=True)
+    b = dt.demod_host(iq, nf, fs, mode, lphy.F_DECODE | lphy.F_EXACT_ROTATION)
+    n_exact = dt.recheck_count(reset=True)
+    assert dt.bounds_violations() == 0
     np.testing.assert_array_equal(a[0], b[0])
     np.testing.assert_array_equal(a[1], b[1])
     np.testing.assert_array_equal(a[2].view(np.uint8), b[2].view(np.uint8))

@@ -63,7 +63,9 @@ def test_speculative_normalisation(oracle, lphy, sf, nf, mode):
     fs = iq.shape[1]
     d = lphy.Demodulator(sf)
     a = d.demod_host(iq, nf, fs, mode, lphy.F_DECODE)
-    b = d.demod_host(iq, nf, fs, mode, lphy.F_DECODE | lphy.F_SCAN_FIRST)
+    dt = lphy.Demodulator(sf, test_build=True)  # the pre-scan schedule: test build only
+    b = dt.demod_host(iq, nf, fs, mode, lphy.F_DECODE | lphy.F_SCAN_FIRST)
+    assert dt.bounds_violations() == 0
     np.testing.assert_array_equal(a[0], b[0])
     np.testing.assert_array_equal(a[1], b[1])
     np.testing.assert_array_equal(a[2].view(np.uint8), b[2].view(np.uint8))
@@ -76,6 +78,46 @@ def test_speculative_normalisation(oracle, lphy, sf, nf, mode):
         assert a[2]["sync_word"][f] == osync, ctx
         assert _bits(a[2]["cfo"][f]) == _bits(omet[0]), ctx
         assert _bits(a[2]["time_offset"][f]) == _bits(omet[1]), ctx
+
+
+@pytest.mark.parametrize("sf", [9, 10])
+@pytest.mark.parametrize("how", ["hann", "exact_rotation"])
+def test_estimate_maxabs_in_symbol0(oracle, lphy, sf, how):
+    """Frames whose max-abs lies in sync symbol 0, with symbol 1's own
+    maximum smaller but still > 1: both estimate units must be scaled by the
+    frame's (symbol 0's) maximum, LoRaDemod.cpp:60-78.  Hann windows and
+    LPHY_F_EXACT_ROTATION route SF 9-10 modes 1/2 to k_frames, whose EB tiles
+    fold the estimate symbols' max-abs only when both units share a tile
+    (SF <= 9); at SF 10 the two-symbol scan must supply it."""
+    N = 1 << sf
+    rng = np.random.default_rng(1000 + sf)
+    base = oracle.modulate(oracle.encode(bytes(range(12))), sf)
+    t = np.arange(base.size, dtype=np.float64)
+    nf = 24
+    iq = np.zeros((nf, base.size), np.complex64)
+    for f in range(nf):
+        x = base * np.exp(2j * np.pi * rng.uniform(-0.4, 0.4) / N * t) * (1.5 + 0.1 * (f % 5))
+        x = x + 0.05 * (rng.standard_normal(base.size) + 1j * rng.standard_normal(base.size))
+        x = x.astype(np.complex64)
+        j = int(rng.integers(0, N))
+        x[j] = np.complex64(complex(3.0 + 0.25 * (f % 4), -0.5))  # the frame's maximum, symbol 0
+        iq[f] = x
+    window = lphy.WINDOW_HANN if how == "hann" else lphy.WINDOW_NONE
+    flags = lphy.F_DECODE | (lphy.F_EXACT_ROTATION if how == "exact_rotation" else 0)
+    d = lphy.Demodulator(sf, window=window, test_build=how == "exact_rotation")
+    syms, _, meta = d.demod_host(iq, nf, iq.shape[1], 2, flags)
+    for f in range(nf):
+        dech = oracle.dechirp(iq[f], sf)
+        m0 = np.max(np.maximum(np.abs(dech[:N].real), np.abs(dech[:N].imag)))
+        m1 = np.max(np.maximum(np.abs(dech[N:2 * N].real), np.abs(dech[N:2 * N].imag)))
+        assert m0 > m1 > 1.0
+        r, osyms, osync, omet = oracle.lora_demodulate(dech, sf, hann=how == "hann")
+        ctx = f"sf {sf} {how} frame {f}"
+        assert meta["status"][f] == 0, ctx
+        assert _bits(meta["cfo"][f]) == _bits(omet[0]), ctx
+        assert _bits(meta["time_offset"][f]) == _bits(omet[1]), ctx
+        assert meta["sync_word"][f] == osync, ctx
+        np.testing.assert_array_equal(syms[f], osyms, err_msg=ctx)
 
 
 def test_speculation_off_without_scratch(oracle, lphy):

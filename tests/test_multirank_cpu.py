@@ -1,11 +1,17 @@
 """The N > 1 path on CPU: world-size-2 gloo process group, frames sharded by
 index (shard.frame_range), each rank demodulating its own frames, decoded
-payloads gathered (shard.gather_payloads) and compared on every rank with the
-whole batch's payloads.  The CPU oracle stands in for the per-rank HIP
+results gathered to rank 0 in one slab per rank (shard.gather_slab: symbols,
+payloads, frame records) and compared with the whole batch's.  The
+launcher of `bench.py --gpus N` is driven the same way (tests/rank_worker.py).  The CPU oracle stands in for the per-rank HIP
 launch here (test infrastructure); the GPU path is the same C-ABI call per
 rank (bench.py)."""
+import json
 import os
 import socket
+import subprocess
+import sys
+import time
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -38,13 +44,23 @@ def _worker(rank, world, port, total, sf, plen, q):
         o = Oracle()
         pays, iqs = _frames(o, total, sf, plen)
         first, count = shard.frame_range(total, world, rank)
-        local = np.zeros((count, plen), np.uint8)
+        cap = max(shard.slab_layout([shard.frame_range(total, world, r)[1]], 2 * plen, plen)[1]
+                  for r in range(world))
+        slab = shard.ResultSlab([count], 2 * plen, plen, torch.device("cpu"), cap)
+        _, pv, _ = slab.views(0)
         for i in range(count):
             x = o.dechirp(iqs[first + i], sf)
             r, syms, sync, _ = o.lora_demodulate(x, sf)
-            local[i] = o.lora_decode(syms)[1]
-        got = shard.gather_payloads(torch.from_numpy(local.reshape(-1).copy()), count, plen, total)
-        q.put((rank, bool(np.array_equal(got.numpy().reshape(total, plen), pays))))
+            pv[i * plen:(i + 1) * plen] = torch.from_numpy(o.lora_decode(syms)[1].copy())
+        parts, _ = shard.gather_slab(slab.buf)
+        ok = True
+        if rank == 0:
+            got = np.concatenate([shard.unpack_slab(parts[r], [shard.frame_range(total, world, r)[1]],
+                                                    2 * plen, plen)[0][1] for r in range(world)])
+            ok = bool(np.array_equal(got, pays))
+        else:
+            ok = parts is None
+        q.put((rank, ok))
     finally:
         dist.destroy_process_group()
 
@@ -64,6 +80,45 @@ def test_two_rank_shard_and_gather(total):
     assert res == {0: True, 1: True}
 
 
+def test_launcher_two_ranks_gather_full_results(tmp_path):
+    """bench.launch_ranks sets up two ranks the way `bench.py --gpus 2` does
+    (child processes with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*); each
+    rank fills a ResultSlab and gathers it to rank 0, which checks every
+    frame's symbols, payload and 32-byte frame record against the oracle
+    (tests/rank_worker.py)."""
+    import bench
+    out = tmp_path / "gather.json"
+    worker = Path(__file__).resolve().parent / "rank_worker.py"
+    rc = bench.launch_ranks([sys.executable, str(worker), str(out), "7"], 2, devices=2)
+    assert rc == 0
+    res = json.loads(out.read_text())
+    assert res == {"world": 2, "frames": 7, "ok": 7, "bad": [], "all_ok": True}
+
+
+def test_launcher_failing_rank_ends_job():
+    import bench
+    code = ("import os, sys, time\n"
+            "sys.exit(5) if os.environ['RANK'] == '1' else time.sleep(60)")
+    t0 = time.time()
+    assert bench.launch_ranks([sys.executable, "-c", code], 2, devices=2) == 5
+    assert time.time() - t0 < 30
+
+
+def test_bench_gpus_without_devices_fails_loudly():
+    """`bench.py --gpus 2` on a node with fewer GPUs (none here, one on a
+    gpurun box) exits non-zero before timing anything; so does a WORLD_SIZE
+    that disagrees with --gpus."""
+    bench = str(Path(__file__).resolve().parent.parent / "bench.py")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, bench, "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                       env={**env, "HIP_VISIBLE_DEVICES": "0"}, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "needs 2 GPUs" in r.stderr, r.stderr
+    r = subprocess.run([sys.executable, bench, "--gpus", "4", "--steps", "1"],
+                       env={**env, "WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"},
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr, r.stderr
+
+
 @pytest.mark.parametrize("total,world", [(10, 3), (65536, 8), (1, 2), (0, 4), (1000000, 8)])
 def test_frame_range_partitions(total, world):
     spans = [shard.frame_range(total, world, r) for r in range(world)]
@@ -74,30 +129,22 @@ def test_frame_range_partitions(total, world):
     assert max(n for _, n in spans) - min(n for _, n in spans) <= 1
 
 
-def _varlen_worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        local = torch.arange(3 + 4 * rank, dtype=torch.uint8)
-        parts = shard.gather_varlen(local)
-        q.put((rank, [p.tolist() for p in parts]))
-    finally:
-        dist.destroy_process_group()
-
-
-def test_gather_varlen_two_ranks():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_varlen_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = dict(q.get(timeout=120) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    want = [list(range(3)), list(range(7))]
-    assert res == {0: want, 1: want}
+@pytest.mark.parametrize("counts", [[7], [3, 0, 5], [0]])
+def test_slab_layout_views_roundtrip(counts):
+    spf, plen = 64, 32
+    slab = shard.ResultSlab(counts, spf, plen, torch.device("cpu"), nbytes=1 << 16)
+    assert slab.nbytes >= slab.used
+    for i, n in enumerate(counts):
+        s, p, m = slab.views(i)
+        assert s.dtype == torch.int16 and s.numel() == n * spf
+        s.copy_(torch.arange(n * spf, dtype=torch.int16) + i)
+        p.fill_(10 + i)
+        m.fill_(20 + i)
+    for i, (gs, gp, gm) in enumerate(shard.unpack_slab(slab.buf, counts, spf, plen)):
+        n = counts[i]
+        assert gs.shape == (n, spf) and gp.shape == (n, plen) and gm.shape == (n, 32)
+        assert (gs.reshape(-1) == np.arange(n * spf) + i).all()
+        assert (gp == 10 + i).all() and (gm == 20 + i).all()
 
 
 @pytest.mark.parametrize("world", [1, 2, 8])

@@ -28,7 +28,7 @@ ap.add_argument("--modes", default="0,2")
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--so", default="")
 ap.add_argument("--unfused", action="store_true")
-ap.add_argument("--exact", action="store_true")
+ap.add_argument("--exact", action="store_true", help="LPHY_F_EXACT_ROTATION (test build: --so .../lib/test/liblphy_hip.so)")
 ap.add_argument("--burst", action="store_true", help="time the reps back-to-back (one event pair)")
 ap.add_argument("--flags", type=int, default=0, help="extra LPHY_F_* bits (e.g. 256 = SCAN_FIRST)")
 ap.add_argument("--check", action="store_true", help="compare outputs across builds")
@@ -52,9 +52,7 @@ flags |= a.flags
 ref = {}
 dems = []
 for so in sos:
-    lphy._LIB = None
-    lphy.load(so)
-    dems.append((so, lphy.Demodulator(a.sf)))
+    dems.append((so, lphy.Demodulator(a.sf, lib_path=so)))
 st = torch.cuda.current_stream().cuda_stream
 dems[0][1].modulate_batch(syms_in, a.frames, 64, iq, 1.0, 0x12, st)
 out = torch.zeros(a.frames * 64, dtype=torch.int16, device=dev)

@@ -18,8 +18,7 @@ for name, flags in variants.items():
     so = os.path.join(ROOT, "tools", "ubench", f"ablate_{name}.so")
     if not os.path.exists(so):
         subprocess.run(f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -fPIC -shared {flags} -I{ROOT}/include -I{PKG}/csrc -o {so} {PKG}/csrc/lphy_hip.hip", shell=True, check=True)
-    lphy._LIB = None
-    lib = lphy.load(__import__("pathlib").Path(so))
+    lib = lphy.use(__import__("pathlib").Path(so))
     d = lphy.Demodulator(sf)
     rng = np.random.default_rng(1)
     pay = rng.integers(0, 256, (frames, 32), dtype=np.uint8)

@@ -14,12 +14,11 @@ import bench  # noqa: E402
 sf, name = int(sys.argv[1]), sys.argv[2]
 mode = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 lphy = bench.lphy
-lphy._LIB = None
-lphy.load(Path(__file__).resolve().parent / f"var_{name}.so")
+lphy.use(Path(__file__).resolve().parent / f"var_{name}.so")
 wl = bench.Workload(sf, 125000, bench.DEFAULT_FRAMES[sf], 0, torch.device("cuda:0"))
 flags = lphy.F_DECODE | lphy.F_STAGE_PROLOGUE | lphy.F_STAGE_SYMBOLS
 ms = wl._event_ms(mode, flags, 10)
-lib = lphy._LIB
+lib = lphy.load()
 out = (C.c_ulonglong * 8)()
 lib.lphy_hip_phase_cycles.argtypes = [C.c_void_p, C.c_void_p]
 lib.lphy_hip_phase_cycles(wl.dem.ctx, out)

@@ -34,8 +34,7 @@ def run(sf, names):
     import bench
     lphy = bench.lphy
     for name in names:
-        lphy._LIB = None
-        lphy.load(HERE / f"var_{name}.so")
+        lphy.use(HERE / f"var_{name}.so")
         wl = bench.Workload(sf, 125000, bench.DEFAULT_FRAMES[sf], 0, torch.device("cuda:0"))
         mode = lphy.MODE_DECHIRP_LORA_DEMODULATE
         D = lphy.F_DECODE
@@ -45,7 +44,7 @@ def run(sf, names):
         sym = wl._event_ms(mode, D | lphy.F_UNFUSED | lphy.F_STAGE_SYMBOLS, 10)
         fin = wl._event_ms(mode, D | lphy.F_STAGE_FINAL, 10)
         extra = ""
-        lib = lphy._LIB
+        lib = lphy.load()
         if hasattr(lib, "lphy_hip_phase_cycles"):
             import ctypes as C
             out = (C.c_ulonglong * 8)()
