@@ -193,12 +193,16 @@ int lphy_hip_modulate_host(lphy_hip_ctx* ctx, const uint16_t* h_syms,
  * stdin (runners/rx_runner.cpp:61-79) - from file descriptor `fd` until EOF
  * or `max_frames` frames, whichever comes first, as consecutive frames of
  * `frame_samples` samples, and demodulates them (lphy_hip_demod_batch,
- * `mode`, `flags`) in chunks of `chunk_frames`: the read of one chunk into
+ * `mode`, `flags`) in chunks of `chunk_frames` (0: whole frames of about
+ * 64 MiB): the read of one chunk into
  * pinned host memory and its H2D copy (copy stream) overlap the
  * demodulation of the previous one (compute stream).  Results land in the
  * caller's host arrays in stream order (frame f at h_syms +
  * f*lphy_hip_syms_per_frame, h_bytes + f*(syms/2) with LPHY_F_DECODE,
- * h_meta + f).  `max_frames` is their capacity in frames and is required
+ * h_meta + f).  A seekable fd is read by a pool of reader threads
+ * (LPHY_STREAM_READERS, default one per usable CPU but one); the pinned
+ * slots and streams stay with the context for its next call.
+ * `max_frames` is their capacity in frames and is required
  * (0 gives -EINVAL): reading stops there and the rest of the stream is left
  * unread on `fd` for a later call.  Synchronous.
  * *frames_out = whole frames demodulated; *tail_bytes (optional) = bytes of

@@ -85,6 +85,10 @@ struct lphy_hip_ctx {
     void* d_stage = nullptr;
     unsigned long long* d_counters = nullptr;  // [0] rechecks, [1..8] phase clocks (experiments)
     size_t stage_bytes = 0;
+    // the streaming entry point's pinned slots and streams (lphy_stream.hip),
+    // made by its first call, kept for the next ones, freed with the context
+    void* stream_ext = nullptr;
+    void (*stream_ext_free)(void*) = nullptr;
     // (per-call scratch of the device entry points - the SF 11-12 speculation
     // records, the producer's phases, the compensation's shift buffer - comes
     // from the stream-ordered allocator on the caller's stream, so concurrent
@@ -271,6 +275,18 @@ const char* lphy_hip_version(void) {
 // streaming ingestion in lphy_stream.hip.
 int lphy_hip_ctx_device(const lphy_hip_ctx* c) { return c ? c->device : -1; }
 
+// Internal: the streaming ingestion's state kept with the context (made by
+// `make` on first use, released by `destroy` with the context).
+void* lphy_hip_ctx_stream_ext(lphy_hip_ctx* c, void* (*make)(), void (*destroy)(void*)) {
+    if (!c) return nullptr;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->stream_ext) {
+        c->stream_ext = make();
+        c->stream_ext_free = destroy;
+    }
+    return c->stream_ext;
+}
+
 namespace {
 // A context's own state: the host entry points' stream and the counters
 // (the tables are set by the caller).
@@ -376,6 +392,7 @@ void lphy_hip_ctx_destroy(lphy_hip_ctx* c) {
         (void)hipStreamSynchronize(c->stream);
         (void)hipStreamDestroy(c->stream);
     }
+    if (c->stream_ext && c->stream_ext_free) c->stream_ext_free(c->stream_ext);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->d_counters) (void)hipFree(c->d_counters);
     c->tab.reset();  // the tables go with the last context holding them

@@ -594,12 +594,12 @@ __device__ __forceinline__ void iq_check(const DemodArgs& A, unsigned long long 
 
 __device__ __forceinline__ void store_symbol(const DemodArgs& A, const SymCtx& c, uint16_t idx) {
     bound_check(c.f, (long long)A.frames);
-    bound_check(c.have_sync ? (long long)c.s - 2 : (long long)c.s, (long long)A.out_per_frame);
     if (c.have_sync && c.s < 2) {
         if (c.s == 0) A.meta[c.f].sw0 = idx;
         else A.meta[c.f].sw1 = idx;
     } else {
         const unsigned o = c.have_sync ? c.s - 2 : c.s;
+        bound_check(o, (long long)A.out_per_frame);
         A.syms[(unsigned long long)c.f * A.out_per_frame + o] = idx;
     }
 }
@@ -2344,6 +2344,7 @@ __global__ __launch_bounds__(kTile) void k_post(DemodArgs A, FinalArgs F, int fi
 }
 
 #include "lphy_wave.h"
+#include "lphy_wave2.h"
 
 // ---------------------------------------------------------------------------
 // lora_modulate (LoRaMod.cpp:8-43 + ChirpGenerator.hpp:24-51), bit-exact.
@@ -2589,10 +2590,31 @@ int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symb
 
 // Fused SF 11-12 path (lphy_wave.h): one 256-thread workgroup per CU (its
 // LDS), four independent waves each.
+// k_wave2 (lphy_wave2.h, two waves per SIMD) unless LPHY_WAVE_V1=1 (A/B:
+// the one-wave-per-SIMD k_wave)
+inline bool wave_v1() {
+    static int env = -1;
+    if (env < 0) {
+        const char* e = getenv("LPHY_WAVE_V1");
+        env = (e && e[0] == '1') ? 1 : 0;
+    }
+    return env == 1;
+}
+
 template <int SF, int MODE>
 int launch_wave_mode(const DemodArgs& A, hipStream_t st) {
     FrameArgs P{};
     P.A = A;
+    if (!wave_v1()) {
+        constexpr unsigned WPB = W2Lds<SF, MODE>::WPB;
+        unsigned long long blocks = (unsigned long long)cu_count();
+        const unsigned long long need = (A.frames + WPB - 1) / WPB;
+        if (blocks > need) blocks = need;
+        P.waves = (unsigned)(blocks * WPB);
+        hipLaunchKernelGGL((k_wave2<SF, MODE>), dim3((unsigned)blocks), dim3(64 * WPB), 0, st, P);
+        HIP_OK(hipGetLastError());
+        return 0;
+    }
     unsigned long long blocks = (unsigned long long)cu_count();
     const unsigned long long need = (A.frames + WGeo<SF>::WPB - 1) / WGeo<SF>::WPB;
     if (blocks > need) blocks = need;

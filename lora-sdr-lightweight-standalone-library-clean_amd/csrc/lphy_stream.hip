@@ -18,15 +18,20 @@
 #include <hip/hip_runtime.h>
 
 #include <cerrno>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
+#include <sched.h>
 #include <unistd.h>
 
 #include "../../include/lphy_hip.h"
 
-extern "C" int lphy_hip_ctx_device(const lphy_hip_ctx* c);  // lphy_hip.hip
+extern "C" int lphy_hip_ctx_device(const lphy_hip_ctx* c);  // lphy_hip.hip (internal)
+extern "C" void* lphy_hip_ctx_stream_ext(lphy_hip_ctx* c, void* (*make)(), void (*destroy)(void*));
 
 namespace {
 
@@ -42,6 +47,7 @@ namespace {
     } while (0)
 
 constexpr int NSLOT = 3;
+constexpr size_t kAutoChunkBytes = size_t(64) << 20;  // chunk_frames = 0: ~64 MiB chunks
 
 // Fill buf with up to `want` bytes from fd; stops early only at EOF.
 // Returns the byte count, or -errno.
@@ -59,60 +65,138 @@ long long read_full(int fd, char* buf, size_t want) {
     return (long long)got;
 }
 
-// A seekable fd (a file) is read by kReaders threads with pread, each a
-// contiguous part of the chunk (one thread's memcpy out of the page cache
-// runs at ~5 GB/s, a tenth of PCIe); a pipe or a socket is read in order.
-// The fd's offset is left after the bytes consumed, as read() would.
-constexpr int kReaders = 8;
+// The CPUs this process may use: the affinity mask, capped by the cgroup
+// CPU quota (a GPU box reports the whole host but grants a share of it).
+int usable_cpus() {
+    int n = (int)std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        long long period = 0;
+        if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+            const long long quota = atoll(q);
+            const int c = (int)((quota + period - 1) / period);
+            if (c > 0 && c < n) n = c;
+        }
+        fclose(f);
+    }
+    return n > 0 ? n : 1;
+}
+
+// A seekable fd (a file) is read by a pool of reader threads with pread,
+// each a contiguous part of the chunk (one thread's copy out of the page
+// cache runs at ~3 GB/s, a twentieth of PCIe); a pipe or a socket is read
+// in order.  The fd's offset is left after the bytes consumed, as read()
+// would.  Readers: LPHY_STREAM_READERS, default one per usable CPU but one
+// (the calling thread drives the GPU), at most 32.
 constexpr size_t kParMin = size_t(4) << 20;  // below this one read() suffices
 
-long long read_chunk(int fd, bool seekable, char* buf, size_t want) {
-    if (!seekable || want < kParMin) return read_full(fd, buf, want);
-    const off_t base = ::lseek(fd, 0, SEEK_CUR);
-    if (base < 0) return read_full(fd, buf, want);
-    const size_t part = (want + kReaders - 1) / kReaders;
-    std::vector<long long> got(kReaders, 0);
-    std::vector<std::thread> th;
-    int parts = 0;
-    for (int k = 0; k < kReaders; ++k) {
-        const size_t o = (size_t)k * part;
-        if (o >= want) break;
-        const size_t n = want - o < part ? want - o : part;
-        auto part_read = [&, k, o, n] {
-            size_t g = 0;
-            while (g < n) {
-                const ssize_t r = ::pread(fd, buf + o + g, n - g, base + (off_t)(o + g));
+class ReaderPool {
+  public:
+    explicit ReaderPool(int n) {
+        for (int k = 0; k < n; ++k) {
+            try {
+                th_.emplace_back([this, k] { run(k); });
+            } catch (...) {  // no exception may cross the C ABI: fewer readers
+                break;
+            }
+        }
+    }
+    ~ReaderPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int size() const { return (int)th_.size(); }
+    // read [base, base + want) of fd into buf with all readers; returns the
+    // bytes of the contiguous prefix read (short at EOF) or -errno
+    long long read(int fd, off_t base, char* buf, size_t want) {
+        const int n = size();
+        if (n == 0) return -EAGAIN;
+        std::unique_lock<std::mutex> lk(mu_);
+        fd_ = fd;
+        base_ = base;
+        buf_ = buf;
+        want_ = want;
+        part_ = (want + n - 1) / n;
+        got_.assign(n, 0);
+        pending_ = n;
+        ++gen_;
+        cv_.notify_all();
+        done_cv_.wait(lk, [this] { return pending_ == 0; });
+        size_t total = 0;
+        for (int k = 0; k < n; ++k) {
+            if (got_[k] < 0) return got_[k];
+            total += (size_t)got_[k];
+            const size_t o = (size_t)k * part_;
+            const size_t len = o >= want ? 0 : (want - o < part_ ? want - o : part_);
+            if ((size_t)got_[k] < len) break;
+        }
+        return (long long)total;
+    }
+
+  private:
+    void run(int k) {
+        unsigned long long seen = 0;
+        for (;;) {
+            int fd;
+            off_t base;
+            char* buf;
+            size_t o, len;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                fd = fd_;
+                base = base_;
+                buf = buf_;
+                o = (size_t)k * part_;
+                len = o >= want_ ? 0 : (want_ - o < part_ ? want_ - o : part_);
+            }
+            long long g = 0;
+            while ((size_t)g < len) {
+                const ssize_t r = ::pread(fd, buf + o + g, len - (size_t)g, base + (off_t)(o + (size_t)g));
                 if (r == 0) break;
                 if (r < 0) {
                     if (errno == EINTR) continue;
-                    got[k] = -(long long)errno;
-                    return;
+                    g = -(long long)errno;
+                    break;
                 }
-                g += (size_t)r;
+                g += r;
             }
-            got[k] = (long long)g;
-        };
-        // no exception may cross the C ABI: when a thread cannot be started
-        // (std::system_error under a thread limit) this thread reads the part
-        try {
-            th.emplace_back(part_read);
-        } catch (...) {
-            part_read();
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                got_[k] = g;
+                if (--pending_ == 0) done_cv_.notify_one();
+            }
         }
-        ++parts;
     }
-    for (auto& t : th) t.join();
-    // the bytes read are the contiguous prefix up to the first short part (EOF)
-    size_t total = 0;
-    for (int k = 0; k < parts; ++k) {
-        if (got[k] < 0) return got[k];
-        total += (size_t)got[k];
-        const size_t o = (size_t)k * part;
-        const size_t n = want - o < part ? want - o : part;
-        if ((size_t)got[k] < n) break;
-    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    bool stop_ = false;
+    unsigned long long gen_ = 0;
+    int fd_ = -1;
+    off_t base_ = 0;
+    char* buf_ = nullptr;
+    size_t want_ = 0, part_ = 0;
+    std::vector<long long> got_;
+    int pending_ = 0;
+};
+
+long long read_chunk(ReaderPool* pool, int fd, bool seekable, char* buf, size_t want) {
+    if (!seekable || want < kParMin || !pool || pool->size() == 0) return read_full(fd, buf, want);
+    const off_t base = ::lseek(fd, 0, SEEK_CUR);
+    if (base < 0) return read_full(fd, buf, want);
+    const long long total = pool->read(fd, base, buf, want);
+    if (total < 0) return total;
     if (::lseek(fd, base + (off_t)total, SEEK_SET) < 0) return -(long long)errno;
-    return (long long)total;
+    return total;
 }
 
 struct Slot {
@@ -129,6 +213,67 @@ struct Slot {
     bool busy = false;
 };
 
+// The slots and streams of a context's streaming calls, kept with the
+// context (lphy_hip_ctx_stream_ext) so that repeated calls allocate nothing;
+// regrown when a call needs larger chunks.
+struct StreamState {
+    Slot sl[NSLOT];
+    hipStream_t copy_st = nullptr, comp_st = nullptr;
+    size_t chunk_bytes = 0, sym_cap = 0, byte_cap = 0, meta_cap = 0;
+    void release() {
+        if (comp_st) (void)hipStreamSynchronize(comp_st);
+        if (copy_st) (void)hipStreamSynchronize(copy_st);
+        for (Slot& s : sl) {
+            if (s.pin_iq) (void)hipHostFree(s.pin_iq);
+            if (s.d_iq) (void)hipFree(s.d_iq);
+            if (s.d_syms) (void)hipFree(s.d_syms);
+            if (s.d_bytes) (void)hipFree(s.d_bytes);
+            if (s.d_meta) (void)hipFree(s.d_meta);
+            if (s.pin_syms) (void)hipHostFree(s.pin_syms);
+            if (s.pin_bytes) (void)hipHostFree(s.pin_bytes);
+            if (s.pin_meta) (void)hipHostFree(s.pin_meta);
+            if (s.h2d) (void)hipEventDestroy(s.h2d);
+            if (s.done) (void)hipEventDestroy(s.done);
+            s = Slot{};
+        }
+        chunk_bytes = sym_cap = byte_cap = meta_cap = 0;
+    }
+    ~StreamState() {
+        release();
+        if (copy_st) (void)hipStreamDestroy(copy_st);
+        if (comp_st) (void)hipStreamDestroy(comp_st);
+    }
+    int ensure(size_t cbytes, size_t syms, size_t bytes, size_t metas) {
+        if (!copy_st && hipStreamCreateWithFlags(&copy_st, hipStreamNonBlocking) != hipSuccess) return -EIO;
+        if (!comp_st && hipStreamCreateWithFlags(&comp_st, hipStreamNonBlocking) != hipSuccess) return -EIO;
+        if (cbytes <= chunk_bytes && syms <= sym_cap && bytes <= byte_cap && metas <= meta_cap) return 0;
+        release();
+        for (Slot& s : sl) {
+            if (hipHostMalloc((void**)&s.pin_iq, cbytes, hipHostMallocDefault) != hipSuccess ||
+                hipMalloc((void**)&s.d_iq, cbytes) != hipSuccess ||
+                hipMalloc((void**)&s.d_syms, syms * sizeof(uint16_t)) != hipSuccess ||
+                hipMalloc((void**)&s.d_bytes, bytes) != hipSuccess ||
+                hipMalloc((void**)&s.d_meta, metas * sizeof(lphy_frame_meta)) != hipSuccess ||
+                hipHostMalloc((void**)&s.pin_syms, syms * sizeof(uint16_t), hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void**)&s.pin_bytes, bytes, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void**)&s.pin_meta, metas * sizeof(lphy_frame_meta), hipHostMallocDefault) !=
+                    hipSuccess ||
+                hipEventCreateWithFlags(&s.h2d, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+                release();
+                return -ENOMEM;
+            }
+        }
+        chunk_bytes = cbytes;
+        sym_cap = syms;
+        byte_cap = bytes;
+        meta_cap = metas;
+        return 0;
+    }
+};
+
+void free_stream_state(void* p) { delete static_cast<StreamState*>(p); }
+
 }  // namespace
 
 extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_samples,
@@ -138,25 +283,33 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
                                      size_t* tail_bytes) {
     // max_frames is the capacity of h_syms / h_bytes / h_meta in frames: the
     // C ABI takes no other size, so an unbounded read could overrun them
-    if (!ctx || fd < 0 || frame_samples == 0 || chunk_frames == 0 || max_frames == 0 || !h_meta ||
-        !frames_out)
-        return -EINVAL;
+    if (!ctx || fd < 0 || frame_samples == 0 || max_frames == 0 || !h_meta || !frames_out) return -EINVAL;
     if (mode < 0 || mode > 2) return -EINVAL;
     if ((flags & LPHY_F_DECODE) && !h_bytes) return -EINVAL;
     const size_t per = lphy_hip_syms_per_frame(ctx, frame_samples, mode);
     if (per && !h_syms) return -EINVAL;
     const bool dec = (flags & LPHY_F_DECODE) != 0;
     const size_t frame_bytes = frame_samples * 2 * sizeof(float);
+    if (chunk_frames == 0) {  // chunks of ~64 MiB, whole frames
+        chunk_frames = kAutoChunkBytes / frame_bytes;
+        if (chunk_frames == 0) chunk_frames = 1;
+    }
+    if (chunk_frames > max_frames) chunk_frames = max_frames;
     const size_t chunk_bytes = chunk_frames * frame_bytes;
     *frames_out = 0;
     if (tail_bytes) *tail_bytes = 0;
 
     int rc = 0;
-    Slot sl[NSLOT];
-    hipStream_t copy_st = nullptr, comp_st = nullptr;
     size_t next = 0;  // stream frames read so far
     unsigned long long chunk = 0;
-    int dev = 0;
+    const bool seekable = ::lseek(fd, 0, SEEK_CUR) >= 0;
+    int nreaders = usable_cpus() - 1;
+    if (const char* e = getenv("LPHY_STREAM_READERS")) nreaders = atoi(e);
+    nreaders = nreaders < 1 ? 1 : (nreaders > 32 ? 32 : nreaders);
+    ReaderPool pool(seekable && chunk_bytes >= kParMin ? nreaders : 0);
+    StreamState* S = nullptr;
+    Slot* sl = nullptr;
+    hipStream_t copy_st = nullptr, comp_st = nullptr;
 
     // results of a slot into the caller's arrays (after its event)
     auto harvest = [&](Slot& s) -> int {
@@ -169,26 +322,16 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
         return 0;
     };
 
-    const bool seekable = ::lseek(fd, 0, SEEK_CUR) >= 0;
-    dev = lphy_hip_ctx_device(ctx);
-    ST_OK(hipSetDevice(dev));
-    ST_OK(hipStreamCreateWithFlags(&copy_st, hipStreamNonBlocking));
-    ST_OK(hipStreamCreateWithFlags(&comp_st, hipStreamNonBlocking));
-    for (Slot& s : sl) {
-        ST_OK(hipHostMalloc((void**)&s.pin_iq, chunk_bytes, hipHostMallocDefault));
-        ST_OK(hipMalloc((void**)&s.d_iq, chunk_bytes));
-        ST_OK(hipMalloc((void**)&s.d_syms, (per ? per : 1) * chunk_frames * sizeof(uint16_t)));
-        ST_OK(hipMalloc((void**)&s.d_bytes, (per / 2 ? per / 2 : 1) * chunk_frames));
-        ST_OK(hipMalloc((void**)&s.d_meta, chunk_frames * sizeof(lphy_frame_meta)));
-        ST_OK(hipHostMalloc((void**)&s.pin_syms, (per ? per : 1) * chunk_frames * sizeof(uint16_t),
-                            hipHostMallocDefault));
-        ST_OK(hipHostMalloc((void**)&s.pin_bytes, (per / 2 ? per / 2 : 1) * chunk_frames,
-                            hipHostMallocDefault));
-        ST_OK(hipHostMalloc((void**)&s.pin_meta, chunk_frames * sizeof(lphy_frame_meta),
-                            hipHostMallocDefault));
-        ST_OK(hipEventCreateWithFlags(&s.h2d, hipEventDisableTiming));
-        ST_OK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
-    }
+    ST_OK(hipSetDevice(lphy_hip_ctx_device(ctx)));
+    S = static_cast<StreamState*>(lphy_hip_ctx_stream_ext(
+        ctx, [] { return static_cast<void*>(new StreamState); }, free_stream_state));
+    if (!S) return -ENOMEM;
+    if ((rc = S->ensure(chunk_bytes, (per ? per : 1) * chunk_frames, (per / 2 ? per / 2 : 1) * chunk_frames,
+                        chunk_frames)) != 0)
+        return rc;
+    sl = S->sl;
+    copy_st = S->copy_st;
+    comp_st = S->comp_st;
 
     for (;; ++chunk) {
         Slot& s = sl[chunk % NSLOT];
@@ -196,7 +339,7 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
         size_t want = chunk_bytes;
         if (max_frames - next < chunk_frames) want = (max_frames - next) * frame_bytes;
         if (want == 0) break;
-        const long long got = read_chunk(fd, seekable, s.pin_iq, want);
+        const long long got = read_chunk(&pool, fd, seekable, s.pin_iq, want);
         if (got < 0) { rc = -EIO; goto done; }
         const size_t nf = (size_t)got / frame_bytes;
         if ((size_t)got % frame_bytes) {
@@ -233,19 +376,7 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
 done:
     if (comp_st) (void)hipStreamSynchronize(comp_st);
     if (copy_st) (void)hipStreamSynchronize(copy_st);
-    for (Slot& s : sl) {
-        if (s.pin_iq) (void)hipHostFree(s.pin_iq);
-        if (s.d_iq) (void)hipFree(s.d_iq);
-        if (s.d_syms) (void)hipFree(s.d_syms);
-        if (s.d_bytes) (void)hipFree(s.d_bytes);
-        if (s.d_meta) (void)hipFree(s.d_meta);
-        if (s.pin_syms) (void)hipHostFree(s.pin_syms);
-        if (s.pin_bytes) (void)hipHostFree(s.pin_bytes);
-        if (s.pin_meta) (void)hipHostFree(s.pin_meta);
-        if (s.h2d) (void)hipEventDestroy(s.h2d);
-        if (s.done) (void)hipEventDestroy(s.done);
-    }
-    if (copy_st) (void)hipStreamDestroy(copy_st);
-    if (comp_st) (void)hipStreamDestroy(comp_st);
+    if (sl)
+        for (int k = 0; k < NSLOT; ++k) sl[k].busy = false;
     return rc;
 }

@@ -1,0 +1,525 @@
+// lphy_wave2.h — the SF 9-12 fused launch at two waves per SIMD (k_wave2).
+// Included by lphy_kernels.h after lphy_wave.h, whose unit geometry (WGeo:
+// one wavefront per unit of 64 x 64 complex values), transform passes,
+// exchange, keyed top two, estimate fold and schedule (WSched) it reuses.
+//
+// k_wave (one 256-thread workgroup per CU, one wave per SIMD) kept each
+// unit's IQ in a per-wave 32 KiB LDS buffer filled by LDS-DMA, so the next
+// unit's copy could only start once the current unit's exchange had read
+// the buffer, and with one wave per SIMD nothing covered the waits or the
+// packed-f32 dependency pads (VALU issue 61 % of the wave's
+// cycles, waits 20 %).  Here:
+//   * 512-thread workgroups, 8 independent waves per CU (2 per SIMD, at most
+//     256 VGPR + AGPR each): one wave's loads and LDS waits run under its
+//     partner's arithmetic;
+//   * the unit's IQ goes from HBM straight into the lane's 64 registers
+//     (64 coalesced 8-byte loads per lane: lane (h, l) reads samples
+//     l + LPS m of its symbol's window), no LDS staging copy;
+//   * the 64 x LPS exchange between the passes borrows one of NBUF shared
+//     LDS buffers (3 or 4 per CU, an LDS compare-and-swap lock each) for the
+//     ~130 LDS operations it takes, so 8 waves fit beside the down-chirp;
+//   * the estimate units fold the two estimate symbols' max-abs from their
+//     own registers (SF 9-11: both symbols are in one unit; SF 12: the first
+//     estimate unit scans symbol 1 before it scales symbol 0), with no
+//     separate two-symbol scan, and units load no window for symbols a frame
+//     does not have (the last unit of a frame at SF 9-10, the estimate
+//     unit's spare halves).
+// Results are bit-identical to k_wave: the same arithmetic in the same
+// order on the same values (tests/test_gpu_*: oracle, goldens, k_wave).
+//
+// Reference: the per-symbol loop of LoRaDemod.cpp:142-176 / phy.cpp:204-238,
+// the estimate of LoRaDemod.cpp:80-136 / phy.cpp:81-148, the normalisation
+// of LoRaDemod.cpp:60-78.
+
+template <int SF, int MODE>
+struct W2Lds {
+    using W = WGeo<SF>;
+    static constexpr bool DN = (MODE & 3) != LPHY_MODE_LORA_DEMODULATE;  // down-chirp in LDS
+    static constexpr int DNC = DN ? W::N : 0;                              // its entries
+    static constexpr int NBUF0 = (163840 - 64 - 8 * DNC) / (8 * W::BUF);
+    static constexpr int NBUF = NBUF0 > 4 ? 4 : NBUF0;                     // exchange buffers
+    static_assert(NBUF >= 2, "two exchange buffers at least");
+    static constexpr int WPB = 8;                                          // waves per workgroup
+};
+
+typedef __attribute__((address_space(3))) unsigned lds_u32;
+
+// Borrow one of the CU's exchange buffers: lane 0 takes the first free one
+// from `start` on by an LDS compare-and-swap (acquire), the wave learns it
+// by readfirstlane; with none free the wave sleeps and sweeps again.  A
+// holder never waits for anything but its own LDS operations, so every
+// wait ends.
+template <int NBUF>
+__device__ __forceinline__ int wbuf_acquire(lds_u32* locks, int start) {
+    for (;;) {
+        int got = -1;
+        if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+            for (int k = 0; k < NBUF; ++k) {
+                int b = start + k;
+                b = b >= NBUF ? b - NBUF : b;
+                unsigned expected = 0u;
+                if (__hip_atomic_compare_exchange_strong((unsigned*)&locks[b], &expected, 1u, __ATOMIC_ACQUIRE,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                    got = b;
+                    break;
+                }
+            }
+        }
+        got = __builtin_amdgcn_readfirstlane(got);
+        if (got >= 0) return got;
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+// Give the buffer back once this wave's reads of it are done (release: the
+// compiler orders the store after them; the LDS serves one wave's requests
+// in order, so the next holder's writes follow them).
+__device__ __forceinline__ void wbuf_release(lds_u32* locks, int b) {
+    if ((threadIdx.x & 63) == 0)
+        __hip_atomic_store((unsigned*)&locks[b], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Max-abs of symbol s of frame f (the [dechirped] samples, as the
+// reference's normalisation scans them, LoRaDemod.cpp:60-78) by the whole
+// wave, NaN when one is not finite; wscan2's arithmetic over one symbol.
+template <int SF, int MODE>
+__device__ __noinline__ float wscan1(KArgs ka, unsigned f, unsigned s, const lds_cf32* ldnl) {
+    const DemodArgs& A = kargs(ka);
+    constexpr int N = 1 << SF;
+    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    const cf32* const dnl = (const cf32*)ldnl;
+    const int lane = threadIdx.x & 63;
+    const cf32* fr = A.iq + (unsigned long long)f * A.frame_samples + (unsigned long long)s * N;
+    iq_check(A, f, (long long)s * N + N - 1);
+    float fm = 0.0f;
+    cf32 sum = czero();
+    constexpr int U = 16;
+#pragma unroll 1
+    for (int r = 0; r < N / (64 * U); ++r) {
+        cf32 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = fr[(r * U + u) * 64 + lane];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            cf32 a = x[u];
+            if constexpr (DECH) a = cmul(a, dnl[((r * U + u) * 64 + lane) & (N - 1)]);
+            fm = max3_abs(fm, a.x, a.y);
+            sum = sum + a;
+        }
+    }
+    const bool bad = !(sum.x == sum.x && sum.y == sum.y) || !(fm <= 3.40282347e38f);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) fm = fmaxf(fm, __shfl_xor(fm, off, 64));
+    return __ballot(bad) ? __builtin_nanf("") : fm;
+}
+
+struct WEst {
+    UnitResult ur;  // the lane's half (SF 9-11) or the unit's symbol (SF 12)
+    float mx;       // the two estimate symbols' max-abs (when computed here)
+};
+
+// An estimate unit (KISS's arithmetic, bit for bit: LoRaDemod.cpp:80-136,
+// phy.cpp:81-148): SF 9-11 symbols 0 and 1 in halves 0 and 1, SF 12 symbol
+// j.  With `find_mx` (modes 1/2, the frame's first estimate unit) the unit
+// also folds the two estimate symbols' max-abs from its own samples - SF 12:
+// symbol 1 by wscan1 first - and normalises with it; otherwise with `mx`.
+template <int SF, int MODE>
+__device__ __noinline__ WEst west2(KArgs ka, lds_cf32* lpool, lds_u32* locks, const lds_cf32* ldnl, unsigned f,
+                                   unsigned j, float mx, bool find_mx) {
+    using W = WGeo<SF>;
+    using L = W2Lds<SF, MODE>;
+    constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
+    constexpr bool M0 = (MODE & 3) == LPHY_MODE_DEMODULATE;
+    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    const DemodArgs& A = kargs(ka);
+    const cf32* const dnl = (const cf32*)ldnl;
+    const int lane = threadIdx.x & 63, h = lane / LPS, l = lane % LPS;
+    // the half's symbol: SF 12 symbol j; below, halves 0 and 1 (the others idle)
+    const bool mine = SPW == 1 || h < 2;
+    const unsigned s = SPW == 1 ? j : (unsigned)(h < 2 ? h : 0);
+    cf32 v[64];
+    const cf32* src = A.iq + (unsigned long long)f * A.frame_samples + (unsigned long long)s * N + l;
+    iq_check(A, f, (long long)s * N + l + LPS * 63);
+    if (mine) {
+#pragma unroll
+        for (int e = 0; e < 64; ++e) v[e] = src[LPS * e];
+    } else {
+#pragma unroll
+        for (int e = 0; e < 64; ++e) v[e] = czero();
+    }
+    if constexpr (DECH) {
+#pragma unroll
+        for (int e = 0; e < 64; ++e) v[e] = cmul(v[e], dnl[l + LPS * e]);
+    }
+    if constexpr (!M0) {
+        if (find_mx) {
+            float fm = 0.0f;
+            cf32 sum = czero();
+#pragma unroll
+            for (int e = 0; e < 64; ++e) {
+                fm = max3_abs(fm, v[e].x, v[e].y);
+                sum = sum + v[e];
+            }
+            const bool bad = !(sum.x == sum.x && sum.y == sum.y) || !(fm <= 3.40282347e38f);
+            // over the two estimate symbols' lanes (all 64 at SF 11-12)
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) fm = fmaxf(fm, __shfl_xor(fm, off, 64));
+            mx = __ballot(bad) ? __builtin_nanf("") : fm;
+            if constexpr (SPW == 1) {
+                const float m1 = wscan1<SF, MODE>(ka, f, 1u, ldnl);
+                mx = (mx == mx && m1 == m1) ? fmaxf(mx, m1) : __builtin_nanf("");
+            }
+        }
+    }
+    lphy_frame_meta nm{};
+    nm.scale = 1.0f;
+    if constexpr (!M0) nm = norm_meta_hot(mx, true, A.no_scratch);
+    const bool live = nm.status == 0;
+#pragma unroll
+    for (int e = 0; e < 64; ++e) {
+        cf32 x = v[e];
+        if constexpr (!M0) x = cscale(x, nm.scale);
+        v[e] = live ? x : czero();
+    }
+    const WTw<SF> T{};  // unused by the exact pass
+    wpass1<SF, false>(v, ctw(A.tw));
+    const int b = wbuf_acquire<L::NBUF>(locks, (threadIdx.x >> 6) & (L::NBUF - 1));
+    cf32* const buf = (cf32*)(lpool + b * W::BUF);
+    wexchange<SF>(v, buf, h, l);
+    // pass 2's per-lane twiddles from an LDS copy of the KISS table
+    wait_lgkm0();  // the exchange reads are done
+    wdma_table<SF>(A.tw, buf, lane);
+    wait_vm0();
+    wpass2<SF, false>(v, T, buf, l);
+    wait_lgkm0();
+    wbuf_release(locks, b);
+    float sumsq = 0.0f;
+#pragma unroll
+    for (int e = 0; e < 64; ++e) {
+        const cf32 sq = v[e] * v[e];
+        sumsq += sq.x + sq.y;
+    }
+    const unsigned long long nb = __ballot(!(sumsq == sumsq));
+    WEst r;
+    r.ur = wunit_result<SF>(v, h, l, lane);
+    r.ur.nan = (LPS == 64 ? nb : ((nb >> (LPS * h)) & ((1ull << (LPS & 63)) - 1))) != 0 ? 1 : 0;
+    if (!live) r.ur = UnitResult{0, 0, 0.0f, 0.0f, 0};
+    r.mx = mx;
+    return r;
+}
+
+// The pair's two results (SF 9-11: halves 0 and 1; SF 12: the two units).
+__device__ __forceinline__ UnitResult wur_from(const UnitResult& u, int src) {
+    UnitResult r;
+    r.idx = __shfl(u.idx, src, 64);
+    r.valid = __shfl(u.valid, src, 64);
+    r.findex = __shfl(u.findex, src, 64);
+    r.phase = __shfl(u.phase, src, 64);
+    r.nan = __shfl(u.nan, src, 64);
+    return r;
+}
+
+// Frame end under the speculative normalisation (wclose's rule): the
+// samples no symbol window covers are scanned, then the frame's true max-abs
+// confirms the two-symbol normalisation, sends the frame to the exact re-run
+// (NaN / inf), or settles it here: both estimates again with the exact
+// scale, and the symbols kept when the time shift is unchanged and every
+// certified symbol's lead covers the larger sample bound and the rate
+// difference (settle_frames' rule), else k_post's exact re-run.
+template <int SF, int MODE>
+__device__ __noinline__ void wclose2(KArgs ka, lds_cf32* lpool, lds_u32* locks, const lds_cf32* ldnl, unsigned f,
+                                     float rate, float scale, int t_off, float mx01, float m, float r, bool nan,
+                                     bool open) {
+    using W = WGeo<SF>;
+    constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
+    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    const DemodArgs& A = kargs(ka);
+    const cf32* const dnl = (const cf32*)ldnl;
+    const int lane = threadIdx.x & 63;
+    const unsigned S = (unsigned)A.total_syms;
+    const unsigned cnt = DECH ? S * N : (unsigned)A.frame_samples;
+    const unsigned end = covered_end(S, N, cnt, t_off);
+    bool fbad = false;
+    if (end < cnt) m = fmaxf(m, wave_range_maxabs<SF, MODE>(A, f, end, cnt, dnl, fbad));
+    const float mt = fmaxf(m, mx01);
+    const lphy_frame_meta mg = norm_meta(mx01, true, 0), me = norm_meta(mt, true, 0);
+    bound_check(f, (long long)A.frames);
+    if (nan || fbad || !(mt <= 3.40282347e38f)) {
+        if (lane == 0) A.meta[f].status = kStatusFixup;
+        return;
+    }
+    if (me.scale == mg.scale && me.normalised == mg.normalised) return;
+    // settle: the estimate units with the frame's true max-abs (norm_meta_hot
+    // of it gives me.scale)
+    UnitResult ua{0, 0, 0.0f, 0.0f, 0}, ub = ua;
+#pragma unroll 1
+    for (int j = 0; j < W::NE; ++j) {
+        const WEst e = west2<SF, MODE>(ka, lpool, locks, ldnl, f, (unsigned)j, mt, false);
+        if constexpr (SPW == 1) {
+            if (j == 0) ua = e.ur;
+            else ub = e.ur;
+        } else {
+            ua = wur_from(e.ur, 0);
+            ub = wur_from(e.ur, LPS);
+        }
+    }
+    lphy_frame_meta e = me;
+    EstFold fold;
+    if (ua.valid) fold.add(ua.idx, ua.findex, 0, ua.phase);
+    else fold.add(0, 0.0f, 0, 0.0f);
+    if (ub.valid) fold.add(ub.idx, ub.findex, 0, ub.phase);
+    else fold.add(0, 0.0f, 0, 0.0f);
+    fold.finish(e, 2, N, 1);
+    const float a = fmaxf(1.0f, mt * scale) * 1.0001f;
+    const float b1 = cert_bound<SF>(rate, rate * (float)t_off, 1.0f);
+    const float d = fabsf(e.rate - rate) * (1.0f + 4.0f * kU);
+    const float A1 = (float)N * 1.41421366f * 1.0001f;
+    const bool ok = !ua.nan && !ub.nan && e.t_off == t_off && t_off >= -N && t_off <= N &&
+                    r > 4.0f * a + 4.0f * d * (float)N * A1 * a / b1;
+    if (lane == 0) {
+        e.status = !ok ? kStatusFixup : (open ? kStatusRecheck : 0);
+        meta_put_est(&A.meta[f], e);
+    }
+}
+
+template <int SF, int MODE>
+__global__ __launch_bounds__(512) void k_wave2(FrameArgs P) {
+    using W = WGeo<SF>;
+    using L = W2Lds<SF, MODE>;
+    constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
+    constexpr bool M0 = (MODE & 3) == LPHY_MODE_DEMODULATE;
+    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    const DemodArgs& A = P.A;
+    const KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+    // the down-chirp at LDS offset 0 (its wrapped index is the byte address
+    // itself), the exchange buffers after it, their locks last
+    __shared__ cf32 lds_all[L::DNC + L::NBUF * W::BUF];
+    __shared__ unsigned locks_s[L::NBUF];
+    cf32* const dnl = lds_all;
+    lds_cf32* const pool = (lds_cf32*)(lds_all + L::DNC);
+    lds_u32* const locks = (lds_u32*)locks_s;
+
+    const int tid = threadIdx.x;
+    if constexpr (L::DN) {
+        for (int i = tid; i < N; i += 512) dnl[i] = A.down[i];
+    }
+    if (tid < L::NBUF) locks_s[tid] = 0u;
+    __syncthreads();  // the only workgroup barrier: waves are independent below
+
+    const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = lane / LPS, l = lane % LPS;
+    const unsigned nframes = (unsigned)A.frames;
+    const unsigned S = (unsigned)A.total_syms;
+    const unsigned Wn = P.waves;
+    const unsigned w = blockIdx.x * L::WPB + wv;
+    if (w >= nframes) return;
+    WSched<SF> sch;
+    sch.nk = (nframes - 1 - w) / Wn + 1;
+    sch.ND = (S + SPW - 1) / SPW;
+    sch.p = sch.ND >= 2 ? sch.ND - 2 : 0;
+    const bool spec = !M0 && A.spec != 0;
+    // the wave's first choice of exchange buffer (spreads the waves)
+    const int bstart = wv & (L::NBUF - 1);
+
+    WFrame rec0{0.0f, 1.0f, 0.0f, 0, 0}, rec1 = rec0;
+    auto rec = [&](unsigned k) -> WFrame { return (k & 1) ? rec1 : rec0; };
+    auto set_rec = [&](unsigned k, const WFrame& r) {
+        if (k & 1) rec1 = r;
+        else rec0 = r;
+    };
+    auto fglob = [&](unsigned k) { return w + k * Wn; };
+
+    cf32 Qr[8], Pr[8];
+    unsigned rot_frame = 0xffffffffu;
+    constexpr float kBig = 3.0e38f;
+    float sp_mx = 0.0f, sp_r = kBig;
+    unsigned sp_fl = 0u;
+    UnitResult ur0{0, 0, 0.0f, 0.0f, 0};  // SF 12: the first estimate unit's result
+
+    for (WCursor cu = sch.first(); sch.kind(cu) != kWDead;) {
+        const WCursor nx = sch.next(cu);
+        const unsigned k = sch.frame(cu), f = fglob(k);
+        if (sch.kind(cu) == kWSym) {
+            const WFrame R = rec(k);
+            const unsigned s = SPW * cu.j + (unsigned)h;
+            const bool live = s < S;
+            lphy_frame_meta m{};
+            m.rate = R.rate;
+            m.scale = R.scale;
+            m.t_off = R.t_off;
+            m.status = R.ok ? 0 : -1;
+            m.have_sync = 1;
+            const SymCtx c = sym_ctx(A, f, live ? s : 0u, live, N, m);
+            // the unit's IQ, straight into the registers (no window for a
+            // symbol the frame does not have)
+            cf32 v[64];
+            {
+                const cf32* src = A.iq + (unsigned long long)f * A.frame_samples + c.base + (unsigned)l;
+                if (live) {
+                    iq_check(A, f, (long long)c.base + l + LPS * 63);
+#pragma unroll
+                    for (int e = 0; e < 64; ++e) v[e] = src[LPS * e];
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 64; ++e) v[e] = czero();
+                }
+            }
+            if (k != rot_frame) {
+                rot_frame = k;
+                const WRot rt = wrot<SF, MODE>(R.rate, R.scale);
+#pragma unroll
+                for (int b = 0; b < 8; ++b) Qr[b] = rt.q[b];
+#pragma unroll
+                for (int a = 0; a < 8; ++a)
+                    Pr[a] = cf32{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(rt.p.x), a)),
+                                 __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rt.p.y), a))};
+            }
+            // staging in place: [exact dechirp at the window's own chirp
+            // indices,] max-abs fold, certified rotation
+            float amax = 0.0f;
+            const unsigned d0 = ((c.base + (unsigned)l) & (unsigned)(N - 1)) << 3;
+            // in chunks of 8 samples, chunk q + 1's down-chirp reads issued
+            // before chunk q's arithmetic (sched barriers keep the order and
+            // the registers: 16 in flight, not 128)
+            cf32 dq[2][8];
+            auto ld_chunk = [&](int q, cf32 (&ds)[8]) __attribute__((always_inline)) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int e = 8 * q + i;
+                    if constexpr (DECH) ds[i] = lds_ld(dnl, (int)((d0 + (unsigned)((LPS * e) << 3)) & (unsigned)(8 * N - 1)));
+                    if constexpr (M0) ds[i] = dnl[l + LPS * e];
+                }
+            };
+            ld_chunk(0, dq[0]);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                if (q + 1 < 8) ld_chunk(q + 1, dq[(q + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int e = 8 * q + i;
+                    cf32 p = v[e];
+                    if constexpr (DECH) p = cmul(p, dq[q & 1][i]);
+                    amax = max3_abs(amax, p.x, p.y);
+                    if constexpr (M0) p = cmul(p, dq[q & 1][i]);
+                    v[e] = cmul_fma(cmul_fma(p, Qr[i]), Pr[q]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            wpass1<SF, true>(v, ctw(A.tw));
+            // pass 2's per-lane twiddles (9 loads, cached), issued before the
+            // exchange so they land during it; not kept across units (VGPRs)
+            WTw<SF> T;
+            T.load(A.tw, l);
+            const int b = wbuf_acquire<L::NBUF>(locks, bstart);
+            wexchange<SF>(v, (cf32*)(pool + b * W::BUF), h, l);
+            wait_lgkm0();  // the exchange reads are done
+            wbuf_release(locks, b);
+            wpass2<SF, true>(v, T, A.tw, l);
+            // keyed top two over the half's bins l + LPS e (see k_wave)
+            unsigned k1 = 0u, k2 = 0u;
+#pragma unroll
+            for (int e = 0; e < 64; ++e) {
+                const float m2 = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
+                const unsigned key = (__float_as_uint(m2) & ~63u) | (unsigned)e;
+                k2 = med3_u32(k1, k2, key);
+                k1 = k1 > key ? k1 : key;
+            }
+            unsigned K1, K2;
+            wave_top2_merge<LPS>(k1, k2, h, K1, K2);
+            const unsigned long long bm = __ballot(k1 == K1);
+            const unsigned long long hm = LPS == 64 ? bm : ((bm >> (LPS * h)) & ((1ull << (LPS & 63)) - 1));
+            ArgMax2 b2;
+            b2.v = __uint_as_float(K1 & ~63u);
+            b2.v2 = __uint_as_float(K2 | 63u);
+            b2.i = (__ffsll((long long)hm) - 1) + LPS * (int)(K1 & 63u);
+            float am = 1.0f;  // modes 1/2: normalised frame (see fast_certified)
+            if constexpr (M0) {
+#pragma unroll
+                for (int off = 1; off < LPS; off <<= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
+                am = amax;
+            }
+            const float cb1 = cert_bound<SF>(c.rate, c.start, 1.0f, kWaveExtra);
+            const float cgap = cert_gap(b2);
+            const bool cert = cgap > 4.0f * (cb1 * am) && (float)N * 1.41421366f * am * 1.0001f < 1e18f &&
+                              am >= 1e-20f && b2.v >= 1e-30f;
+            const bool redo = c.ok && (!cert || A.debug_recheck);  // (DEBUG_RECHECK: tests)
+            if (live && l == 0) {
+                const uint16_t out = redo ? kSymRecheck : (uint16_t)b2.i;
+                if (c.have_sync && c.s < 2) store_symbol(A, c, c.ok ? out : (uint16_t)0);
+                else if (c.ok) store_symbol(A, c, out);
+                if (redo) A.meta[c.f].status = kStatusRecheck;
+            }
+            if (spec && c.ok) {
+                sp_mx = fmaxf(sp_mx, amax);
+                const cf32 q = v[0] * v[0];
+                const float q2 = q.x + q.y;
+                if (!(q2 == q2)) sp_fl |= 1u;  // a NaN sample reaches every bin
+                if (l == 0) {
+                    if (redo) sp_fl |= 2u;
+                    else sp_r = fminf(sp_r, cgap * __builtin_amdgcn_rcpf(cb1) * (1.0f - 4.0f * kU));
+                }
+            }
+            // the frame's last symbol unit closes it (speculative normalisation)
+            if (spec && cu.phase == 3 && cu.j + 1 == sch.ND) {
+                float mm = sp_mx, rr = sp_r;
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    mm = fmaxf(mm, __shfl_xor(mm, off, 64));
+                    rr = fminf(rr, __shfl_xor(rr, off, 64));
+                }
+                const bool nan = __ballot(sp_fl & 1u) != 0, open = __ballot(sp_fl & 2u) != 0;
+                sp_mx = 0.0f;
+                sp_r = kBig;
+                sp_fl = 0u;
+                if (R.ok)
+                    wclose2<SF, MODE>(ka, pool, locks, (const lds_cf32*)dnl, f, R.rate, R.scale, R.t_off, R.mx, mm,
+                                      rr, nan, open);
+            }
+        } else {
+            // estimate unit(s): SF 12 symbol j, below symbols 0 and 1 in halves 0 and 1
+            const WFrame R0 = rec(k);
+            const bool first = cu.j == 0;
+            const WEst est = west2<SF, MODE>(ka, pool, locks, (const lds_cf32*)dnl, f, cu.j, R0.mx, first);
+            const UnitResult ur = est.ur;
+            bool fold_now = true;
+            UnitResult ua = ur, ub = ur;
+            if constexpr (SPW == 1) {
+                if (first) {
+                    ur0 = ur;
+                    fold_now = false;
+                } else {
+                    ua = ur0;
+                }
+            } else {
+                ua = wur_from(ur, 0);
+                ub = wur_from(ur, LPS);
+            }
+            WFrame r = R0;
+            if (first) r.mx = est.mx;
+            if (fold_now) {
+                lphy_frame_meta m{};
+                m.scale = 1.0f;
+                m.have_sync = 1;
+                if constexpr (!M0) m = norm_meta_hot(r.mx, true, A.no_scratch);
+                if (m.status == 0) {
+                    EstFold fold;
+                    if (ua.valid) fold.add(ua.idx, ua.findex, 0, ua.phase);
+                    else fold.add(0, 0.0f, 0, 0.0f);
+                    if (ub.valid) fold.add(ub.idx, ub.findex, 0, ub.phase);
+                    else fold.add(0, 0.0f, 0, 0.0f);
+                    fold.finish(m, 2, N, 1);
+                    if (ua.nan || ub.nan) m.status = kStatusFixup;
+                }
+                bound_check(f, (long long)A.frames);
+                if (lane == 0) meta_put_est(&A.meta[f], m);
+                r.rate = m.rate;
+                r.scale = m.scale;
+                r.t_off = m.t_off;
+                r.ok = m.status == 0 ? 1 : 0;
+            }
+            set_rec(k, r);
+        }
+        cu = nx;
+    }
+}

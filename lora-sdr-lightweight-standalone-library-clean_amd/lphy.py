@@ -257,11 +257,9 @@ class Demodulator:
         """Demodulate the float32 I/Q frames read from `fd` until EOF or
         max_frames.  The result arrays hold `capacity` frames (default:
         max_frames); at most min(max_frames, capacity) frames are read.
-        chunk_frames = 0 picks ~32 MiB chunks (three are pinned per call; in
-        tools/stream_bench.py smaller chunks streamed faster).  Returns
-        (symbols, payload, meta, tail_bytes) for the whole frames read."""
-        if chunk_frames <= 0:
-            chunk_frames = max(1, (32 << 20) // (frame_samples * 8))
+        chunk_frames = 0 lets the library pick ~64 MiB chunks (its pinned slots
+        are kept with the context for the next call).  Returns (symbols,
+        payload, meta, tail_bytes) for the whole frames read."""
         cap = capacity or max_frames
         if cap <= 0:
             raise ValueError("capacity or max_frames required")

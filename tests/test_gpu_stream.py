@@ -108,7 +108,8 @@ def test_stream_argument_errors(lphy):
     lib = d.lib
     assert lib.lphy_hip_demod_stream(d.ctx, -1, 66 * 128, 4, 0, 0, 4, syms.ctypes.data, None,
                                      meta.ctypes.data, C.byref(n), C.byref(t)) == -22
-    assert lib.lphy_hip_demod_stream(d.ctx, 0, 66 * 128, 0, 0, 0, 4, syms.ctypes.data, None,
+    # no frame length (chunk_frames = 0 is valid: the library picks ~64 MiB chunks)
+    assert lib.lphy_hip_demod_stream(d.ctx, 0, 0, 0, 0, 0, 4, syms.ctypes.data, None,
                                      meta.ctypes.data, C.byref(n), C.byref(t)) == -22
     # no capacity: the C ABI cannot bound the writes into the caller's arrays
     assert lib.lphy_hip_demod_stream(d.ctx, 0, 66 * 128, 4, 0, 0, 0, syms.ctypes.data, None,
