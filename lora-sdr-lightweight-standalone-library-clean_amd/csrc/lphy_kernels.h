@@ -2601,6 +2601,16 @@ inline bool wave_v1() {
     return env == 1;
 }
 
+// SF 9-10: units spanning frames (k_wave2s) unless LPHY_WAVE_SPAN=0 (A/B)
+inline bool wave_span() {
+    static int env = -1;
+    if (env < 0) {
+        const char* e = getenv("LPHY_WAVE_SPAN");
+        env = (e && e[0] == '0') ? 0 : 1;
+    }
+    return env == 1;
+}
+
 template <int SF, int MODE>
 int launch_wave_mode(const DemodArgs& A, hipStream_t st) {
     FrameArgs P{};
@@ -2611,6 +2621,13 @@ int launch_wave_mode(const DemodArgs& A, hipStream_t st) {
         const unsigned long long need = (A.frames + WPB - 1) / WPB;
         if (blocks > need) blocks = need;
         P.waves = (unsigned)(blocks * WPB);
+        if constexpr (WGeo<SF>::SPW >= 4) {
+            if (wave_span()) {
+                hipLaunchKernelGGL((k_wave2s<SF, MODE>), dim3((unsigned)blocks), dim3(64 * WPB), 0, st, P);
+                HIP_OK(hipGetLastError());
+                return 0;
+            }
+        }
         hipLaunchKernelGGL((k_wave2<SF, MODE>), dim3((unsigned)blocks), dim3(64 * WPB), 0, st, P);
         HIP_OK(hipGetLastError());
         return 0;

@@ -409,10 +409,16 @@ __global__ __launch_bounds__(512) void k_wave2(FrameArgs P) {
             wpass1<SF, true>(v, ctw(A.tw));
             // pass 2's per-lane twiddles (9 loads, cached), issued before the
             // exchange so they land during it; not kept across units (VGPRs)
+            // (the lane indices made opaque: the exchange's lane addresses and
+            // these loads are then recomputed / reissued each unit, a few VALU
+            // and 9 cached loads, rather than hoisted out of the loop, where
+            // the compiler spills them and reloads each from scratch)
+            int hx = h, lx = l;
+            asm volatile("" : "+v"(hx), "+v"(lx));
             WTw<SF> T;
-            T.load(A.tw, l);
+            T.load(A.tw, lx);
             const int b = wbuf_acquire<L::NBUF>(locks, bstart);
-            wexchange<SF>(v, (cf32*)(pool + b * W::BUF), h, l);
+            wexchange<SF>(v, (cf32*)(pool + b * W::BUF), hx, lx);
             wait_lgkm0();  // the exchange reads are done
             wbuf_release(locks, b);
             wpass2<SF, true>(v, T, A.tw, l);
@@ -521,5 +527,382 @@ __global__ __launch_bounds__(512) void k_wave2(FrameArgs P) {
             set_rec(k, r);
         }
         cu = nx;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_wave2s: the same units spanning frames (SF 9-10: 8 / 4 symbols per unit).
+// k_wave2 gives every frame whole units of its own: at SF 9 a frame's 66
+// symbols take 9 units, the last with 2 live halves of 8, and its estimate
+// unit uses 2 halves of 8 - 10 units for 8.5 units of work.  Here a wave's
+// frames w, w + W, ... form one stream of symbols (frame k's symbol s at
+// position k S + s) cut into units of SPW consecutive symbols, whatever
+// frames they belong to, and one estimate unit takes the two estimate
+// symbols of EPU = SPW / 2 frames.  An estimate unit runs as soon as a
+// symbol unit needs a frame not yet estimated.  Per-frame state lives in a
+// per-wave LDS ring of RING records (the rotation, normalisation and time
+// shift of the estimate, and the speculation's running max-abs, least
+// certificate ratio and flags, which each unit's halves fold in with LDS
+// atomics); the unit holding a frame's last symbol closes it (wclose2).
+// Each lane rotates with its own frame's tables.
+// ---------------------------------------------------------------------------
+struct WRec {  // 32 B
+    float rate, scale, mx;  // estimate: rotation rate, normalisation, estimate symbols' max-abs
+    int t_off;
+    unsigned ok;    // estimate folded, status 0
+    unsigned mxs;   // symbol units' max-abs (float bits, LDS atomic max)
+    unsigned rmin;  // least certificate ratio (float bits, LDS atomic min)
+    unsigned fl;    // 1 a NaN, 2 a symbol left to the exact re-run (LDS atomic or)
+};
+typedef __attribute__((address_space(3))) WRec lds_rec;
+
+template <int SF>
+struct W2Span {
+    static constexpr int SPW = WGeo<SF>::SPW;
+    static constexpr int EPU = SPW / 2;  // frames per estimate unit
+    static constexpr int RING = EPU + 2 <= 4 ? 4 : (EPU + 2 <= 8 ? 8 : (EPU + 2 <= 16 ? 16 : 32));
+};
+
+// Estimate unit of frames fb .. fb + EPU - 1 (wave-local k0 ..): half h
+// holds symbol h % 2 of frame fb + h / 2 (fglob: the batch frame of a
+// wave-local one).  Each frame's max-abs is folded over its two halves
+// (modes 1/2), the frame normalised with it, the halves transformed with
+// KISS's arithmetic; returns the half's detector outputs and its frame's
+// max-abs.  Dead halves (frames past the wave's last) load nothing.
+template <int SF, int MODE>
+__device__ __noinline__ WEst west2s(KArgs ka, lds_cf32* lpool, lds_u32* locks, const lds_cf32* ldnl, unsigned fg,
+                                    bool live_frame) {
+    using W = WGeo<SF>;
+    using L = W2Lds<SF, MODE>;
+    constexpr int N = W::N, LPS = W::LPS;
+    constexpr bool M0 = (MODE & 3) == LPHY_MODE_DEMODULATE;
+    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    const DemodArgs& A = kargs(ka);
+    const cf32* const dnl = (const cf32*)ldnl;
+    const int lane = threadIdx.x & 63, h = lane / LPS, l = lane % LPS;
+    const unsigned s = (unsigned)(h & 1);
+    cf32 v[64];
+    if (live_frame) {
+        iq_check(A, fg, (long long)s * N + l + LPS * 63);
+        const cf32* src = A.iq + (unsigned long long)fg * A.frame_samples + (unsigned long long)s * N + l;
+#pragma unroll
+        for (int e = 0; e < 64; ++e) v[e] = src[LPS * e];
+    } else {
+#pragma unroll
+        for (int e = 0; e < 64; ++e) v[e] = czero();
+    }
+    if constexpr (DECH) {
+#pragma unroll
+        for (int e = 0; e < 64; ++e) v[e] = cmul(v[e], dnl[l + LPS * e]);
+    }
+    float mx = 0.0f;
+    if constexpr (!M0) {
+        float fm = 0.0f;
+        cf32 sum = czero();
+#pragma unroll
+        for (int e = 0; e < 64; ++e) {
+            fm = max3_abs(fm, v[e].x, v[e].y);
+            sum = sum + v[e];
+        }
+        const bool bad = !(sum.x == sum.x && sum.y == sum.y) || !(fm <= 3.40282347e38f);
+        // over the frame's two halves (2 LPS lanes)
+#pragma unroll
+        for (int off = LPS; off >= 1; off >>= 1) fm = fmaxf(fm, __shfl_xor(fm, off, 64));
+        const unsigned long long bm = __ballot(bad);
+        const unsigned pair = (unsigned)(lane / (2 * LPS));
+        constexpr unsigned long long PM = 2 * LPS >= 64 ? ~0ull : ((1ull << (2 * LPS)) - 1ull);
+        mx = ((bm >> (pair * 2 * LPS)) & PM) != 0 ? __builtin_nanf("") : fm;
+    }
+    lphy_frame_meta nm{};
+    nm.scale = 1.0f;
+    if constexpr (!M0) nm = norm_meta_hot(mx, true, A.no_scratch);
+    const bool live = live_frame && nm.status == 0;
+#pragma unroll
+    for (int e = 0; e < 64; ++e) {
+        cf32 x = v[e];
+        if constexpr (!M0) x = cscale(x, nm.scale);
+        v[e] = live ? x : czero();
+    }
+    const WTw<SF> T{};  // unused by the exact pass
+    wpass1<SF, false>(v, ctw(A.tw));
+    const int b = wbuf_acquire<L::NBUF>(locks, (threadIdx.x >> 6) & (L::NBUF - 1));
+    cf32* const buf = (cf32*)(lpool + b * W::BUF);
+    wexchange<SF>(v, buf, h, l);
+    wait_lgkm0();
+    wdma_table<SF>(A.tw, buf, lane);
+    wait_vm0();
+    wpass2<SF, false>(v, T, buf, l);
+    wait_lgkm0();
+    wbuf_release(locks, b);
+    float sumsq = 0.0f;
+#pragma unroll
+    for (int e = 0; e < 64; ++e) {
+        const cf32 sq = v[e] * v[e];
+        sumsq += sq.x + sq.y;
+    }
+    const unsigned long long nb = __ballot(!(sumsq == sumsq));
+    WEst r;
+    r.ur = wunit_result<SF>(v, h, l, lane);
+    r.ur.nan = ((nb >> (LPS * h)) & ((1ull << (LPS & 63)) - 1)) != 0 ? 1 : 0;
+    if (!live) r.ur = UnitResult{0, 0, 0.0f, 0.0f, 0};
+    r.mx = mx;
+    return r;
+}
+
+// The frame's rotation tables for lanes whose frames differ (k_wave2s):
+// q[b] = [scale] e^{j rate (l + LPS b)} and p = e^{j rate 8 LPS (l & 7)} of
+// the lane's own frame (LPS >= 8: every half's lanes 0..7 give its table).
+template <int SF, int MODE>
+__device__ __noinline__ WRot wrot_lane(float rate, float scale) {
+    constexpr int LPS = WGeo<SF>::LPS;
+    static_assert(LPS >= 8, "p from the half's own lanes");
+    const int lane = threadIdx.x & 63, l = lane % LPS;
+    WRot r;
+#pragma unroll 1
+    for (int b = 0; b < 8; ++b) {
+        float sn, cs;
+        lphy_libm::sincosf_exact(rate * (float)(l + LPS * b), &sn, &cs);
+        cf32 t = cf32{cs, sn};
+        if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) t = cscale(t, scale);
+        r.q[b] = t;
+    }
+    float sn, cs;
+    lphy_libm::sincosf_exact(rate * (float)(8 * LPS * (l & 7)), &sn, &cs);
+    r.p = cf32{cs, sn};
+    return r;
+}
+
+template <int SF, int MODE>
+__global__ __launch_bounds__(512) void k_wave2s(FrameArgs P) {
+    using W = WGeo<SF>;
+    using L = W2Lds<SF, MODE>;
+    using SP = W2Span<SF>;
+    constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW, EPU = SP::EPU, RING = SP::RING;
+    constexpr bool M0 = (MODE & 3) == LPHY_MODE_DEMODULATE;
+    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
+    static_assert(SPW >= 4 && LPS >= 8, "spanning units: SF 9-10");
+    const DemodArgs& A = P.A;
+    const KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+    __shared__ cf32 lds_all[L::DNC + L::NBUF * W::BUF];
+    __shared__ unsigned locks_s[L::NBUF];
+    __shared__ WRec rings[L::WPB][RING];
+    cf32* const dnl = lds_all;
+    lds_cf32* const pool = (lds_cf32*)(lds_all + L::DNC);
+    lds_u32* const locks = (lds_u32*)locks_s;
+
+    const int tid = threadIdx.x;
+    if constexpr (L::DN) {
+        for (int i = tid; i < N; i += 512) dnl[i] = A.down[i];
+    }
+    if (tid < L::NBUF) locks_s[tid] = 0u;
+    __syncthreads();  // the only workgroup barrier: waves are independent below
+
+    const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = lane / LPS, l = lane % LPS;
+    const unsigned nframes = (unsigned)A.frames;
+    const unsigned S = (unsigned)A.total_syms;
+    const unsigned Wn = P.waves;
+    const unsigned w = blockIdx.x * L::WPB + wv;
+    if (w >= nframes) return;
+    const unsigned nk = (nframes - 1 - w) / Wn + 1;
+    const unsigned long long total = (unsigned long long)nk * S;
+    const unsigned NU = (unsigned)((total + SPW - 1) / SPW);
+    const bool spec = !M0 && A.spec != 0;
+    const int bstart = wv & (L::NBUF - 1);
+    WRec* const ring = rings[wv];
+    constexpr float kBig = 3.0e38f;
+
+    cf32 Qr[8], Pr[8];
+    unsigned rot_k = 0xffffffffu;  // the lane's frame its tables are for
+    // the lane's stream position for the next symbol unit: frame kh, symbol sh
+    unsigned kh = 0, sh = (unsigned)h;
+    unsigned est = 0;  // frames whose estimate is folded
+    for (unsigned u = 0; u < NU;) {
+        const unsigned kmax_raw = (unsigned)__builtin_amdgcn_readlane((int)kh, 63);
+        const unsigned kmax = kmax_raw < nk ? kmax_raw : nk - 1;
+        if (est <= kmax) {
+            // estimate unit: frames est .. est + EPU - 1, half h symbol h % 2
+            const unsigned ke = est + (unsigned)(h >> 1);
+            const bool lf = ke < nk;
+            const unsigned fe = w + (lf ? ke : 0u) * Wn;
+            const WEst e = west2s<SF, MODE>(ka, pool, locks, (const lds_cf32*)dnl, fe, lf);
+            // the frame's fold on the first lane of its even half
+            const UnitResult ub = wur_from(e.ur, (lane + LPS) & 63);
+            if ((h & 1) == 0 && l == 0 && lf) {
+                lphy_frame_meta m{};
+                m.scale = 1.0f;
+                m.have_sync = 1;
+                if constexpr (!M0) m = norm_meta_hot(e.mx, true, A.no_scratch);
+                if (m.status == 0) {
+                    EstFold fold;
+                    if (e.ur.valid) fold.add(e.ur.idx, e.ur.findex, 0, e.ur.phase);
+                    else fold.add(0, 0.0f, 0, 0.0f);
+                    if (ub.valid) fold.add(ub.idx, ub.findex, 0, ub.phase);
+                    else fold.add(0, 0.0f, 0, 0.0f);
+                    fold.finish(m, 2, N, 1);
+                    if (e.ur.nan || ub.nan) m.status = kStatusFixup;
+                }
+                bound_check(fe, (long long)A.frames);
+                meta_put_est(&A.meta[fe], m);
+                WRec r;
+                r.rate = m.rate;
+                r.scale = m.scale;
+                r.mx = e.mx;
+                r.t_off = m.t_off;
+                r.ok = m.status == 0 ? 1u : 0u;
+                r.mxs = 0u;
+                r.rmin = __float_as_uint(kBig);
+                r.fl = 0u;
+                ring[ke % RING] = r;
+            }
+            est += EPU;
+            continue;
+        }
+        // symbol unit u: half h is symbol sh of frame kh
+        const bool live = kh < nk;
+        const unsigned f = w + (live ? kh : 0u) * Wn;
+        const WRec R = ring[(live ? kh : kmax) % RING];
+        lphy_frame_meta m{};
+        m.rate = R.rate;
+        m.scale = R.scale;
+        m.t_off = R.t_off;
+        m.status = R.ok ? 0 : -1;
+        m.have_sync = 1;
+        const SymCtx c = sym_ctx(A, f, live ? sh : 0u, live, N, m);
+        cf32 v[64];
+        {
+            const cf32* src = A.iq + (unsigned long long)f * A.frame_samples + c.base + (unsigned)l;
+            if (live) {
+                iq_check(A, f, (long long)c.base + l + LPS * 63);
+#pragma unroll
+                for (int e = 0; e < 64; ++e) v[e] = src[LPS * e];
+            } else {
+#pragma unroll
+                for (int e = 0; e < 64; ++e) v[e] = czero();
+            }
+        }
+        if (__ballot(live && kh != rot_k)) {
+            const WRot rt = wrot_lane<SF, MODE>(R.rate, R.scale);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) Qr[b] = rt.q[b];
+#pragma unroll
+            for (int a = 0; a < 8; ++a)
+                Pr[a] = cf32{__shfl(rt.p.x, h * LPS + a, 64), __shfl(rt.p.y, h * LPS + a, 64)};
+            rot_k = kh;
+        }
+        float amax = 0.0f;
+        const unsigned d0 = ((c.base + (unsigned)l) & (unsigned)(N - 1)) << 3;
+        cf32 dq[2][8];
+        auto ld_chunk = [&](int q, cf32 (&ds)[8]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int e = 8 * q + i;
+                if constexpr (DECH) ds[i] = lds_ld(dnl, (int)((d0 + (unsigned)((LPS * e) << 3)) & (unsigned)(8 * N - 1)));
+                if constexpr (M0) ds[i] = dnl[l + LPS * e];
+            }
+        };
+        ld_chunk(0, dq[0]);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (q + 1 < 8) ld_chunk(q + 1, dq[(q + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int e = 8 * q + i;
+                cf32 p = v[e];
+                if constexpr (DECH) p = cmul(p, dq[q & 1][i]);
+                amax = max3_abs(amax, p.x, p.y);
+                if constexpr (M0) p = cmul(p, dq[q & 1][i]);
+                v[e] = cmul_fma(cmul_fma(p, Qr[i]), Pr[q]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        wpass1<SF, true>(v, ctw(A.tw));
+        int hx = h, lx = l;
+        asm volatile("" : "+v"(hx), "+v"(lx));
+        WTw<SF> T;
+        T.load(A.tw, lx);
+        const int b = wbuf_acquire<L::NBUF>(locks, bstart);
+        wexchange<SF>(v, (cf32*)(pool + b * W::BUF), hx, lx);
+        wait_lgkm0();
+        wbuf_release(locks, b);
+        wpass2<SF, true>(v, T, A.tw, l);
+        unsigned k1 = 0u, k2 = 0u;
+#pragma unroll
+        for (int e = 0; e < 64; ++e) {
+            const float m2 = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
+            const unsigned key = (__float_as_uint(m2) & ~63u) | (unsigned)e;
+            k2 = med3_u32(k1, k2, key);
+            k1 = k1 > key ? k1 : key;
+        }
+        unsigned K1, K2;
+        wave_top2_merge<LPS>(k1, k2, h, K1, K2);
+        const unsigned long long bm = __ballot(k1 == K1);
+        const unsigned long long hm = (bm >> (LPS * h)) & ((1ull << (LPS & 63)) - 1);
+        ArgMax2 b2;
+        b2.v = __uint_as_float(K1 & ~63u);
+        b2.v2 = __uint_as_float(K2 | 63u);
+        b2.i = (__ffsll((long long)hm) - 1) + LPS * (int)(K1 & 63u);
+        float am = 1.0f;
+        if constexpr (M0) {
+#pragma unroll
+            for (int off = 1; off < LPS; off <<= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
+            am = amax;
+        }
+        const float cb1 = cert_bound<SF>(c.rate, c.start, 1.0f, kWaveExtra);
+        const float cgap = cert_gap(b2);
+        const bool cert = cgap > 4.0f * (cb1 * am) && (float)N * 1.41421366f * am * 1.0001f < 1e18f &&
+                          am >= 1e-20f && b2.v >= 1e-30f;
+        const bool redo = c.ok && (!cert || A.debug_recheck);
+        if (live && l == 0) {
+            const uint16_t out = redo ? kSymRecheck : (uint16_t)b2.i;
+            if (c.have_sync && c.s < 2) store_symbol(A, c, c.ok ? out : (uint16_t)0);
+            else if (c.ok) store_symbol(A, c, out);
+            if (redo) A.meta[c.f].status = kStatusRecheck;
+        }
+        if (spec) {
+            // the half's share of its frame's speculation state: max-abs of its
+            // samples (NaN dropped as fmaxf does: the NaN flag carries it), the
+            // certificate ratio, the flags; folded into the frame's record
+            float mm = c.ok ? amax : 0.0f;
+            const cf32 q0 = v[0] * v[0];
+            const float q2 = q0.x + q0.y;
+            unsigned fl = (c.ok && !(q2 == q2)) ? 1u : 0u;
+            float rr = kBig;
+            if (c.ok && l == 0) {
+                if (redo) fl |= 2u;
+                else rr = cgap * __builtin_amdgcn_rcpf(cb1) * (1.0f - 4.0f * kU);
+            }
+#pragma unroll
+            for (int off = LPS / 2; off >= 1; off >>= 1) {
+                mm = fmaxf(mm, __shfl_xor(mm, off, 64));
+                rr = fminf(rr, __shfl_xor(rr, off, 64));
+                fl |= (unsigned)__shfl_xor((int)fl, off, 64);
+            }
+            if (live && l == 0 && R.ok) {
+                WRec* rp = &ring[kh % RING];
+                atomicMax(&rp->mxs, __float_as_uint(mm));
+                atomicMin(&rp->rmin, __float_as_uint(rr));
+                if (fl) atomicOr(&rp->fl, fl);
+            }
+            // the half holding a frame's last symbol closes that frame
+            const unsigned long long cm = __ballot(live && sh == S - 1 && l == 0);
+            if (cm) {
+                const int src = __ffsll((long long)cm) - 1;
+                const unsigned kc = (unsigned)__builtin_amdgcn_readlane((int)kh, src);
+                wait_lgkm0();  // this wave's atomics above are done
+                const WRec Rc = ring[kc % RING];
+                if (Rc.ok)
+                    wclose2<SF, MODE>(ka, pool, locks, (const lds_cf32*)dnl, w + kc * Wn, Rc.rate, Rc.scale,
+                                      Rc.t_off, Rc.mx, __uint_as_float(Rc.mxs), __uint_as_float(Rc.rmin),
+                                      (Rc.fl & 1u) != 0, (Rc.fl & 2u) != 0);
+            }
+        }
+        sh += SPW;
+        if (sh >= S) {
+            sh -= S;
+            ++kh;
+        }
+        ++u;
     }
 }
