@@ -426,16 +426,27 @@ def write_perf_csv(path: str, run_id: str, rows: list) -> None:
 
 
 def frames_fused(sf: int) -> bool:
-    """Whether the bench frame shape takes a fused launch (k_frames up to
-    SF 8, k_wave from SF 9)."""
+    """Whether the bench frame shape takes a fused launch (every SF unless
+    LPHY_FUSED=0: k_frames up to SF 8, k_wave2s at SF 9-10, k_wave2 at 11-12;
+    lphy_hip.hip frames_fit / wave_fit)."""
     return os.environ.get("LPHY_FUSED", "1") != "0"
 
 
 def fused_kernel(sf: int) -> str:
-    """Name of the fused launch's kernel (as the PMC summaries key it):
-    k_frames up to SF 8, k_wave from SF 9 (LPHY_WAVE_MIN_SF moves it)."""
+    """Name of the fused launch's kernel, as the PMC summaries key it, by the
+    library's own rule (lphy_hip.hip wave_fit, lphy_kernels.h
+    launch_wave_mode): k_frames below LPHY_WAVE_MIN_SF (default 9);
+    above it k_wave2s where units span frames (SF 9-10, unless
+    LPHY_WAVE_SPAN=0), k_wave2 otherwise, k_wave with LPHY_WAVE_V1=1."""
     lo = int(os.environ.get("LPHY_WAVE_MIN_SF", "9"))
-    return f"k_frames<{sf}>" if sf < max(9, min(lo, 13)) else f"k_wave<{sf}>"
+    lo = lo if 9 <= lo <= 13 else 9
+    if sf < lo or sf > 12:
+        return f"k_frames<{sf}>"
+    if os.environ.get("LPHY_WAVE_V1") == "1":
+        return f"k_wave<{sf}>"
+    if sf <= 10 and os.environ.get("LPHY_WAVE_SPAN", "1") != "0":
+        return f"k_wave2s<{sf}>"
+    return f"k_wave2<{sf}>"
 
 
 def measured_traffic(kernel: str, frames: int):

@@ -152,12 +152,12 @@ inline bool frames_fit(unsigned sf, unsigned osr, int est_units, size_t total) {
     return total + 1 >= 2 * wt;
 }
 
-// Whether the fused SF 11-12 kernel (k_wave) takes this batch: a symbol per
-// wavefront (pair at SF 11), the two-symbol estimate, no window, the
-// certified rotation, and in modes 1/2 the speculative normalisation (its
-// scan covers the two estimate symbols only).
-// Lowest SF the wave-per-symbol kernel (k_wave) takes; k_frames below it
-// (same-box A/B, DESIGN §4.5: SF 10 1.64 -> 1.21 ms, SF 9 1.32 -> 1.31 ms).
+// Whether the fused SF 9-12 kernels (k_wave2 / k_wave2s, 64 x 64 values per
+// wavefront unit) take this batch: osr 1, the two-symbol estimate, no
+// window, the certified rotation, and in modes 1/2 the speculative
+// normalisation.  Hann windows, LPHY_F_EXACT_ROTATION and the pre-scan
+// schedule stay on k_frames (SF 9-10) or the separate launches (SF 11-12).
+// wave_min_sf: the lowest SF they take, k_frames below it;
 // LPHY_WAVE_MIN_SF (9..13) moves the boundary for A/B timing.
 unsigned wave_min_sf() {
     static const unsigned v = [] {
@@ -219,20 +219,23 @@ int ensure_stage(lphy_hip_ctx* c, size_t bytes) {
 
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
-// Per-call device scratch.  On a caller's stream it is allocated and
-// released in that stream's order (hipMallocAsync / hipFreeAsync), so its
-// lifetime is exactly the call's kernels.  The producer and compensation
-// entry points do not use the stream-ordered pool on the null stream (a
-// transcript run once read a recycled block there): a plain
-// hipMalloc, and the release waits for the stream.  demod_batch pools on
-// every stream (`pool_null`), so its device callers never synchronise.  The
-// *_host entry points lend a slice of their staging buffer instead (they
-// hold c->mu and synchronise before returning).
+// Per-call device scratch of the device-buffer entry points, one policy for
+// all of them (demod_batch's SF 11-12 speculation records, the producer's
+// phases, the compensation's shift buffer): allocated and released in the
+// caller's stream order (hipMallocAsync / hipFreeAsync from the stream-
+// ordered pool, the null stream included), so its lifetime is exactly the
+// call's kernels and no caller synchronises.  (Round 2-3 kept a plain
+// hipMalloc plus a stream sync for the producers on the null stream, over a
+// transcript that read a recycled block once and was never reproduced;
+// round 3 removed the scratch-lowered table that was its likely cause,
+// DESIGN §8.)  The *_host entry points lend a slice of their reserved
+// staging instead (they run on the context's own stream and synchronise it
+// before returning).
 struct StreamScratch {
     void* p = nullptr;
     hipStream_t st;
     bool owned = false, pooled = false, pool_null = false;
-    explicit StreamScratch(hipStream_t s, void* lent = nullptr, bool pool_on_null = false)
+    explicit StreamScratch(hipStream_t s, void* lent = nullptr, bool pool_on_null = true)
         : p(lent), st(s), pool_null(pool_on_null) {}
     int get(size_t bytes) {
         if (p) return 0;  // lent by the caller
@@ -484,7 +487,7 @@ int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t f
     // prologue, the symbols and the fix-up in this one call
     // (per call, in the caller's stream order: released after this call's
     // last kernel, k_post, which is launched below while `spec` is in scope)
-    StreamScratch spec(st, lent_spec, true);
+    StreamScratch spec(st, lent_spec);
     if (!fused && A.spec && c->sf >= 11 && c->osr == 1 && !A.exact_rotation && total >= 2 &&
         (all || (stages & both) == both)) {
         if (int rc = spec.get(frames * sizeof(uint4))) return rc;

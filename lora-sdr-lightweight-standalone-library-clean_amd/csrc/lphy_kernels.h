@@ -74,7 +74,7 @@ struct DemodArgs {
     // atomic max / min), flags (1 NaN, 2 symbol left open)}; nullptr = off
     uint4* spec_big;
     int debug_recheck;       // LPHY_F_DEBUG_RECHECK: mark estimated frames kStatusRecheck before k_demod
-    int wave;                // the fused SF 11-12 launch (k_wave) ran (it settles its frames itself)
+    int wave;                // the fused SF 9-12 launch (k_wave2 / k_wave2s) ran (it settles its frames itself)
     // persistent demod workers: symbol stride per step split into whole
     // frames + symbols (host-computed, so the kernel never divides)
     unsigned stride_f, stride_s;
