@@ -26,6 +26,8 @@
 #include <thread>
 #include <vector>
 #include <sched.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include "../../include/lphy_hip.h"
@@ -299,6 +301,7 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
     *frames_out = 0;
     if (tail_bytes) *tail_bytes = 0;
 
+    if (hipSetDevice(lphy_hip_ctx_device(ctx)) != hipSuccess) return -EIO;
     int rc = 0;
     size_t next = 0;  // stream frames read so far
     unsigned long long chunk = 0;
@@ -306,7 +309,40 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
     int nreaders = usable_cpus() - 1;
     if (const char* e = getenv("LPHY_STREAM_READERS")) nreaders = atoi(e);
     nreaders = nreaders < 1 ? 1 : (nreaders > 32 ? 32 : nreaders);
-    ReaderPool pool(seekable && chunk_bytes >= kParMin ? nreaders : 0);
+    // LPHY_STREAM_MMAP=1 (experiment, tools/stream_bench.py): a regular file
+    // is mapped and the mapping registered with HIP (pinned in place), so the
+    // copy engine reads the page cache directly - no host copy; falls back
+    // to the readers when mapping or registration fails
+    char* map = nullptr;
+    size_t map_len = 0, map_skip = 0, map_avail = 0;
+    off_t map_base = 0;
+    bool mapped = false;
+    if (seekable && getenv("LPHY_STREAM_MMAP") && getenv("LPHY_STREAM_MMAP")[0] == '1') {
+        struct stat stt;
+        const off_t cur = ::lseek(fd, 0, SEEK_CUR);
+        if (cur >= 0 && fstat(fd, &stt) == 0 && S_ISREG(stt.st_mode) && stt.st_size > cur) {
+            const long pg = sysconf(_SC_PAGESIZE);
+            map_base = cur & ~(off_t)(pg - 1);
+            map_skip = (size_t)(cur - map_base);
+            map_avail = (size_t)(stt.st_size - cur);
+            if (map_avail > max_frames * frame_bytes) map_avail = max_frames * frame_bytes;
+            map_len = map_skip + map_avail;
+            void* m = mmap(nullptr, map_len, PROT_READ, MAP_SHARED, fd, map_base);
+            if (m != MAP_FAILED) {
+                map = static_cast<char*>(m);
+                (void)madvise(map, map_len, MADV_SEQUENTIAL);
+                if (hipHostRegister(map, map_len, hipHostRegisterReadOnly) == hipSuccess) {
+                    mapped = true;
+                } else {
+                    (void)hipGetLastError();
+                    munmap(map, map_len);
+                    map = nullptr;
+                }
+            }
+        }
+    }
+    size_t map_used = 0;
+    ReaderPool pool(!mapped && seekable && chunk_bytes >= kParMin ? nreaders : 0);
     StreamState* S = nullptr;
     Slot* sl = nullptr;
     hipStream_t copy_st = nullptr, comp_st = nullptr;
@@ -339,7 +375,15 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
         size_t want = chunk_bytes;
         if (max_frames - next < chunk_frames) want = (max_frames - next) * frame_bytes;
         if (want == 0) break;
-        const long long got = read_chunk(&pool, fd, seekable, s.pin_iq, want);
+        const char* src = s.pin_iq;
+        long long got;
+        if (mapped) {  // the registered mapping itself is the copy's source
+            got = (long long)(want < map_avail - map_used ? want : map_avail - map_used);
+            src = map + map_skip + map_used;
+            map_used += (size_t)got;
+        } else {
+            got = read_chunk(&pool, fd, seekable, s.pin_iq, want);
+        }
         if (got < 0) { rc = -EIO; goto done; }
         const size_t nf = (size_t)got / frame_bytes;
         if ((size_t)got % frame_bytes) {
@@ -348,7 +392,7 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
             if (tail_bytes) *tail_bytes = (size_t)got % frame_bytes;
         }
         if (nf == 0) break;
-        ST_OK(hipMemcpyAsync(s.d_iq, s.pin_iq, nf * frame_bytes, hipMemcpyHostToDevice, copy_st));
+        ST_OK(hipMemcpyAsync(s.d_iq, src, nf * frame_bytes, hipMemcpyHostToDevice, copy_st));
         ST_OK(hipEventRecord(s.h2d, copy_st));
         ST_OK(hipStreamWaitEvent(comp_st, s.h2d, 0));
         ST_OK(hipMemsetAsync(s.d_meta, 0, nf * sizeof(lphy_frame_meta), comp_st));
@@ -378,5 +422,11 @@ done:
     if (copy_st) (void)hipStreamSynchronize(copy_st);
     if (sl)
         for (int k = 0; k < NSLOT; ++k) sl[k].busy = false;
+    if (mapped) {
+        (void)hipHostUnregister(map);
+        munmap(map, map_len);
+        // the fd's offset after the bytes consumed, as the readers leave it
+        (void)::lseek(fd, map_base + (off_t)(map_skip + map_used), SEEK_SET);
+    }
     return rc;
 }
