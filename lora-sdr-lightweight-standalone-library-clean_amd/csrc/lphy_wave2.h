@@ -51,7 +51,11 @@ typedef __attribute__((address_space(3))) unsigned lds_u32;
 // wait ends.
 template <int NBUF>
 __device__ __forceinline__ int wbuf_acquire(lds_u32* locks, int start) {
-    for (;;) {
+    // (a safety cap: after ~2^20 sweeps - far beyond any holder's ~1 us -
+    // the wave proceeds with its first choice rather than spin forever; the
+    // exchange may then be wrong, which the parity tests would show, but
+    // the GPU never hangs on a lost lock)
+    for (unsigned spin = 0; spin < (1u << 20); ++spin) {
         int got = -1;
         if ((threadIdx.x & 63) == 0) {
 #pragma unroll
@@ -70,6 +74,7 @@ __device__ __forceinline__ int wbuf_acquire(lds_u32* locks, int start) {
         if (got >= 0) return got;
         __builtin_amdgcn_s_sleep(2);
     }
+    return start;
 }
 // Give the buffer back once this wave's reads of it are done (release: the
 // compiler orders the store after them; the LDS serves one wave's requests
