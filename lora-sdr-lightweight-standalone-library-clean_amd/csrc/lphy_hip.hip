@@ -209,9 +209,10 @@ bool fused_enabled() {
 
 int ensure_stage(lphy_hip_ctx* c, size_t bytes) {
     if (c->stage_bytes >= bytes) return 0;
-    if (c->d_stage) (void)hipFree(c->d_stage);
+    void* old = c->d_stage;
     c->d_stage = nullptr;
     c->stage_bytes = 0;
+    if (old) HIP_OK(hipFree(old));
     HIP_OK(hipMalloc(&c->d_stage, bytes));
     c->stage_bytes = bytes;
     return 0;
@@ -722,10 +723,8 @@ size_t host_stage_bytes(const lphy_hip_ctx* c, size_t frames, size_t frame_sampl
 
 int ensure_host_stage(lphy_hip_ctx* c, size_t bytes) {
     if (c->stage_bytes >= bytes) return 0;
-    if (c->d_stage) {
-        HIP_OK(hipStreamSynchronize(c->stream));
-        (void)hipFree(c->d_stage);
-    }
+    // the old staging may still be read by this context's stream
+    if (c->d_stage) HIP_OK(hipStreamSynchronize(c->stream));
     return ensure_stage(c, bytes);
 }
 }  // namespace

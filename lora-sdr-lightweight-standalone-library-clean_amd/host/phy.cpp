@@ -14,7 +14,9 @@
 //   * the reference's stateless free functions (lora_decode, lora_modulate)
 //     use a context per calling thread, created by that thread's first
 //     init() / lora_demod_init() (or its first call);
-//   * the shared tables are the one process-wide cache (read-only).
+//   * the shared tables are the one process-wide cache (read-only); a freed
+//     workspace's context goes back to a per-configuration pool for the
+//     next init() (no device allocation on workspace churn).
 #include <lora_phy/phy.hpp>
 #include <lphy_hip.h>
 
@@ -64,16 +66,62 @@ lphy_hip_ctx* base_ctx(unsigned sf, unsigned bw_hz, int window, int* err) {
     return c;
 }
 
+// Contexts of freed workspaces (and of ended threads) wait here, per
+// (sf, bw, window), for the next init() / lora_demod_init() of that
+// configuration: a workspace churn costs no device allocation after the
+// first, and the device memory is held until the process exits (at most
+// the peak number of live workspaces' contexts).  Never destroyed, like
+// the table cache, so no HIP call runs during static teardown.
+using CtxKey = std::tuple<unsigned, unsigned, int>;
+struct CtxPool {
+    std::mutex mu;
+    std::map<CtxKey, std::vector<lphy_hip_ctx*>> idle;
+    std::unordered_map<const lphy_hip_ctx*, CtxKey> key_of;
+};
+CtxPool& ctx_pool() {
+    static CtxPool* p = new CtxPool;
+    return *p;
+}
+
+void release_ctx(lphy_hip_ctx* c) {
+    if (!c) return;
+    CtxPool& p = ctx_pool();
+    std::lock_guard<std::mutex> lk(p.mu);
+    auto it = p.key_of.find(c);
+    if (it == p.key_of.end()) return;  // not ours
+    p.idle[it->second].push_back(c);
+}
+
 // A context of one's own over the shared tables, staging reserved for
 // `samples` samples per call.
 lphy_hip_ctx* own_ctx(unsigned sf, unsigned bw_hz, unsigned osr, int window, size_t samples, int* err) {
-    lphy_hip_ctx* b = base_ctx(sf, bw_hz, window, err);
-    if (!b) return nullptr;
+    const CtxKey key = std::make_tuple(sf, bw_hz, window);
     lphy_hip_ctx* c = nullptr;
-    int rc = lphy_hip_ctx_share(&c, b, osr ? osr : 1u);
+    {
+        CtxPool& p = ctx_pool();
+        std::lock_guard<std::mutex> lk(p.mu);
+        auto it = p.idle.find(key);
+        if (it != p.idle.end() && !it->second.empty()) {
+            c = it->second.back();
+            it->second.pop_back();
+        }
+    }
+    int rc = 0;
+    if (c) {
+        rc = lphy_hip_ctx_set_osr(c, osr ? osr : 1u);
+    } else {
+        lphy_hip_ctx* b = base_ctx(sf, bw_hz, window, err);
+        if (!b) return nullptr;
+        rc = lphy_hip_ctx_share(&c, b, osr ? osr : 1u);
+        if (!rc) {
+            CtxPool& p = ctx_pool();
+            std::lock_guard<std::mutex> lk(p.mu);
+            p.key_of.emplace(c, key);
+        }
+    }
     if (!rc) rc = lphy_hip_ctx_reserve(c, 1, samples);
     if (rc) {
-        lphy_hip_ctx_destroy(c);
+        release_ctx(c);
         if (err) *err = rc;
         return nullptr;
     }
@@ -85,7 +133,7 @@ lphy_hip_ctx* own_ctx(unsigned sf, unsigned bw_hz, unsigned osr, int window, siz
 struct ThreadCtx {
     std::map<std::tuple<unsigned, unsigned, unsigned>, lphy_hip_ctx*> m;
     ~ThreadCtx() {
-        for (auto& kv : m) lphy_hip_ctx_destroy(kv.second);
+        for (auto& kv : m) release_ctx(kv.second);
     }
 };
 thread_local ThreadCtx t_ctx;
@@ -122,10 +170,16 @@ lphy_hip_ctx* ws_ctx(const lora_workspace* ws, unsigned sf, unsigned osr, int* e
     std::unique_lock<std::shared_mutex> lk(ws_mu);
     auto r = ws_map.emplace(ws, c);
     if (!r.second) {  // another thread got there first
-        lphy_hip_ctx_destroy(c);
+        release_ctx(c);
         return r.first->second;
     }
     return c;
+}
+
+lphy_hip_ctx* ws_ctx_if_any(const lora_workspace* ws) {
+    std::shared_lock<std::shared_mutex> lk(ws_mu);
+    auto it = ws_map.find(ws);
+    return it != ws_map.end() ? it->second : nullptr;
 }
 
 // lora_demod_workspace keeps its context pointer in the reference layout's
@@ -208,7 +262,7 @@ int init(lora_workspace* ws, const lora_params* cfg) {  // phy.cpp:27-52
         std::unique_lock<std::shared_mutex> lk(ws_mu);
         auto it = ws_map.find(ws);
         if (it != ws_map.end()) {
-            lphy_hip_ctx_destroy(it->second);  // re-init: the new configuration wins
+            release_ctx(it->second);  // re-init: the new configuration wins
             it->second = c;
         } else {
             ws_map.emplace(ws, c);
@@ -234,8 +288,12 @@ ssize_t decode(lora_workspace* ws, const uint16_t* symbols, size_t symbol_count,
     if (!ws || !symbols || !payload) return -EINVAL;
     if (symbol_count % 2) return -EINVAL;  // LoRaDecoder.cpp:10
     if (symbol_count / 2 > payload_cap) return -ERANGE;  // checked before writing
+    // decode reads symbols only, so a workspace init() never saw (the
+    // reference's decode needs none of its fields) takes this thread's
+    // decoder context rather than one made for its unset SF
     int err = -ENODEV;
-    lphy_hip_ctx* c = ws_ctx(ws, deduce_sf(ws), get_osr(ws), &err);
+    lphy_hip_ctx* c = ws_ctx_if_any(ws);
+    if (!c) c = decode_ctx(&err);
     if (!c) return err;
     lphy_frame_meta m{};
     int rc = lphy_hip_decode_host(c, symbols, symbol_count, payload, &m);
@@ -331,7 +389,7 @@ int demodulate_batch(const lora_workspace* ws, const std::complex<float>* iq, si
 // ---------------------------------------------------------------------------
 void lora_demod_init(lora_demod_workspace* ws, unsigned sf, window_type win,
                      std::complex<float>* scratch, size_t max_samples) {  // LoRaDemod.cpp:11-33
-    if (lphy_hip_ctx* old = demod_ws_ctx(ws)) lphy_hip_ctx_destroy(old);  // re-init without free
+    if (lphy_hip_ctx* old = demod_ws_ctx(ws)) release_ctx(old);  // re-init without free
     ws->N = size_t(1) << sf;
     ws->window_kind = win;
     fill_window(ws->window, ws->N, win);
@@ -356,7 +414,7 @@ void lora_demod_init(lora_demod_workspace* ws, unsigned sf, window_type win,
 }
 
 void lora_demod_free(lora_demod_workspace* ws) {  // LoRaDemod.cpp:35-48
-    if (lphy_hip_ctx* c = demod_ws_ctx(ws)) lphy_hip_ctx_destroy(c);
+    if (lphy_hip_ctx* c = demod_ws_ctx(ws)) release_ctx(c);
     std::memset(ws->fft_buf, 0, sizeof ws->fft_buf);
     ws->detector = nullptr;
     ws->fft = nullptr;

@@ -45,11 +45,12 @@ def _nan_bits_equal(a, b):
 # max-abs over team pairs of 4 and 32 lanes (NaN / inf there must reach the
 # exact re-run as the 2-symbol scan made them)
 @pytest.mark.parametrize("sf,osr", [(7, 1), (9, 1), (11, 1), (8, 2), (5, 1), (8, 1)])
-@pytest.mark.parametrize("flags", [0, 32, 64])
+@pytest.mark.parametrize("flags", [0, 32, 64])  # 32 = F_DECODE, 64 = F_EXACT_ROTATION
 def test_nonfinite_frames_all_modes(oracle, lphy, sf, osr, flags):
     iq = _frames(oracle, sf, osr, 6, seed=sf * 10 + osr)
     nf, fs = iq.shape
-    d = lphy.Demodulator(sf, osr=osr)
+    # flags 64 = LPHY_F_EXACT_ROTATION: the test build's comparison flag
+    d = lphy.Demodulator(sf, osr=osr, test_build=flags == lphy.F_EXACT_ROTATION)
     modes = [lphy.MODE_DEMODULATE, lphy.MODE_LORA_DEMODULATE]
     if osr == 1:
         modes.append(lphy.MODE_DECHIRP_LORA_DEMODULATE)
