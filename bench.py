@@ -427,7 +427,7 @@ def write_perf_csv(path: str, run_id: str, rows: list) -> None:
 
 def frames_fused(sf: int) -> bool:
     """Whether the bench frame shape takes a fused launch (every SF unless
-    LPHY_FUSED=0: k_frames up to SF 8, k_wave2s at SF 9-10, k_wave2 at 11-12;
+    LPHY_FUSED=0: k_frames up to SF 8, k_wave2s at SF 9, k_wave at 10-12;
     lphy_hip.hip frames_fit / wave_fit)."""
     return os.environ.get("LPHY_FUSED", "1") != "0"
 
@@ -435,18 +435,21 @@ def frames_fused(sf: int) -> bool:
 def fused_kernel(sf: int) -> str:
     """Name of the fused launch's kernel, as the PMC summaries key it, by the
     library's own rule (lphy_hip.hip wave_fit, lphy_kernels.h
-    launch_wave_mode): k_frames below LPHY_WAVE_MIN_SF (default 9);
-    above it k_wave2s where units span frames (SF 9-10, unless
-    LPHY_WAVE_SPAN=0), k_wave2 otherwise, k_wave with LPHY_WAVE_V1=1."""
+    wave_kind): k_frames below LPHY_WAVE_MIN_SF (default 9); above it
+    k_wave2s at SF 9 and k_wave at SF 10-12, or the kernel LPHY_WAVE=1 | 2 |
+    2s names."""
     lo = int(os.environ.get("LPHY_WAVE_MIN_SF", "9"))
     lo = lo if 9 <= lo <= 13 else 9
     if sf < lo or sf > 12:
         return f"k_frames<{sf}>"
-    if os.environ.get("LPHY_WAVE_V1") == "1":
-        return f"k_wave<{sf}>"
-    if sf <= 10 and os.environ.get("LPHY_WAVE_SPAN", "1") != "0":
+    w = os.environ.get("LPHY_WAVE", "")
+    if w == "2s" and sf <= 10:
         return f"k_wave2s<{sf}>"
-    return f"k_wave2<{sf}>"
+    if w == "2":
+        return f"k_wave2<{sf}>"
+    if w == "1" or sf >= 10:
+        return f"k_wave<{sf}>"
+    return f"k_wave2s<{sf}>"
 
 
 def measured_traffic(kernel: str, frames: int):

@@ -2588,41 +2588,43 @@ int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symb
     return 0;
 }
 
-// Fused SF 11-12 path (lphy_wave.h): one 256-thread workgroup per CU (its
-// LDS), four independent waves each.
-// k_wave2 (lphy_wave2.h, two waves per SIMD) unless LPHY_WAVE_V1=1 (A/B:
-// the one-wave-per-SIMD k_wave)
-inline bool wave_v1() {
-    static int env = -1;
-    if (env < 0) {
-        const char* e = getenv("LPHY_WAVE_V1");
-        env = (e && e[0] == '1') ? 1 : 0;
-    }
-    return env == 1;
-}
+// Fused wave-per-symbol path, SF 9-12: which kernel.
+//   k_wave   (lphy_wave.h): one wave per SIMD, 256-thread workgroups, the
+//            next symbols staged through LDS by DMA while a symbol computes;
+//   k_wave2  (lphy_wave2.h): two waves per SIMD, IQ loaded straight into
+//            registers, LDS exchange buffers shared under locks;
+//   k_wave2s (lphy_wave2.h, SF 9-10): k_wave2 with units spanning frames.
+// Defaults follow the round-4 measurements: k_wave2s at SF 9,
+// k_wave at SF 10-12.  LPHY_WAVE=1 | 2 | 2s picks one (A/B; 2s only at
+// SF 9-10).
+enum class WaveKind { V1, V2, V2S };
 
-// SF 9-10: units spanning frames (k_wave2s) unless LPHY_WAVE_SPAN=0 (A/B)
-inline bool wave_span() {
-    static int env = -1;
-    if (env < 0) {
-        const char* e = getenv("LPHY_WAVE_SPAN");
-        env = (e && e[0] == '0') ? 0 : 1;
+template <int SF>
+WaveKind wave_kind() {
+    static int env = -2;
+    if (env == -2) {
+        const char* e = getenv("LPHY_WAVE");
+        env = !e ? -1 : (e[0] == '1' ? 0 : (e[0] == '2' && e[1] == 's' ? 2 : (e[0] == '2' ? 1 : -1)));
     }
-    return env == 1;
+    if (env == 0) return WaveKind::V1;
+    if (env == 1) return WaveKind::V2;
+    if (env == 2 && WGeo<SF>::SPW >= 4) return WaveKind::V2S;
+    return SF == 9 ? WaveKind::V2S : WaveKind::V1;
 }
 
 template <int SF, int MODE>
 int launch_wave_mode(const DemodArgs& A, hipStream_t st) {
     FrameArgs P{};
     P.A = A;
-    if (!wave_v1()) {
+    const WaveKind kind = wave_kind<SF>();
+    if (kind != WaveKind::V1) {
         constexpr unsigned WPB = W2Lds<SF, MODE>::WPB;
         unsigned long long blocks = (unsigned long long)cu_count();
         const unsigned long long need = (A.frames + WPB - 1) / WPB;
         if (blocks > need) blocks = need;
         P.waves = (unsigned)(blocks * WPB);
         if constexpr (WGeo<SF>::SPW >= 4) {
-            if (wave_span()) {
+            if (kind == WaveKind::V2S) {
                 hipLaunchKernelGGL((k_wave2s<SF, MODE>), dim3((unsigned)blocks), dim3(64 * WPB), 0, st, P);
                 HIP_OK(hipGetLastError());
                 return 0;
