@@ -25,6 +25,7 @@
 #include "lphy_kernels.h"
 #include "lphy_testing.h"
 
+#include <cstring>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -83,6 +84,11 @@ struct lphy_hip_ctx {
     std::mutex mu;
     hipStream_t stream = nullptr;
     void* d_stage = nullptr;
+    // pinned mirror of the staging's first h_stage_bytes (up to kPinnedMax):
+    // a call whose buffers fit moves them with one DMA copy each way instead
+    // of the runtime's pageable path (per-packet latency)
+    void* h_stage = nullptr;
+    size_t h_stage_bytes = 0;
     unsigned long long* d_counters = nullptr;  // [0] rechecks, [1..8] phase clocks (experiments)
     size_t stage_bytes = 0;
     // the streaming entry point's pinned slots and streams (lphy_stream.hip),
@@ -198,6 +204,23 @@ int launch_post(unsigned sf, int mode, const DemodArgs& A, const FinalArgs& F, b
 }
 
 
+// Smallest batch the fused kernels take.  They give each frame one
+// wavefront that walks its symbols in order, so a small batch leaves most
+// of the GPU idle and the separate launches (symbol-parallel k_demod) finish
+// first.  Crossovers measured per SF, mode 2 with decode, device time per
+// call (tools/fused_crossover.py, profiles/r4/fused_crossover.json); the
+// per-packet latency of the lora_phy:: API rides on the small end.
+// LPHY_FUSED_MIN_FRAMES overrides (0: always fused when the shape fits).
+size_t fused_min_frames(unsigned sf) {
+    static const long env = [] {
+        const char* e = getenv("LPHY_FUSED_MIN_FRAMES");
+        return e ? atol(e) : -1L;
+    }();
+    if (env >= 0) return (size_t)env;
+    static const size_t t[13] = {256, 256, 256, 256, 256, 256, 256, 256, 1536, 768, 384, 384, 384};
+    return t[sf <= 12 ? sf : 12];
+}
+
 bool fused_enabled() {
     static int env = -1;
     if (env < 0) {
@@ -207,6 +230,8 @@ bool fused_enabled() {
     return env == 1;
 }
 
+constexpr size_t kPinnedMax = size_t(32) << 20;
+
 int ensure_stage(lphy_hip_ctx* c, size_t bytes) {
     if (c->stage_bytes >= bytes) return 0;
     void* old = c->d_stage;
@@ -215,6 +240,14 @@ int ensure_stage(lphy_hip_ctx* c, size_t bytes) {
     if (old) HIP_OK(hipFree(old));
     HIP_OK(hipMalloc(&c->d_stage, bytes));
     c->stage_bytes = bytes;
+    const size_t hb = std::min(bytes, kPinnedMax);
+    if (hb > c->h_stage_bytes) {
+        if (c->h_stage) HIP_OK(hipHostFree(c->h_stage));
+        c->h_stage = nullptr;
+        c->h_stage_bytes = 0;
+        if (hipHostMalloc(&c->h_stage, hb, hipHostMallocDefault) == hipSuccess) c->h_stage_bytes = hb;
+        else c->h_stage = nullptr;  // no pinned mirror: the calls take the pageable path
+    }
     return 0;
 }
 
@@ -398,6 +431,7 @@ void lphy_hip_ctx_destroy(lphy_hip_ctx* c) {
     }
     if (c->stream_ext && c->stream_ext_free) c->stream_ext_free(c->stream_ext);
     if (c->d_stage) (void)hipFree(c->d_stage);
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->d_counters) (void)hipFree(c->d_counters);
     c->tab.reset();  // the tables go with the last context holding them
     delete c;
@@ -480,7 +514,7 @@ int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t f
     // c: the co-running kernels slowed each other ~2x, 1.1x slower overall.)
     const bool wfit = wave_fit(c->sf, c->osr, c->window, A.est_units, total, mode, A);
     const bool fused = (all || (stages & both) == both) && !(flags & LPHY_F_UNFUSED) && fused_enabled() &&
-                       (frames_fit(c->sf, c->osr, A.est_units, total) || wfit);
+                       frames >= fused_min_frames(c->sf) && (frames_fit(c->sf, c->osr, A.est_units, total) || wfit);
     A.wave = fused && (c->sf >= 11 || wfit) ? 1 : 0;
     // SF 11-12 separate launches, modes 1/2: the speculative normalisation
     // of k_frames across workgroups (k_maxabs scans the two estimate
@@ -608,7 +642,16 @@ int compensate_impl(lphy_hip_ctx* c, float* d_iq, size_t count, float cfo, float
 }
 
 // lora_modulate (LoRaMod.cpp:8-43) for `frames` frames; `lent` (optional)
-// holds frames * (nsyms + 2) floats of per-symbol start phases.
+// holds mod_scratch_bytes(): the per-symbol start phases, and below
+// mod_walk_all_below symbols every sample's phase too.
+constexpr size_t mod_walk_all_below = 4096;
+
+size_t mod_scratch_bytes(const lphy_hip_ctx* c, size_t frames, size_t nsyms) {
+    const size_t nph = frames * (nsyms + 2);
+    return align_up(nph * sizeof(float)) +
+           (nph < mod_walk_all_below ? align_up(nph * (size_t)c->N * c->osr * sizeof(float)) : 0);
+}
+
 int modulate_impl(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames, size_t nsyms,
                   float* d_iq, float amplitude, uint8_t sync, hipStream_t st, void* lent) {
     ModArgs A{};
@@ -622,11 +665,23 @@ int modulate_impl(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames, size_t
     A.ampl = std::max(-1.0f, std::min(1.0f, amplitude));  // LoRaMod.cpp:18
     A.sync = sync;
     const size_t nph = frames * (nsyms + 2);
+    const size_t samples = nph * (size_t)c->N * c->osr;
+    // few symbols: every sample's phase from the walk, then sample-parallel
+    // sincos (a per-symbol pass would run a handful of threads N steps each)
+    const bool walk_all = nph < mod_walk_all_below;
     StreamScratch scratch(st, lent);
-    if (int rc = scratch.get(nph * sizeof(float))) return rc;
+    if (int rc = scratch.get(align_up(nph * sizeof(float)) + (walk_all ? samples * sizeof(float) : 0))) return rc;
     A.phase0 = static_cast<float*>(scratch.p);
-    hipLaunchKernelGGL(k_mod_phase, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, A);
-    hipLaunchKernelGGL(k_mod_samples, dim3((unsigned)((nph + 63) / 64)), dim3(64), 0, st, A);
+    A.phases = walk_all ? reinterpret_cast<float*>(static_cast<char*>(scratch.p) + align_up(nph * sizeof(float)))
+                        : nullptr;
+    if (walk_all) {
+        hipLaunchKernelGGL(k_mod_walk<true>, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, A);
+        hipLaunchKernelGGL(k_mod_sincos, dim3((unsigned)((samples + 255) / 256)), dim3(256), 0, st, A,
+                           (unsigned long long)samples);
+    } else {
+        hipLaunchKernelGGL(k_mod_walk<false>, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, A);
+        hipLaunchKernelGGL(k_mod_samples, dim3((unsigned)((nph + 63) / 64)), dim3(64), 0, st, A);
+    }
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -716,7 +771,7 @@ size_t host_stage_bytes(const lphy_hip_ctx* c, size_t frames, size_t frame_sampl
                         demod_layout(c, frames, frame_samples, LPHY_MODE_DEMODULATE).end);
     b = std::max(b, 2 * align_up(n * sizeof(cf32)));                                      // compensate
     b = std::max(b, align_up(syms * sizeof(uint16_t)) + align_up(n * sizeof(cf32)) +
-                        align_up(syms * sizeof(float)));                                  // modulate
+                        mod_scratch_bytes(c, 1, syms - 2));                               // modulate
     b = std::max(b, 3 * align_up(std::max<size_t>(1, frames * syms) * sizeof(uint16_t)));  // decode
     return b;
 }
@@ -752,20 +807,37 @@ int lphy_hip_demod_host(lphy_hip_ctx* c, const float* h_iq, size_t frames,
     uint8_t* d_bytes = (uint8_t*)(base + L.bytes);
     lphy_frame_meta* d_meta = (lphy_frame_meta*)(base + L.meta);
     hipStream_t st = c->stream;
-    HIP_OK(hipMemcpyAsync(d_iq, h_iq, frames * frame_samples * sizeof(cf32), hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemsetAsync(d_meta, 0, frames * sizeof(lphy_frame_meta), st));
-    rc = demod_batch_impl(c, d_iq, frames, frame_samples, d_syms,
-                          (flags & LPHY_F_DECODE) ? d_bytes : nullptr, d_meta, mode, flags, st,
-                          base + L.spec);
+    const size_t iq_n = frames * frame_samples * sizeof(cf32), meta_n = frames * sizeof(lphy_frame_meta);
+    const size_t syms_n = frames * per * sizeof(uint16_t), bytes_n = frames * (per / 2);
+    const bool decode = (flags & LPHY_F_DECODE) != 0;
+    // pinned: IQ and the zeroed records in with one copy, symbols / bytes /
+    // records out with one
+    char* h = L.spec <= c->h_stage_bytes ? (char*)c->h_stage : nullptr;
+    if (h) {
+        std::memcpy(h + L.iq, h_iq, iq_n);
+        std::memset(h + L.meta, 0, meta_n);
+        HIP_OK(hipMemcpyAsync(base, h, L.spec, hipMemcpyHostToDevice, st));
+    } else {
+        HIP_OK(hipMemcpyAsync(d_iq, h_iq, iq_n, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemsetAsync(d_meta, 0, meta_n, st));
+    }
+    rc = demod_batch_impl(c, d_iq, frames, frame_samples, d_syms, decode ? d_bytes : nullptr, d_meta, mode, flags,
+                          st, base + L.spec);
     if (rc) {
         (void)hipStreamSynchronize(st);
         return rc;
     }
-    HIP_OK(hipMemcpyAsync(h_meta, d_meta, frames * sizeof(lphy_frame_meta), hipMemcpyDeviceToHost, st));
-    if (h_syms && per)
-        HIP_OK(hipMemcpyAsync(h_syms, d_syms, frames * per * sizeof(uint16_t), hipMemcpyDeviceToHost, st));
-    if (h_bytes && (flags & LPHY_F_DECODE) && per / 2)
-        HIP_OK(hipMemcpyAsync(h_bytes, d_bytes, frames * (per / 2), hipMemcpyDeviceToHost, st));
+    if (h) {
+        HIP_OK(hipMemcpyAsync(h + L.syms, base + L.syms, L.spec - L.syms, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        std::memcpy(h_meta, h + L.meta, meta_n);
+        if (h_syms && per) std::memcpy(h_syms, h + L.syms, syms_n);
+        if (h_bytes && decode && per / 2) std::memcpy(h_bytes, h + L.bytes, bytes_n);
+        return 0;
+    }
+    HIP_OK(hipMemcpyAsync(h_meta, d_meta, meta_n, hipMemcpyDeviceToHost, st));
+    if (h_syms && per) HIP_OK(hipMemcpyAsync(h_syms, d_syms, syms_n, hipMemcpyDeviceToHost, st));
+    if (h_bytes && decode && per / 2) HIP_OK(hipMemcpyAsync(h_bytes, d_bytes, bytes_n, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     return 0;
 }
@@ -786,12 +858,27 @@ int lphy_hip_decode_host(lphy_hip_ctx* c, const uint16_t* h_syms, size_t count,
     uint8_t* d_bytes = (uint8_t*)(base + sym_b);
     lphy_frame_meta* d_meta = (lphy_frame_meta*)(base + sym_b + byte_b);
     hipStream_t st = c->stream;
-    if (count) HIP_OK(hipMemcpyAsync(d_syms, h_syms, count * sizeof(uint16_t), hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemsetAsync(d_meta, 0, sizeof(lphy_frame_meta), st));
+    const size_t end = sym_b + byte_b + meta_b;
+    char* h = end <= c->h_stage_bytes ? (char*)c->h_stage : nullptr;
+    if (h) {  // pinned: symbols and the zeroed record in, bytes and record out
+        if (count) std::memcpy(h, h_syms, count * sizeof(uint16_t));
+        std::memset(h + sym_b + byte_b, 0, sizeof(lphy_frame_meta));
+        HIP_OK(hipMemcpyAsync(base, h, end, hipMemcpyHostToDevice, st));
+    } else {
+        if (count) HIP_OK(hipMemcpyAsync(d_syms, h_syms, count * sizeof(uint16_t), hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemsetAsync(d_meta, 0, sizeof(lphy_frame_meta), st));
+    }
     rc = lphy_hip_decode_batch(c, d_syms, 1, count, d_bytes, d_meta, st);
     if (rc) {
         (void)hipStreamSynchronize(st);
         return rc;
+    }
+    if (h) {
+        HIP_OK(hipMemcpyAsync(h + sym_b, base + sym_b, byte_b + meta_b, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        std::memcpy(h_meta, h + sym_b + byte_b, sizeof(lphy_frame_meta));
+        if (count / 2) std::memcpy(h_bytes, h + sym_b, count / 2);
+        return 0;
     }
     HIP_OK(hipMemcpyAsync(h_meta, d_meta, sizeof(lphy_frame_meta), hipMemcpyDeviceToHost, st));
     if (count / 2) HIP_OK(hipMemcpyAsync(h_bytes, d_bytes, count / 2, hipMemcpyDeviceToHost, st));
@@ -854,20 +941,27 @@ int lphy_hip_modulate_host(lphy_hip_ctx* c, const uint16_t* h_syms, size_t nsyms
     const size_t samples = (nsyms + 2) * (size_t)c->N * c->osr;
     const size_t sym_b = align_up(std::max<size_t>(1, nsyms) * sizeof(uint16_t));
     const size_t iq_b = align_up(samples * sizeof(cf32));
-    int rc = ensure_host_stage(c, sym_b + iq_b + align_up((nsyms + 2) * sizeof(float)));
+    int rc = ensure_host_stage(c, sym_b + iq_b + mod_scratch_bytes(c, 1, nsyms));
     if (rc) return rc;
     char* base = (char*)c->d_stage;
     uint16_t* d_syms = (uint16_t*)base;
     float* d_iq = (float*)(base + sym_b);
     hipStream_t st = c->stream;
-    if (nsyms) HIP_OK(hipMemcpyAsync(d_syms, h_syms, nsyms * sizeof(uint16_t), hipMemcpyHostToDevice, st));
+    char* h = sym_b + iq_b <= c->h_stage_bytes ? (char*)c->h_stage : nullptr;
+    if (nsyms) {
+        if (h) std::memcpy(h, h_syms, nsyms * sizeof(uint16_t));
+        HIP_OK(hipMemcpyAsync(d_syms, h ? (const void*)h : (const void*)h_syms, nsyms * sizeof(uint16_t),
+                              hipMemcpyHostToDevice, st));
+    }
     rc = modulate_impl(c, d_syms, 1, nsyms, d_iq, amplitude, sync, st, base + sym_b + iq_b);
     if (rc) {
         (void)hipStreamSynchronize(st);
         return rc;
     }
-    HIP_OK(hipMemcpyAsync(h_iq, d_iq, samples * sizeof(cf32), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(h ? (void*)(h + sym_b) : (void*)h_iq, d_iq, samples * sizeof(cf32), hipMemcpyDeviceToHost,
+                          st));
     HIP_OK(hipStreamSynchronize(st));
+    if (h) std::memcpy(h_iq, h + sym_b, samples * sizeof(cf32));
     return 0;
 }
 

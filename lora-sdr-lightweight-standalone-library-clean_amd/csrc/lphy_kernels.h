@@ -2348,14 +2348,21 @@ __global__ __launch_bounds__(kTile) void k_post(DemodArgs A, FinalArgs F, int fi
 
 // ---------------------------------------------------------------------------
 // lora_modulate (LoRaMod.cpp:8-43 + ChirpGenerator.hpp:24-51), bit-exact.
-// Pass 1: one thread per frame walks the phase accumulator through every
-// symbol (no sincos) and records the phase at each symbol start.  Pass 2: one
-// thread per symbol regenerates its samples from that phase.
+// The phase accumulator is one float recurrence through the whole frame
+// (phase += f, f += fStep with one wrap per symbol), so some thread has to
+// walk it in order.  Batches (many symbols): pass 1, one thread per frame,
+// walks it and records the phase at each symbol start; pass 2, one thread
+// per symbol, regenerates its samples from there.  Few symbols (a single
+// frame, the reference's per-packet loop): pass 2 would be a handful of
+// threads each walking N samples with a sincos per step, so instead pass 1
+// records every sample's phase (k_mod_walk) and a sample-parallel pass
+// turns them into IQ (k_mod_sincos).
 // ---------------------------------------------------------------------------
 struct ModArgs {
     const uint16_t* syms;
     cf32* iq;
     float* phase0;           // frames * (nsyms + 2) phase at symbol start
+    float* phases;           // (walk) frames * (nsyms + 2) * N * osr phases
     unsigned long long frames, nsyms;
     int N, osr;
     float bws, ampl;
@@ -2363,8 +2370,6 @@ struct ModArgs {
 };
 
 __device__ __forceinline__ float mod_f0(const ModArgs& A, unsigned long long f, unsigned long long s) {
-    const int shift = 0;
-    (void)shift;
     uint16_t v;
     if (s < 2) {
         int sf = 0;
@@ -2377,25 +2382,83 @@ __device__ __forceinline__ float mod_f0(const ModArgs& A, unsigned long long f, 
     return (2.0f * kPi * (float)v * A.bws) / ((float)A.N * (float)A.osr);
 }
 
-__global__ void k_mod_phase(ModArgs A) {
+// Eight steps of the chirp recurrence (ChirpGenerator.hpp:39-43): f += fStep,
+// wrap once past fMax, phase += f; every rounding as the reference's loop.
+// f only grows between wraps, so when the eighth f is not past fMax none of
+// the eight is and the wrap test is skipped.
+struct ChirpWalk {
+    float fmin, fmax, fstep;
+    __device__ __forceinline__ void step8(float& fr, float& phase, float p[8]) const {
+        float g[8];
+        float x = fr;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            x += fstep;
+            g[k] = x;
+        }
+        if (g[7] > fmax) {
+            x = fr;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                x += fstep;
+                if (x > fmax) x -= (fmax - fmin);
+                g[k] = x;
+            }
+        }
+        fr = g[7];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            phase += g[k];
+            p[k] = phase;
+        }
+    }
+    __device__ __forceinline__ void step1(float& fr, float& phase) const {
+        fr += fstep;
+        if (fr > fmax) fr -= (fmax - fmin);
+        phase += fr;
+    }
+};
+
+__device__ __forceinline__ ChirpWalk chirp_walk(const ModArgs& A) {
+    ChirpWalk w;
+    w.fmin = -kPi * A.bws / (float)A.osr;
+    w.fmax = kPi * A.bws / (float)A.osr;
+    w.fstep = (2.0f * kPi * A.bws) / (float)(A.N * A.osr * A.osr);
+    return w;
+}
+
+// the symbol-end wrap (ChirpGenerator.hpp:49, evaluated in double there)
+__device__ __forceinline__ float wrap_phase(float phase) {
+    const double w = floor((double)(phase / (2.0f * kPi))) * 2 * (double)kPi;
+    return (float)((double)phase - w);
+}
+
+template <bool ALL>
+__global__ void k_mod_walk(ModArgs A) {
     const unsigned long long f = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= A.frames) return;
-    const float fmin = -kPi * A.bws / (float)A.osr;
-    const float fmax = kPi * A.bws / (float)A.osr;
-    const float fstep = (2.0f * kPi * A.bws) / (float)(A.N * A.osr * A.osr);
+    const ChirpWalk W = chirp_walk(A);
     const int step = A.N * A.osr;
     float phase = 0.0f;
     const unsigned long long ns = A.nsyms + 2;
     for (unsigned long long s = 0; s < ns; ++s) {
         A.phase0[f * ns + s] = phase;
-        float fr = fmin + mod_f0(A, f, s);
-        for (int i = 0; i < step; ++i) {
-            fr += fstep;
-            if (fr > fmax) fr -= (fmax - fmin);
-            phase += fr;
+        float fr = W.fmin + mod_f0(A, f, s);
+        int i = 0;
+        float* out = ALL ? A.phases + (f * ns + s) * (unsigned long long)step : nullptr;
+        for (; i + 8 <= step; i += 8) {
+            float p[8];
+            W.step8(fr, phase, p);
+            if constexpr (ALL) {
+                *reinterpret_cast<float4*>(out + i) = make_float4(p[0], p[1], p[2], p[3]);
+                *reinterpret_cast<float4*>(out + i + 4) = make_float4(p[4], p[5], p[6], p[7]);
+            }
         }
-        const double w = floor((double)(phase / (2.0f * kPi))) * 2 * (double)kPi;
-        phase = (float)((double)phase - w);
+        for (; i < step; ++i) {
+            W.step1(fr, phase);
+            if constexpr (ALL) out[i] = phase;
+        }
+        phase = wrap_phase(phase);
     }
 }
 
@@ -2404,21 +2467,25 @@ __global__ void k_mod_samples(ModArgs A) {
     const unsigned long long ns = A.nsyms + 2;
     if (g >= A.frames * ns) return;
     const unsigned long long f = g / ns, s = g % ns;
-    const float fmin = -kPi * A.bws / (float)A.osr;
-    const float fmax = kPi * A.bws / (float)A.osr;
-    const float fstep = (2.0f * kPi * A.bws) / (float)(A.N * A.osr * A.osr);
+    const ChirpWalk W = chirp_walk(A);
     const int step = A.N * A.osr;
     float phase = A.phase0[g];
-    float fr = fmin + mod_f0(A, f, s);
+    float fr = W.fmin + mod_f0(A, f, s);
     cf32* out = A.iq + (f * ns + s) * (unsigned long long)step;
     for (int i = 0; i < step; ++i) {
-        fr += fstep;
-        if (fr > fmax) fr -= (fmax - fmin);
-        phase += fr;
+        W.step1(fr, phase);
         float sn, cs;
         lphy_libm::sincosf_exact(phase, &sn, &cs);
-        out[i] = cf32{A.ampl * cs, A.ampl * sn};
+        out[i] = cf32{A.ampl * cs, A.ampl * sn};  // std::polar(ampl, phase)
     }
+}
+
+__global__ void k_mod_sincos(ModArgs A, unsigned long long count) {
+    const unsigned long long g = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= count) return;
+    float sn, cs;
+    lphy_libm::sincosf_exact(A.phases[g], &sn, &cs);
+    A.iq[g] = cf32{A.ampl * cs, A.ampl * sn};
 }
 
 // compensate_offsets (phy.cpp:150-180): rotation then integer time shift.

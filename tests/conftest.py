@@ -10,6 +10,12 @@ for p in (str(ROOT / "tests" / "golden"), str(ROOT / "tests"), str(PKG), str(ROO
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# The suite's small batches exercise the fused kernels: the library would
+# give a batch below fused_min_frames (lphy_hip.hip) to the separate
+# launches, which the tests reach with LPHY_F_UNFUSED and the lora_phy::
+# probes (tests/test_gpu_cxx_api.py, run with the library's defaults).
+os.environ.setdefault("LPHY_FUSED_MIN_FRAMES", "0")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) — run via gpurun")

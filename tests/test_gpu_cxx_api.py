@@ -6,6 +6,7 @@ bits, CRC flags and payload bytes over the scenarios of the reference's own
 tests (error_code, roundtrip, no_alloc, e2e_chain profiles, bit_exact on
 modulation_tests.bin, equal_power_bin, scratch_buffer_error,
 odd_symbol_count, sync_word) and impaired frames."""
+import os
 import subprocess
 from pathlib import Path
 
@@ -17,6 +18,15 @@ PKG = ROOT / "lora-sdr-lightweight-standalone-library-clean_amd"
 REF_PROBE = ROOT / "oracle" / "_ref" / "lora_phy_api_probe_ref"
 
 
+def prod_env(**kw):
+    """The probes run the drop-in with the library's own launch choices (the
+    suite's conftest forces the fused kernels for small batches; a packet
+    at a time takes the separate launches by default, fused_min_frames)."""
+    env = {k: v for k, v in os.environ.items() if k != "LPHY_FUSED_MIN_FRAMES"}
+    env.update(kw)
+    return env
+
+
 def test_cxx_api_transcript_matches_reference(tmp_path):
     if not REF_PROBE.exists():
         pytest.skip("reference probe not built (oracle/Makefile probe)")
@@ -25,14 +35,17 @@ def test_cxx_api_transcript_matches_reference(tmp_path):
                     "-o", str(exe), str(ROOT / "tests" / "cpp" / "lora_phy_api_probe.cpp"),
                     f"-L{PKG / 'lib'}", "-llora_phy_amd", f"-Wl,-rpath,{PKG / 'lib'}"], check=True)
     golden = str(ROOT / "tests" / "golden")
-    ours = subprocess.run([str(exe), golden], capture_output=True, text=True, timeout=300)
-    assert ours.returncode == 0, ours.stderr
     ref = subprocess.run([str(REF_PROBE), golden], capture_output=True, text=True, timeout=300)
     assert ref.returncode == 0, ref.stderr
-    a, b = ours.stdout.splitlines(), ref.stdout.splitlines()
-    assert len(a) == len(b) and len(b) >= 25
-    bad = [(x, y) for x, y in zip(a, b) if x != y]
-    assert not bad, "\n".join(f"ours: {x[:300]}\nref:  {y[:300]}" for x, y in bad[:5])
+    b = ref.stdout.splitlines()
+    # default launch choices, then the fused kernels forced for every call
+    for env in (prod_env(), prod_env(LPHY_FUSED_MIN_FRAMES="0")):
+        ours = subprocess.run([str(exe), golden], capture_output=True, text=True, timeout=300, env=env)
+        assert ours.returncode == 0, ours.stderr
+        a = ours.stdout.splitlines()
+        assert len(a) == len(b) and len(b) >= 25
+        bad = [(x, y) for x, y in zip(a, b) if x != y]
+        assert not bad, "\n".join(f"ours: {x[:300]}\nref:  {y[:300]}" for x, y in bad[:5])
 
 
 LW_REF_PROBE = ROOT / "oracle" / "_ref" / "lorawan_api_probe_ref"
@@ -48,7 +61,7 @@ def test_lorawan_api_transcript_matches_reference(tmp_path):
     subprocess.run(["g++", "-O2", "-std=gnu++17", f"-I{ROOT / 'include'}", "-o", str(exe),
                     str(ROOT / "tests" / "cpp" / "lorawan_api_probe.cpp"), f"-L{PKG / 'lib'}", "-llora_phy_amd",
                     f"-Wl,-rpath,{PKG / 'lib'}"], check=True)
-    ours = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    ours = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=prod_env())
     assert ours.returncode == 0, ours.stderr
     ref = subprocess.run([str(LW_REF_PROBE)], capture_output=True, text=True, timeout=300)
     assert ref.returncode == 0, ref.stderr
@@ -75,7 +88,7 @@ def test_cxx_api_threads_match_reference(tmp_path, threads, sf, frames):
                     "-o", str(exe), str(ROOT / "tests" / "cpp" / "lora_phy_threads_probe.cpp"),
                     f"-L{PKG / 'lib'}", "-llora_phy_amd", f"-Wl,-rpath,{PKG / 'lib'}", "-lpthread"], check=True)
     args = [str(threads), str(sf), str(frames)]
-    ours = subprocess.run([str(exe)] + args, capture_output=True, text=True, timeout=300)
+    ours = subprocess.run([str(exe)] + args, capture_output=True, text=True, timeout=300, env=prod_env())
     assert ours.returncode == 0, ours.stderr
     ref = subprocess.run([str(T_REF_PROBE)] + args, capture_output=True, text=True, timeout=300)
     assert ref.returncode == 0, ref.stderr
