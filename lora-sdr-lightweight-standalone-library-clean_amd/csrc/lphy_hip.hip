@@ -675,11 +675,12 @@ int modulate_impl(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames, size_t
     A.phases = walk_all ? reinterpret_cast<float*>(static_cast<char*>(scratch.p) + align_up(nph * sizeof(float)))
                         : nullptr;
     if (walk_all) {
-        hipLaunchKernelGGL(k_mod_walk<true>, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, A);
+        hipLaunchKernelGGL(k_mod_freq, dim3((unsigned)((nph + 63) / 64)), dim3(64), 0, st, A);
+        hipLaunchKernelGGL(k_mod_accumulate, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, A);
         hipLaunchKernelGGL(k_mod_sincos, dim3((unsigned)((samples + 255) / 256)), dim3(256), 0, st, A,
                            (unsigned long long)samples);
     } else {
-        hipLaunchKernelGGL(k_mod_walk<false>, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, A);
+        hipLaunchKernelGGL(k_mod_walk, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, A);
         hipLaunchKernelGGL(k_mod_samples, dim3((unsigned)((nph + 63) / 64)), dim3(64), 0, st, A);
     }
     HIP_OK(hipGetLastError());

@@ -2354,9 +2354,11 @@ __global__ __launch_bounds__(kTile) void k_post(DemodArgs A, FinalArgs F, int fi
 // walks it and records the phase at each symbol start; pass 2, one thread
 // per symbol, regenerates its samples from there.  Few symbols (a single
 // frame, the reference's per-packet loop): pass 2 would be a handful of
-// threads each walking N samples with a sincos per step, so instead pass 1
-// records every sample's phase (k_mod_walk) and a sample-parallel pass
-// turns them into IQ (k_mod_sincos).
+// threads each walking N samples with a sincos per step, so instead each
+// symbol's frequency sequence is built in parallel (k_mod_freq), one thread
+// per frame adds them up in order (k_mod_accumulate, one dependent add per
+// sample, loads a block ahead) and a sample-parallel pass turns the phases into IQ
+// (k_mod_sincos).
 // ---------------------------------------------------------------------------
 struct ModArgs {
     const uint16_t* syms;
@@ -2433,7 +2435,7 @@ __device__ __forceinline__ float wrap_phase(float phase) {
     return (float)((double)phase - w);
 }
 
-template <bool ALL>
+// Batch pass 1: the phase at every symbol start.
 __global__ void k_mod_walk(ModArgs A) {
     const unsigned long long f = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= A.frames) return;
@@ -2445,18 +2447,109 @@ __global__ void k_mod_walk(ModArgs A) {
         A.phase0[f * ns + s] = phase;
         float fr = W.fmin + mod_f0(A, f, s);
         int i = 0;
-        float* out = ALL ? A.phases + (f * ns + s) * (unsigned long long)step : nullptr;
         for (; i + 8 <= step; i += 8) {
             float p[8];
             W.step8(fr, phase, p);
-            if constexpr (ALL) {
-                *reinterpret_cast<float4*>(out + i) = make_float4(p[0], p[1], p[2], p[3]);
-                *reinterpret_cast<float4*>(out + i + 4) = make_float4(p[4], p[5], p[6], p[7]);
-            }
         }
-        for (; i < step; ++i) {
-            W.step1(fr, phase);
-            if constexpr (ALL) out[i] = phase;
+        for (; i < step; ++i) W.step1(fr, phase);
+        phase = wrap_phase(phase);
+    }
+}
+
+// Few-symbol pass 1a: each symbol's frequency sequence (ChirpGenerator.hpp:
+// 39-40; it restarts at fMin + f0 every symbol, so symbols run in parallel),
+// one thread per symbol, into phases[].
+__global__ void k_mod_freq(ModArgs A) {
+    const unsigned long long g = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long ns = A.nsyms + 2;
+    if (g >= A.frames * ns) return;
+    const ChirpWalk W = chirp_walk(A);
+    const int step = A.N * A.osr;
+    float fr = W.fmin + mod_f0(A, g / ns, g % ns);
+    float* out = A.phases + g * (unsigned long long)step;
+    int i = 0;
+    for (; (step & 3) == 0 && i + 4 <= step; i += 4) {  // 16-B aligned rows
+        float q[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            fr += W.fstep;
+            if (fr > W.fmax) fr -= (W.fmax - W.fmin);
+            q[k] = fr;
+        }
+        *reinterpret_cast<float4*>(out + i) = make_float4(q[0], q[1], q[2], q[3]);
+    }
+    for (; i < step; ++i) {
+        fr += W.fstep;
+        if (fr > W.fmax) fr -= (W.fmax - W.fmin);
+        out[i] = fr;
+    }
+}
+
+// Few-symbol pass 1b: the phase accumulator through the frame, in order
+// (ChirpGenerator.hpp:41, 49), one thread per frame: phases[] holds each
+// sample's f on entry and its phase on return.  The chain is one dependent
+// add per sample, so the loads must never be what it waits for: blocks of
+// 64 samples in registers, the next block's 16 loads issued before the
+// current block's adds (ping-pong).  Loads and stores share vmcnt, so when
+// a block starts, the 16 stores of the previous block and the 16 loads of
+// the next are younger than its own loads: the explicit vmcnt(32) says so
+// (the compiler's own analysis of the loop falls back to a near-full
+// drain).  Rows of a multiple of 64 samples (SF >= 6 at osr 1); the rest
+// take the plain loop.
+constexpr int kAccBlock = 64;
+
+__device__ __forceinline__ void acc_load(float4 (&b)[kAccBlock / 4], const float* p) {
+#pragma unroll
+    for (int k = 0; k < kAccBlock / 4; ++k) b[k] = *reinterpret_cast<const float4*>(p + 4 * k);
+}
+
+__device__ __forceinline__ void acc_run(float4 (&b)[kAccBlock / 4], float& phase, float* p) {
+    __builtin_amdgcn_s_waitcnt(0x8F70);  // vmcnt(32): this block's loads have landed
+#pragma unroll
+    for (int k = 0; k < kAccBlock / 4; ++k) {
+        float4 o;
+        phase += b[k].x;
+        o.x = phase;
+        phase += b[k].y;
+        o.y = phase;
+        phase += b[k].z;
+        o.z = phase;
+        phase += b[k].w;
+        o.w = phase;
+        *reinterpret_cast<float4*>(p + 4 * k) = o;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_mod_accumulate(ModArgs A) {
+    const unsigned long long f = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= A.frames) return;
+    const unsigned long long step = (unsigned long long)A.N * A.osr;
+    const unsigned long long ns = A.nsyms + 2;
+    float* io = A.phases + f * ns * step;
+    float phase = 0.0f;
+    if (step % kAccBlock == 0) {
+        const unsigned long long nb = ns * step / kAccBlock, per = step / kAccBlock;
+        float4 b0[kAccBlock / 4], b1[kAccBlock / 4];
+        acc_load(b0, io);
+        // (the look-ahead loads are unconditional - past the end they
+        // re-read the last block - so every path has the same VMEM count
+        // and the compiler's waits stay relaxed)
+        for (unsigned long long k = 0; k < nb; k += 2) {
+            acc_load(b1, io + (k + 1 < nb ? k + 1 : nb - 1) * kAccBlock);
+            acc_run(b0, phase, io + k * kAccBlock);
+            if ((k + 1) % per == 0) phase = wrap_phase(phase);
+            if (k + 1 >= nb) break;
+            acc_load(b0, io + (k + 2 < nb ? k + 2 : nb - 1) * kAccBlock);
+            acc_run(b1, phase, io + (k + 1) * kAccBlock);
+            if ((k + 2) % per == 0) phase = wrap_phase(phase);
+        }
+        return;
+    }
+    for (unsigned long long s = 0; s < ns; ++s) {
+        float* row = io + s * step;
+        for (unsigned long long i = 0; i < step; ++i) {
+            phase += row[i];
+            row[i] = phase;
         }
         phase = wrap_phase(phase);
     }
