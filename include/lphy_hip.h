@@ -130,10 +130,14 @@ size_t lphy_hip_syms_per_frame(const lphy_hip_ctx* ctx, size_t frame_samples,
  * Limits: frames * (frame_samples / (N*osr)) < 2^32 symbols per call and
  * frame_samples < 2^31 (32-bit symbol bookkeeping in the kernels): larger
  * batches give -ERANGE; split them across calls.
- * Memory: the fused launches (k_frames up to SF 8 and for windowed SF 9-10,
- * k_wave at SF 9-12: osr 1, no window, modes 1/2 with the speculative
- * normalisation or mode 0) allocate nothing.  The SF 11-12 separate launches
- * (LPHY_F_UNFUSED, osr > 1, a window) take per-call speculation records
+ * Launch choice: the fused launches (k_frames up to SF 8 and for windowed
+ * SF 9-10; k_wave2s at SF 9 and k_wave at SF 10-12 for osr 1, no window,
+ * modes 1/2 with the speculative normalisation or mode 0) for batches of at
+ * least a per-SF crossover (256 frames at SF <= 7 ... 384 at SF 10-12,
+ * DESIGN.md 4.7; LPHY_FUSED_MIN_FRAMES overrides), the separate
+ * symbol-parallel launches below it (a packet at a time).
+ * Memory: the fused launches allocate nothing.  The SF 11-12 separate launches
+ * (LPHY_F_UNFUSED, small batches, osr > 1, a window) take per-call speculation records
  * (16 B per frame) from the stream-ordered pool on `stream`, released in
  * stream order, so calls on different streams of one context never share
  * them; the *_host forms lend them from the reserved staging instead. */
