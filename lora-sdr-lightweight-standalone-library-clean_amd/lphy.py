@@ -26,7 +26,10 @@ PKG = Path(__file__).resolve().parent
 LIB_DIR = PKG / "lib"
 HIP_SO = LIB_DIR / "liblphy_hip.so"
 TEST_SO = LIB_DIR / "test" / "liblphy_hip.so"
-DEFAULT_SO = TEST_SO if os.environ.get("LPHY_LIB") == "test" else HIP_SO
+# LPHY_LIB=test: the test build; LPHY_LIB=<path>: another build of the
+# library (timing experiments, tools/ubench/variants.py)
+_ENV_LIB = os.environ.get("LPHY_LIB", "")
+DEFAULT_SO = TEST_SO if _ENV_LIB == "test" else (Path(_ENV_LIB) if _ENV_LIB else HIP_SO)
 SHIM_SO = LIB_DIR / "liblora_phy_amd.so"
 
 MODE_DEMODULATE = 0
