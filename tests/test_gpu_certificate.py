@@ -12,9 +12,10 @@ geometrically from 1 to 2^10 over the frame's symbols, under CFO and delay.
 Every output (symbols, sync word, cfo / time_offset bits) must equal the
 oracle's, and lphy_hip_recheck_count must show the exact re-run fired.
 
-Kernels: SF 7 k_frames; SF 9 and 11-12 k_wave2 (no window) and, with a Hann
-window, k_frames (SF 9) or the separate launches' certified k_demod (SF
-11-12)."""
+Kernels: SF 7-8 k_frames (modes 1/2: symbol tiles on the matrix cores,
+lphy_mfma.h, whose f16 roundings the certificate charges; mode 0 packed
+f32); SF 9 k_wave2s, SF 11-12 k_wave (no window) and, with a Hann window,
+k_frames (SF 9) or the separate launches' certified k_demod (SF 11-12)."""
 import numpy as np
 import pytest
 
@@ -50,12 +51,12 @@ def _two_tone_frames(oracle, sf, nf, seed):
     return np.stack(frames)
 
 
-@pytest.mark.parametrize("sf,nf", [(7, 48), (9, 20), (11, 6), (12, 4)])
+@pytest.mark.parametrize("sf,nf", [(7, 48), (8, 24), (9, 20), (11, 6), (12, 4)])
 @pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("hann", [False, True])
 def test_near_ties_straddling_the_certificate(oracle, lphy, sf, nf, mode, hann):
-    if sf == 7 and hann:
-        pytest.skip("SF 7 takes k_frames either way")
+    if sf <= 8 and hann:
+        pytest.skip("SF 7-8 take k_frames either way")
     iq = _two_tone_frames(oracle, sf, nf, seed=sf * 13 + mode + 7 * hann)
     d = lphy.Demodulator(sf, window=lphy.WINDOW_HANN if hann else lphy.WINDOW_NONE)
     d.recheck_count(reset=True)
