@@ -665,11 +665,19 @@ __device__ __forceinline__ unsigned med3_u32(unsigned a, unsigned b, unsigned c)
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
+// (row shift with bound_ctrl: lanes past the row read 0, the keys' least
+// value, and no copy of the old value is needed, so the compiler can fold
+// the shift of k2 into the v_max_u32 that consumes it)
+template <int N>
+__device__ __forceinline__ unsigned dpp_row_shl_z(unsigned v) {
+    static_assert(N >= 1 && N <= 15, "row_shl range");
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x100 | N, 0xF, 0xF, true);
+}
 template <int SF, int OFF = Geo<SF>::LPS / 2>
 __device__ __forceinline__ void team_top2_keys(unsigned& k1, unsigned& k2) {
     if constexpr (OFF >= 1) {
-        const unsigned o1 = (unsigned)dpp_row_shl<OFF>((int)k1);
-        const unsigned o2 = (unsigned)dpp_row_shl<OFF>((int)k2);
+        const unsigned o1 = dpp_row_shl_z<OFF>(k1);
+        const unsigned o2 = dpp_row_shl_z<OFF>(k2);
         k2 = med3_u32(k1, o1, k2 > o2 ? k2 : o2);
         k1 = k1 > o1 ? k1 : o1;
         team_top2_keys<SF, OFF / 2>(k1, k2);

@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <immintrin.h>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -86,13 +87,40 @@ int usable_cpus() {
     return n > 0 ? n : 1;
 }
 
-// A seekable fd (a file) is read by a pool of reader threads with pread,
-// each a contiguous part of the chunk (one thread's copy out of the page
-// cache runs at ~3 GB/s, a twentieth of PCIe); a pipe or a socket is read
-// in order.  The fd's offset is left after the bytes consumed, as read()
-// would.  Readers: LPHY_STREAM_READERS, default one per usable CPU but one
-// (the calling thread drives the GPU), at most 32.
+// A seekable fd (a file) is read by a pool of reader threads, each a
+// contiguous part of the chunk (one thread's copy out of the page cache runs
+// at ~3-5 GB/s, a tenth of PCIe); a pipe or a socket is read in order.  A
+// regular file is mapped (read-only) and the readers copy from the mapping
+// with non-temporal stores: the pinned slot is written without being read
+// first, which pread's kernel copy does, and the syscall per part goes away
+// (tools/stream_bench.py; LPHY_STREAM_COPY=pread selects the pread readers).
+// The fd's offset is left after the bytes consumed, as read() would.
+// Readers: LPHY_STREAM_READERS, default one per usable CPU but one (the
+// calling thread drives the GPU), at most 32.
 constexpr size_t kParMin = size_t(4) << 20;  // below this one read() suffices
+
+// dst 32-byte aligned; streaming stores, then a fence so the copy engine
+// (which reads the slot after the readers return) sees every byte
+__attribute__((target("avx2"))) void copy_nt_avx2(char* dst, const char* src, size_t n) {
+    size_t i = 0;
+    for (; i + 128 <= n; i += 128) {
+        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i));
+        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 32));
+        const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 64));
+        const __m256i d = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 96));
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i), a);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 32), b);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 64), c);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 96), d);
+    }
+    memcpy(dst + i, src + i, n - i);
+    _mm_sfence();
+}
+void copy_part(char* dst, const char* src, size_t n) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2 && (reinterpret_cast<uintptr_t>(dst) & 31) == 0) copy_nt_avx2(dst, src, n);
+    else memcpy(dst, src, n);
+}
 
 class ReaderPool {
   public:
@@ -114,6 +142,12 @@ class ReaderPool {
         for (auto& t : th_) t.join();
     }
     int size() const { return (int)th_.size(); }
+    // the file bytes [off, off + len) mapped at `map` (nullptr: pread)
+    void set_map(const char* map, off_t off, size_t len) {
+        map_ = map;
+        map_off_ = off;
+        map_len_ = len;
+    }
     // read [base, base + want) of fd into buf with all readers; returns the
     // bytes of the contiguous prefix read (short at EOF) or -errno
     long long read(int fd, off_t base, char* buf, size_t want) {
@@ -124,7 +158,7 @@ class ReaderPool {
         base_ = base;
         buf_ = buf;
         want_ = want;
-        part_ = (want + n - 1) / n;
+        part_ = ((want + n - 1) / n + 4095) & ~size_t(4095);  // page-aligned parts
         got_.assign(n, 0);
         pending_ = n;
         ++gen_;
@@ -161,6 +195,11 @@ class ReaderPool {
                 len = o >= want_ ? 0 : (want_ - o < part_ ? want_ - o : part_);
             }
             long long g = 0;
+            const off_t at = base + (off_t)o;
+            if (map_ && len && at >= map_off_ && (size_t)(at - map_off_) + len <= map_len_) {
+                copy_part(buf + o, map_ + (at - map_off_), len);
+                g = (long long)len;
+            }
             while ((size_t)g < len) {
                 const ssize_t r = ::pread(fd, buf + o + g, len - (size_t)g, base + (off_t)(o + (size_t)g));
                 if (r == 0) break;
@@ -185,6 +224,9 @@ class ReaderPool {
     unsigned long long gen_ = 0;
     int fd_ = -1;
     off_t base_ = 0;
+    const char* map_ = nullptr;
+    off_t map_off_ = 0;
+    size_t map_len_ = 0;
     char* buf_ = nullptr;
     size_t want_ = 0, part_ = 0;
     std::vector<long long> got_;
@@ -343,6 +385,21 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
     }
     size_t map_used = 0;
     ReaderPool pool(!mapped && seekable && chunk_bytes >= kParMin ? nreaders : 0);
+    // the readers' source mapping (regular files; LPHY_STREAM_COPY=pread: none)
+    char* rmap = nullptr;
+    size_t rmap_len = 0;
+    if (!mapped && pool.size() > 0 && !(getenv("LPHY_STREAM_COPY") && strcmp(getenv("LPHY_STREAM_COPY"), "pread") == 0)) {
+        struct stat stt;
+        if (fstat(fd, &stt) == 0 && S_ISREG(stt.st_mode) && stt.st_size > 0) {
+            rmap_len = (size_t)stt.st_size;
+            void* m = mmap(nullptr, rmap_len, PROT_READ, MAP_SHARED, fd, 0);
+            if (m != MAP_FAILED) {
+                rmap = static_cast<char*>(m);
+                (void)madvise(rmap, rmap_len, MADV_SEQUENTIAL);
+                pool.set_map(rmap, 0, rmap_len);
+            }
+        }
+    }
     StreamState* S = nullptr;
     Slot* sl = nullptr;
     hipStream_t copy_st = nullptr, comp_st = nullptr;
@@ -361,10 +418,13 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
     ST_OK(hipSetDevice(lphy_hip_ctx_device(ctx)));
     S = static_cast<StreamState*>(lphy_hip_ctx_stream_ext(
         ctx, [] { return static_cast<void*>(new StreamState); }, free_stream_state));
-    if (!S) return -ENOMEM;
+    if (!S) {
+        rc = -ENOMEM;
+        goto done;
+    }
     if ((rc = S->ensure(chunk_bytes, (per ? per : 1) * chunk_frames, (per / 2 ? per / 2 : 1) * chunk_frames,
                         chunk_frames)) != 0)
-        return rc;
+        goto done;
     sl = S->sl;
     copy_st = S->copy_st;
     comp_st = S->comp_st;
@@ -422,6 +482,7 @@ done:
     if (copy_st) (void)hipStreamSynchronize(copy_st);
     if (sl)
         for (int k = 0; k < NSLOT; ++k) sl[k].busy = false;
+    if (rmap) munmap(rmap, rmap_len);
     if (mapped) {
         (void)hipHostUnregister(map);
         munmap(map, map_len);

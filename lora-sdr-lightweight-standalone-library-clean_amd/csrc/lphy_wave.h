@@ -471,7 +471,9 @@ __device__ __forceinline__ void wdma(const DemodArgs& A, cf32* buf, const WDma& 
 // values.  Every lane of symbol h gets its top two.
 template <int CTRL>
 __device__ __forceinline__ unsigned dpp_u32(unsigned v) {
-    return (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
+    // (permutations: every lane has a source; no old value, so the move can
+    // fold into its consumer)
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
 }
 __device__ __forceinline__ void top2_add(unsigned& K1, unsigned& K2, unsigned o1, unsigned o2) {
     K2 = med3_u32(K1, o1, K2 > o2 ? K2 : o2);
