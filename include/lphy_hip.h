@@ -204,7 +204,10 @@ int lphy_hip_modulate_host(lphy_hip_ctx* ctx, const uint16_t* h_syms,
  * caller's host arrays in stream order (frame f at h_syms +
  * f*lphy_hip_syms_per_frame, h_bytes + f*(syms/2) with LPHY_F_DECODE,
  * h_meta + f).  A seekable fd is read by a pool of reader threads
- * (LPHY_STREAM_READERS, default one per usable CPU but one); the pinned
+ * (LPHY_STREAM_READERS, default one per usable CPU but one); a regular file
+ * is mapped read-only and the readers copy out of the mapping with
+ * non-temporal stores (LPHY_STREAM_COPY=pread: pread instead; as with any
+ * mapping, truncating the file during the call raises SIGBUS); the pinned
  * slots and streams stay with the context for its next call.
  * `max_frames` is their capacity in frames and is required
  * (0 gives -EINVAL): reading stops there and the rest of the stream is left

@@ -671,7 +671,11 @@ __device__ __forceinline__ unsigned med3_u32(unsigned a, unsigned b, unsigned c)
 template <int N>
 __device__ __forceinline__ unsigned dpp_row_shl_z(unsigned v) {
     static_assert(N >= 1 && N <= 15, "row_shl range");
+#ifdef LPHY_AB_DPP_OLD  // A/B timing only: the old-value form
+    return (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x100 | N, 0xF, 0xF, false);
+#else
     return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x100 | N, 0xF, 0xF, true);
+#endif
 }
 template <int SF, int OFF = Geo<SF>::LPS / 2>
 __device__ __forceinline__ void team_top2_keys(unsigned& k1, unsigned& k2) {

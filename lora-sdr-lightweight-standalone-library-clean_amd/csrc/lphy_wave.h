@@ -473,7 +473,11 @@ template <int CTRL>
 __device__ __forceinline__ unsigned dpp_u32(unsigned v) {
     // (permutations: every lane has a source; no old value, so the move can
     // fold into its consumer)
+#ifdef LPHY_AB_DPP_OLD  // A/B timing only: the old-value form
+    return (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
+#else
     return (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+#endif
 }
 __device__ __forceinline__ void top2_add(unsigned& K1, unsigned& K2, unsigned o1, unsigned o2) {
     K2 = med3_u32(K1, o1, K2 > o2 ? K2 : o2);
