@@ -677,6 +677,24 @@ __device__ __forceinline__ unsigned dpp_row_shl_z(unsigned v) {
     return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x100 | N, 0xF, 0xF, true);
 #endif
 }
+// Top two of {k1, k2, a, b} for distinct keys with k1 >= k2: the second
+// largest is max(k2, med3(k1, a, b)) (if k1 leads {k1, a, b}, the middle is
+// max(a, b); otherwise the middle is the larger of k1 and the other new
+// key, and k1 >= k2).  One v_max3_u32, one v_med3_u32 and one v_max_u32
+// per two keys, against a v_med3_u32 and a v_max_u32 per key.
+__device__ __forceinline__ void top2_pair(unsigned& k1, unsigned& k2, unsigned a, unsigned b) {
+#ifdef LPHY_AB_TOP2_SINGLE  // A/B timing only: one key at a time
+    k2 = med3_u32(k1, k2, a);
+    k1 = k1 > a ? k1 : a;
+    k2 = med3_u32(k1, k2, b);
+    k1 = k1 > b ? k1 : b;
+#else
+    const unsigned m = med3_u32(k1, a, b);
+    const unsigned t = k1 > a ? k1 : a;
+    k1 = t > b ? t : b;
+    k2 = k2 > m ? k2 : m;
+#endif
+}
 template <int SF, int OFF = Geo<SF>::LPS / 2>
 __device__ __forceinline__ void team_top2_keys(unsigned& k1, unsigned& k2) {
     if constexpr (OFF >= 1) {
@@ -707,19 +725,19 @@ __device__ __forceinline__ ArgMax2 team_argmax2_keyed_first(const cf32 (&v)[16],
             if (bin_of<SF>(e, 0) != (e % GS) * MH + (e / GS) * XS) return false;
         return true;
     }(), "bin_of separable in the lane and element digits");
-    unsigned k1 = 0u, k2 = 0u;
-#pragma unroll
-    for (int e = 0; e < G::E; ++e) {
+    static_assert(G::E % 2 == 0, "keys taken in pairs");
+    auto key_of = [&](int e) __attribute__((always_inline)) {
 #ifdef LPHY_KEY_FMA  // A/B: |X|^2 = fma(x, x, fl(y y)), scalar f32 (within cert_gap's 8 u)
         const float m2 = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
 #else
         const cf32 sq = v[e] * v[e];
         const float m2 = sq.x + sq.y;
 #endif
-        const unsigned key = (__float_as_uint(m2) & ~15u) | (unsigned)e;
-        k2 = med3_u32(k1, k2, key);
-        k1 = k1 > key ? k1 : key;
-    }
+        return (__float_as_uint(m2) & ~15u) | (unsigned)e;
+    };
+    unsigned k1 = 0u, k2 = 0u;
+#pragma unroll
+    for (int e = 0; e < G::E; e += 2) top2_pair(k1, k2, key_of(e), key_of(e + 1));
     if constexpr (LB > 0) {
         k1 = (k1 & ~(MASK & ~15u)) | ((unsigned)lam << 4);
         team_top2_keys<SF>(k1, k2);

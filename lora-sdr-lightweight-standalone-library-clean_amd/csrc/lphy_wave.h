@@ -1058,13 +1058,13 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             // low 6 bits the element; see team_argmax2_keyed_first)
             unsigned k1 = 0u, k2 = 0u;
 #pragma unroll
-            for (int e = 0; e < 64; ++e) {
+            for (int e = 0; e < 64; e += 2) {
                 // |X|^2 = fma(x, x, fl(y y)): within 2 u, inside cert_gap's 8 u;
                 // scalar f32 ops (no packed-f32 dependency pad)
-                const float m2 = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
-                const unsigned key = (__float_as_uint(m2) & ~63u) | (unsigned)e;
-                k2 = med3_u32(k1, k2, key);
-                k1 = k1 > key ? k1 : key;
+                const float ma = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
+                const float mb = __builtin_fmaf(v[e + 1].x, v[e + 1].x, v[e + 1].y * v[e + 1].y);
+                top2_pair(k1, k2, (__float_as_uint(ma) & ~63u) | (unsigned)e,
+                          (__float_as_uint(mb) & ~63u) | (unsigned)(e + 1));
             }
             unsigned K1, K2;
             wave_top2_merge<LPS>(k1, k2, h, K1, K2);

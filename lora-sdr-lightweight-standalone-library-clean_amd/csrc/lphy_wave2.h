@@ -430,11 +430,11 @@ __global__ __launch_bounds__(512) void k_wave2(FrameArgs P) {
             // keyed top two over the half's bins l + LPS e (see k_wave)
             unsigned k1 = 0u, k2 = 0u;
 #pragma unroll
-            for (int e = 0; e < 64; ++e) {
-                const float m2 = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
-                const unsigned key = (__float_as_uint(m2) & ~63u) | (unsigned)e;
-                k2 = med3_u32(k1, k2, key);
-                k1 = k1 > key ? k1 : key;
+            for (int e = 0; e < 64; e += 2) {
+                const float ma = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
+                const float mb = __builtin_fmaf(v[e + 1].x, v[e + 1].x, v[e + 1].y * v[e + 1].y);
+                top2_pair(k1, k2, (__float_as_uint(ma) & ~63u) | (unsigned)e,
+                          (__float_as_uint(mb) & ~63u) | (unsigned)(e + 1));
             }
             unsigned K1, K2;
             wave_top2_merge<LPS>(k1, k2, h, K1, K2);
@@ -834,11 +834,11 @@ __global__ __launch_bounds__(512) void k_wave2s(FrameArgs P) {
         wpass2<SF, true>(v, T, A.tw, l);
         unsigned k1 = 0u, k2 = 0u;
 #pragma unroll
-        for (int e = 0; e < 64; ++e) {
-            const float m2 = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
-            const unsigned key = (__float_as_uint(m2) & ~63u) | (unsigned)e;
-            k2 = med3_u32(k1, k2, key);
-            k1 = k1 > key ? k1 : key;
+        for (int e = 0; e < 64; e += 2) {
+            const float ma = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
+            const float mb = __builtin_fmaf(v[e + 1].x, v[e + 1].x, v[e + 1].y * v[e + 1].y);
+            top2_pair(k1, k2, (__float_as_uint(ma) & ~63u) | (unsigned)e,
+                      (__float_as_uint(mb) & ~63u) | (unsigned)(e + 1));
         }
         unsigned K1, K2;
         wave_top2_merge<LPS>(k1, k2, h, K1, K2);

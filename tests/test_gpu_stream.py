@@ -125,3 +125,38 @@ def test_stream_argument_errors(lphy):
         with pytest.raises(lphy.LphyError):
             d.demod_stream(fh.fileno(), 66 * 128 + 3, lphy.MODE_DECHIRP_LORA_DEMODULATE, 0,
                            chunk_frames=2, capacity=2)
+
+
+@pytest.mark.parametrize("copy", ["map", "pread"])
+def test_stream_reader_pool_offset_and_resume(oracle, lphy, monkeypatch, copy):
+    """Chunks above the reader pool's threshold (4 MiB): the readers copy
+    out of a mapping of the file (default) or pread it (LPHY_STREAM_COPY).
+    The stream starts at a non-zero file offset, stops at max_frames and a
+    second call resumes from the descriptor's offset; a partial frame
+    trails."""
+    if copy == "pread":
+        monkeypatch.setenv("LPHY_STREAM_COPY", "pread")
+    else:
+        monkeypatch.delenv("LPHY_STREAM_COPY", raising=False)
+    sf, nf, head = 7, 150, 24
+    iq = _frames(oracle, sf, nf, 29)
+    fs = iq.shape[1]
+    mode = lphy.MODE_DECHIRP_LORA_DEMODULATE
+    d = lphy.Demodulator(sf)
+    ref = d.demod_host(iq, nf, fs, mode, lphy.F_DECODE)
+    with tempfile.TemporaryFile() as fh:
+        fh.write(b"\x7f" * head)
+        fh.write(iq.tobytes())
+        fh.write(b"\x02" * 40)
+        fh.flush()
+        fh.seek(head)
+        a = d.demod_stream(fh.fileno(), fs, mode, lphy.F_DECODE, chunk_frames=70,
+                           max_frames=100, capacity=nf)
+        assert a[0].shape[0] == 100 and a[3] == 0
+        assert os.lseek(fh.fileno(), 0, os.SEEK_CUR) == head + 100 * fs * 8
+        b = d.demod_stream(fh.fileno(), fs, mode, lphy.F_DECODE, chunk_frames=70, capacity=nf)
+    assert b[0].shape[0] == nf - 100 and b[3] == 40
+    got = tuple(np.concatenate([x, y]) for x, y in zip(a[:3], b[:3]))
+    _same(got, ref)
+    for f in (0, 99, 100, nf - 1):
+        np.testing.assert_array_equal(got[0][f], _oracle_frame(oracle, lphy, iq[f], sf, mode))
