@@ -117,7 +117,12 @@ __attribute__((target("avx2"))) void copy_nt_avx2(char* dst, const char* src, si
     _mm_sfence();
 }
 void copy_part(char* dst, const char* src, size_t n) {
-    static const bool avx2 = __builtin_cpu_supports("avx2");
+    static const bool avx2 = [] {
+#ifndef __HIP_DEVICE_COMPILE__  // (host code; the device pass only parses it)
+        __builtin_cpu_init();  // a library may run before the CPU model is filled in
+#endif
+        return __builtin_cpu_supports("avx2") != 0;
+    }();
     if (avx2 && (reinterpret_cast<uintptr_t>(dst) & 31) == 0) copy_nt_avx2(dst, src, n);
     else memcpy(dst, src, n);
 }
