@@ -1116,6 +1116,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                 sp_fl = 0u;
                 if (R.ok) wclose<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, f, R.rate, R.scale, R.t_off, R.mx, mm, rr, nan, open, dma_plan(nx));
             }
+            WPH(6);
         } else {
             // estimate unit(s): KISS's arithmetic, bit for bit (LoRaDemod.cpp:80-136,
             // phy.cpp:81-148); SF 12 symbol j, SF 11 symbol h of the pair
@@ -1170,6 +1171,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             WPH(6);
         }
         // the two-symbol scan of the frame whose estimate comes next
+        // (WPH slot 7 from here to the next unit: the scan and the cursor)
         if constexpr (!M0) {
             if (sch.kind(nx) == kWEst && nx.j == 0 && nx.phase == 2) {
                 const unsigned kn = sch.frame(nx);

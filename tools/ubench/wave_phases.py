@@ -1,8 +1,10 @@
-"""k_wave phase clocks (timing aid only): per-wave clock sums of the unit
-phases (DMA wait, staging, pass 1, exchange + DMA issue, pass 2, argmax +
-store, estimate units, other) on the bench workload of one SF.
-Needs a variant built with -DLPHY_PROFILE_PHASES (variants.py build).
-  python tools/ubench/wave_phases.py <sf> <variant> [mode]"""
+"""Per-phase clock shares of the fused SF 9-12 wave kernel (timing aid).
+Build: python tools/ubench/variants.py build <sf> ph<sf>:"-DLPHY_PROFILE_PHASES"
+Run:   python tools/ubench/wave_phases.py <sf>   (GPU box)
+Phases (k_wave, lphy_wave.h WPH): 0 wait for the unit's IQ, 1 staging,
+2 pass 1, 3 exchange + next DMA, 4 pass 2, 5 top two / certificate / stores,
+6 estimate units and frame close, 7 the next frame's two-symbol
+max-abs scan and the schedule cursor."""
 import ctypes as C
 import sys
 from pathlib import Path
@@ -10,26 +12,22 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 import torch  # noqa: E402
+
 import bench  # noqa: E402
 
-sf, name = int(sys.argv[1]), sys.argv[2]
-mode = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 lphy = bench.lphy
-lphy.use(Path(__file__).resolve().parent / f"var_{name}.so")
+sf = int(sys.argv[1]) if len(sys.argv) > 1 else 12
+lphy.use(Path(__file__).resolve().parent / f"var_ph{sf}.so")
 wl = bench.Workload(sf, 125000, bench.DEFAULT_FRAMES[sf], 0, torch.device("cuda:0"))
+mode = lphy.MODE_DECHIRP_LORA_DEMODULATE
 flags = lphy.F_DECODE | lphy.F_STAGE_PROLOGUE | lphy.F_STAGE_SYMBOLS
-ms = wl._event_ms(mode, flags, 10)
 lib = lphy.load()
-out = (C.c_ulonglong * 8)()
 lib.lphy_hip_phase_cycles.argtypes = [C.c_void_p, C.c_void_p]
+out = (C.c_ulonglong * 8)()
+wl._event_ms(mode, flags, 3)
+lib.lphy_hip_phase_cycles(wl.dem.ctx, out)  # clear
+ms = wl._event_ms(mode, flags, 1)
 lib.lphy_hip_phase_cycles(wl.dem.ctx, out)
-wl._event_ms(mode, flags, 1, warmup=0)
-lib.lphy_hip_phase_cycles(wl.dem.ctx, out)
-names = ["dma_wait", "staging", "pass1", "exch+dma", "pass2", "argmax+out", "estimate", "other"]
 tot = sum(out) or 1
-waves = min(256, (wl.frames + 3) // 4) * 4
-units = wl.frames * (66 + 2) / (64 // max((1 << sf) // 64, 1))
-print(f"SF{sf} mode {mode} {name}: {ms:.3f} ms/launch (phase-clock build), per-wave cycles {tot / waves:.0f}, "
-      f"per unit {tot / units:.0f}", flush=True)
-for n, v in zip(names, out):
-    print(f"  {n:11s} {v / tot:6.3f}  {v / units:8.0f} cycles/unit", flush=True)
+names = ["iq_wait", "staging", "pass1", "exchange+dma", "pass2", "top2+cert", "estimate+close", "scan+cursor"]
+print(f"SF{sf} fused {ms:.3f} ms; phase shares: " + ", ".join(f"{n} {out[i] / tot:.3f}" for i, n in enumerate(names)))
