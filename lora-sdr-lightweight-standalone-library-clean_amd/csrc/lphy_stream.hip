@@ -356,44 +356,11 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
     int nreaders = usable_cpus() - 1;
     if (const char* e = getenv("LPHY_STREAM_READERS")) nreaders = atoi(e);
     nreaders = nreaders < 1 ? 1 : (nreaders > 32 ? 32 : nreaders);
-    // LPHY_STREAM_MMAP=1 (experiment, tools/stream_bench.py): a regular file
-    // is mapped and the mapping registered with HIP (pinned in place), so the
-    // copy engine reads the page cache directly - no host copy; falls back
-    // to the readers when mapping or registration fails
-    char* map = nullptr;
-    size_t map_len = 0, map_skip = 0, map_avail = 0;
-    off_t map_base = 0;
-    bool mapped = false;
-    if (seekable && getenv("LPHY_STREAM_MMAP") && getenv("LPHY_STREAM_MMAP")[0] == '1') {
-        struct stat stt;
-        const off_t cur = ::lseek(fd, 0, SEEK_CUR);
-        if (cur >= 0 && fstat(fd, &stt) == 0 && S_ISREG(stt.st_mode) && stt.st_size > cur) {
-            const long pg = sysconf(_SC_PAGESIZE);
-            map_base = cur & ~(off_t)(pg - 1);
-            map_skip = (size_t)(cur - map_base);
-            map_avail = (size_t)(stt.st_size - cur);
-            if (map_avail > max_frames * frame_bytes) map_avail = max_frames * frame_bytes;
-            map_len = map_skip + map_avail;
-            void* m = mmap(nullptr, map_len, PROT_READ, MAP_SHARED, fd, map_base);
-            if (m != MAP_FAILED) {
-                map = static_cast<char*>(m);
-                (void)madvise(map, map_len, MADV_SEQUENTIAL);
-                if (hipHostRegister(map, map_len, hipHostRegisterReadOnly) == hipSuccess) {
-                    mapped = true;
-                } else {
-                    (void)hipGetLastError();
-                    munmap(map, map_len);
-                    map = nullptr;
-                }
-            }
-        }
-    }
-    size_t map_used = 0;
-    ReaderPool pool(!mapped && seekable && chunk_bytes >= kParMin ? nreaders : 0);
+    ReaderPool pool(seekable && chunk_bytes >= kParMin ? nreaders : 0);
     // the readers' source mapping (regular files; LPHY_STREAM_COPY=pread: none)
     char* rmap = nullptr;
     size_t rmap_len = 0;
-    if (!mapped && pool.size() > 0 && !(getenv("LPHY_STREAM_COPY") && strcmp(getenv("LPHY_STREAM_COPY"), "pread") == 0)) {
+    if (pool.size() > 0 && !(getenv("LPHY_STREAM_COPY") && strcmp(getenv("LPHY_STREAM_COPY"), "pread") == 0)) {
         struct stat stt;
         if (fstat(fd, &stt) == 0 && S_ISREG(stt.st_mode) && stt.st_size > 0) {
             rmap_len = (size_t)stt.st_size;
@@ -440,15 +407,7 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
         size_t want = chunk_bytes;
         if (max_frames - next < chunk_frames) want = (max_frames - next) * frame_bytes;
         if (want == 0) break;
-        const char* src = s.pin_iq;
-        long long got;
-        if (mapped) {  // the registered mapping itself is the copy's source
-            got = (long long)(want < map_avail - map_used ? want : map_avail - map_used);
-            src = map + map_skip + map_used;
-            map_used += (size_t)got;
-        } else {
-            got = read_chunk(&pool, fd, seekable, s.pin_iq, want);
-        }
+        const long long got = read_chunk(&pool, fd, seekable, s.pin_iq, want);
         if (got < 0) { rc = -EIO; goto done; }
         const size_t nf = (size_t)got / frame_bytes;
         if ((size_t)got % frame_bytes) {
@@ -457,7 +416,7 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
             if (tail_bytes) *tail_bytes = (size_t)got % frame_bytes;
         }
         if (nf == 0) break;
-        ST_OK(hipMemcpyAsync(s.d_iq, src, nf * frame_bytes, hipMemcpyHostToDevice, copy_st));
+        ST_OK(hipMemcpyAsync(s.d_iq, s.pin_iq, nf * frame_bytes, hipMemcpyHostToDevice, copy_st));
         ST_OK(hipEventRecord(s.h2d, copy_st));
         ST_OK(hipStreamWaitEvent(comp_st, s.h2d, 0));
         ST_OK(hipMemsetAsync(s.d_meta, 0, nf * sizeof(lphy_frame_meta), comp_st));
@@ -488,11 +447,5 @@ done:
     if (sl)
         for (int k = 0; k < NSLOT; ++k) sl[k].busy = false;
     if (rmap) munmap(rmap, rmap_len);
-    if (mapped) {
-        (void)hipHostUnregister(map);
-        munmap(map, map_len);
-        // the fd's offset after the bytes consumed, as the readers leave it
-        (void)::lseek(fd, map_base + (off_t)(map_skip + map_used), SEEK_SET);
-    }
     return rc;
 }
