@@ -206,8 +206,9 @@ int lphy_hip_modulate_host(lphy_hip_ctx* ctx, const uint16_t* h_syms,
  * h_meta + f).  A seekable fd is read by a pool of reader threads
  * (LPHY_STREAM_READERS, default one per usable CPU but one); a regular file
  * is mapped read-only and the readers copy out of the mapping with
- * non-temporal stores (LPHY_STREAM_COPY=pread: pread instead; as with any
- * mapping, truncating the file during the call raises SIGBUS); the pinned
+ * non-temporal stores (LPHY_STREAM_COPY=pread: pread instead; the file
+ * size is re-read before each chunk, but as with any mapping, a truncation
+ * racing a chunk's copy can raise SIGBUS); the pinned
  * slots and streams stay with the context for its next call.
  * `max_frames` is their capacity in frames and is required
  * (0 gives -EINVAL): reading stops there and the rest of the stream is left

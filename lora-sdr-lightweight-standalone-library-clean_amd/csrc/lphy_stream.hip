@@ -407,6 +407,10 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
         size_t want = chunk_bytes;
         if (max_frames - next < chunk_frames) want = (max_frames - next) * frame_bytes;
         if (want == 0) break;
+        if (rmap) {  // a file shortened since the call began: its lost tail is pread (short), not copied
+            struct stat stt;
+            if (fstat(fd, &stt) == 0 && (size_t)stt.st_size < rmap_len) pool.set_map(rmap, 0, (size_t)stt.st_size);
+        }
         const long long got = read_chunk(&pool, fd, seekable, s.pin_iq, want);
         if (got < 0) { rc = -EIO; goto done; }
         const size_t nf = (size_t)got / frame_bytes;
