@@ -1946,7 +1946,87 @@ __device__ __forceinline__ void finalize_frame(const FinalArgs& A, unsigned long
     A.meta[f] = m;
 }
 
-__global__ void k_finalize(FinalArgs A) {
+// A workgroup's 256 rows at once (the register form's rows: 8 to 64
+// symbols, a multiple of 8, 16-byte aligned): the symbols come in and the
+// bytes go out as whole contiguous rows across the workgroup, staged in LDS,
+// instead of each thread's 128-byte row at a 128-byte lane stride; each
+// thread then decodes its frame as finalize_frame_regs does (same bytes,
+// same checksum steps).  Rows of a non-zero status are left as they are.
+struct FinStage {
+    uint4 in[kTile * 9];      // 9 x 16 B per row (8 used): conflict-free 16-byte reads
+    unsigned out[kTile * 9];  // the decoded words
+    unsigned char ok[kTile];  // the row was decoded
+};
+__device__ __forceinline__ bool finalize_block(const FinalArgs& A, unsigned long long f0, FinStage& st) {
+    const unsigned long long nb = A.nsyms / 2;
+    if (!A.decode || (A.nsyms & 1) || nb < 4 || nb > 32 || (nb & 3) || (A.sym_stride & 7) ||
+        (reinterpret_cast<uintptr_t>(A.syms) & 15) || (reinterpret_cast<uintptr_t>(A.bytes) & 3) ||
+        f0 >= A.frames)
+        return false;  // (uniform over the workgroup)
+    const unsigned nw = (unsigned)(nb / 4);
+    const unsigned nf = A.frames - f0 < (unsigned long long)kTile ? (unsigned)(A.frames - f0) : (unsigned)kTile;
+    const unsigned t = threadIdx.x;
+    for (unsigned i = t; i < nf * nw; i += kTile) {
+        const unsigned fr = i / nw, k = i - fr * nw;
+        st.in[fr * 9 + k] = reinterpret_cast<const uint4*>(A.syms + (f0 + fr) * A.sym_stride)[k];
+    }
+    __syncthreads();
+    if (t < nf) {
+        const unsigned long long f = f0 + t;
+        lphy_frame_meta m = A.meta[f];
+        const bool ok = m.status == 0;
+        st.ok[t] = ok ? 1 : 0;
+        if (ok) {
+            if (A.set_sync && m.have_sync)
+                m.sync_word = (uint8_t)((((m.sw0 >> A.shift) & 0x0f) << 4) | ((m.sw1 >> A.shift) & 0x0f));
+            unsigned wd[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                wd[j] = 0u;
+                if ((unsigned)j < nw) {
+                    const uint4 q = st.in[t * 9 + j];
+                    const unsigned qs[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const unsigned hi = hamming84_decode((uint8_t)qs[b]) & 0x0fu;
+                        const unsigned lo = hamming84_decode((uint8_t)(qs[b] >> 16)) & 0x0fu;
+                        wd[j] |= ((hi << 4) | lo) << (8 * b);
+                    }
+                    st.out[t * 9 + j] = wd[j];
+                }
+            }
+            // phy.cpp:252-259, over bytes 2 .. nb-3 (finalize_frame_regs)
+            const int len = (int)nb - 4;
+            unsigned res = 0, v = 0xff;
+#pragma unroll
+            for (int i = 0; i < 28; ++i) {
+                if (i >= len) break;  // uniform
+                const unsigned byte = (wd[(i + 2) >> 2] >> (8 * ((i + 2) & 3))) & 0xffu;
+                const unsigned crc = sx_shift8(res);
+                v = sx_lfsr(v);
+                res = crc ^ byte;
+            }
+            res ^= v;
+            v = sx_lfsr(v);
+            res ^= v << 8;
+            const unsigned pw = st.out[t * 9 + (unsigned)((nb - 2) >> 2)] >> (8 * ((nb - 2) & 3));
+            m.crc_ok = (uint16_t)(pw & 0xffffu) == (uint16_t)res;
+            A.meta[f] = m;
+        }
+    }
+    __syncthreads();
+    for (unsigned i = t; i < nf * nw; i += kTile) {
+        const unsigned fr = i / nw, k = i - fr * nw;
+        if (st.ok[fr]) reinterpret_cast<unsigned*>(A.bytes + (f0 + fr) * nb)[k] = st.out[fr * 9 + k];
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(kTile) void k_finalize(FinalArgs A) {
+    __shared__ FinStage st;
+#ifndef LPHY_AB_FINAL_THREAD  // A/B timing only: a row per thread straight from memory
+    if (blockDim.x == kTile && finalize_block(A, (unsigned long long)blockIdx.x * kTile, st)) return;
+#endif
     const unsigned long long f = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (f < A.frames) finalize_frame(A, f);
 }
@@ -2325,9 +2405,15 @@ __global__ __launch_bounds__(kTile) void k_spec_settle(DemodArgs A) {
 // After the symbol kernels: the exact re-run of the frames they flagged
 // (kStatusFixup: whole frame; kStatusRecheck: the open symbols), then (fin)
 // the per-frame finalisation, one thread per frame.
+template <int SF>
+union PostLds {  // the exact re-runs' workspace, then the finalisation's staging
+    PostShared<SF> sh;
+    FinStage fs;
+};
 template <int SF, int MODE>
 __global__ __launch_bounds__(kTile) void k_post(DemodArgs A, FinalArgs F, int fix, int fin) {
-    __shared__ PostShared<SF> sh;
+    __shared__ PostLds<SF> L;
+    PostShared<SF>& sh = L.sh;
     __shared__ unsigned flist[kTile];
     __shared__ unsigned fcount;
     const unsigned long long f = (unsigned long long)blockIdx.x * kTile + threadIdx.x;
@@ -2355,7 +2441,12 @@ __global__ __launch_bounds__(kTile) void k_post(DemodArgs A, FinalArgs F, int fi
             if (recheck) A.meta[f].status = 0;
         }
     }
-    if (fin && f < A.frames) finalize_frame(F, f);
+    if (!fin) return;
+#ifndef LPHY_AB_FINAL_THREAD  // A/B timing only: a row per thread straight from memory
+    if (fix) __syncthreads();  // the re-runs are done with the shared workspace
+    if (finalize_block(F, (unsigned long long)blockIdx.x * kTile, L.fs)) return;
+#endif
+    if (f < A.frames) finalize_frame(F, f);
 }
 
 #include "lphy_wave.h"
