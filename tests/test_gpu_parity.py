@@ -318,3 +318,38 @@ def test_separate_launch_rechecks_stable(oracle, lphy, sf, mode):
         else:
             r, osyms, osync, omet = oracle.lora_demodulate(iq[f], sf)
         np.testing.assert_array_equal(runs[0][0][f], osyms, err_msg=f"frame {f}")
+
+
+@pytest.mark.parametrize("per,nf", [(64, 300), (60, 300), (8, 513), (6, 5)])
+def test_decode_batch_rows_vs_oracle(oracle, lphy, per, nf):
+    """lphy_hip_decode_batch (k_finalize) over whole workgroups of rows:
+    rows of 8k symbols go through the LDS-staged block form (a partial last
+    workgroup included), others through the row-per-thread form; rows whose
+    record carries a non-zero status are left untouched (bytes and record),
+    as the per-row form leaves them.  Every decoded row and CRC flag against
+    the oracle (LoRaDecoder.cpp:7-21, LoRaCodes.hpp:69-105, 250-281)."""
+    import torch
+    rng = np.random.default_rng(per * 1000 + nf)
+    d = lphy.Demodulator(7)
+    dev = torch.device("cuda:0")
+    syms = rng.integers(0, 1 << 16, (nf, per), dtype=np.uint16)
+    syms[::7, :] = rng.integers(0, 256, (len(syms[::7]), per), dtype=np.uint16)  # clean low bytes too
+    meta = np.zeros(nf, lphy.META_DTYPE)
+    skip = rng.random(nf) < 0.1
+    meta["status"][skip] = -34
+    meta["crc_ok"] = 7
+    t_syms = torch.from_numpy(syms.view(np.int16).reshape(-1).copy()).to(dev)
+    t_pay = torch.full((nf * (per // 2),), 0xAB, dtype=torch.uint8, device=dev)
+    t_meta = torch.from_numpy(meta.view(np.uint8).reshape(-1).copy()).to(dev)
+    d.decode_batch(t_syms, nf, per, t_pay, t_meta, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    pay = t_pay.cpu().numpy().reshape(nf, per // 2)
+    out = t_meta.cpu().numpy().view(lphy.META_DTYPE)
+    for f in range(nf):
+        if skip[f]:
+            assert (pay[f] == 0xAB).all() and out["crc_ok"][f] == 7 and out["status"][f] == -34
+            continue
+        r, obytes, ocrc = oracle.decode(syms[f])
+        assert r == per // 2
+        np.testing.assert_array_equal(pay[f], obytes)
+        assert out["crc_ok"][f] == ocrc and out["status"][f] == 0
