@@ -426,38 +426,30 @@ def write_perf_csv(path: str, run_id: str, rows: list) -> None:
 
 
 def frames_fused(sf: int) -> bool:
-    """Whether the bench frame shape takes a fused launch (every SF unless
-    LPHY_FUSED=0: k_frames up to SF 8, k_wave2s at SF 9, k_wave at 10-12;
-    lphy_hip.hip frames_fit / wave_fit)."""
-    return os.environ.get("LPHY_FUSED", "1") != "0"
+    """Whether the bench frame shape takes a fused launch: every SF (k_frames
+    up to SF 8, k_wave2s at SF 9, k_wave at 10-12; lphy_hip.hip frames_fit /
+    wave_fit: the bench's batches are far above the fused crossover)."""
+    return True
 
 
 def fused_kernel(sf: int) -> str:
     """Name of the fused launch's kernel, as the PMC summaries key it, by the
-    library's own rule (lphy_hip.hip wave_fit, lphy_kernels.h
-    wave_kind): k_frames below LPHY_WAVE_MIN_SF (default 9); above it
-    k_wave2s at SF 9 and k_wave at SF 10-12, or the kernel LPHY_WAVE=1 | 2 |
-    2s names."""
-    lo = int(os.environ.get("LPHY_WAVE_MIN_SF", "9"))
-    lo = lo if 9 <= lo <= 13 else 9
-    if sf < lo or sf > 12:
+    library's own rule for the bench's frames (66 symbols, osr 1, no window;
+    lphy_hip.hip wave_fit, lphy_kernels.h use_wave2s)."""
+    if sf <= 8:
         return f"k_frames<{sf}>"
-    w = os.environ.get("LPHY_WAVE", "")
-    if w == "2s" and sf <= 10:
-        return f"k_wave2s<{sf}>"
-    if w == "2":
-        return f"k_wave2<{sf}>"
-    if w == "1" or sf >= 10:
-        return f"k_wave<{sf}>"
-    return f"k_wave2s<{sf}>"
+    return f"k_wave2s<{sf}>" if sf == 9 else f"k_wave<{sf}>"
 
 
 def measured_traffic(kernel: str, frames: int):
     """HBM bytes per launch of `kernel` from the committed PMC summary
     (profiles/pmc_*.json written by tools/pmc_summary.py from rocprofv3 --pmc
     passes of this bench's configuration; FETCH_SIZE x2 on gfx950 +
-    WRITE_SIZE, per the MI355X guide), or None when no summary matches."""
-    best = None
+    WRITE_SIZE, per the MI355X guide), or None when no summary matches.  Of
+    several summaries of the same kernel and configuration the newest wins:
+    by the "written" stamp pmc_summary.py records (summaries from before it
+    had one rank below every stamped one, then by name)."""
+    best, best_key = None, None
     for f in sorted((ROOT / "profiles").glob("pmc_*.json")):
         try:
             d = json.loads(f.read_text())
@@ -466,7 +458,11 @@ def measured_traffic(kernel: str, frames: int):
         k = d.get("kernels", {}).get(kernel)
         # the bench's mode (2) only; summaries without the HBM passes skipped
         if k and "hbm_bytes_per_launch" in k and d.get("frames") == frames and d.get("mode", 2) == 2:
-            best = {"bytes": k["hbm_bytes_per_launch"], "source": f"{f.name}"}
+            key = (d.get("written", ""), f.name)
+            if best_key is None or key > best_key:
+                best_key = key
+                best = {"bytes": k["hbm_bytes_per_launch"], "source": f"{f.name}",
+                        "written": d.get("written")}
     return best
 
 
@@ -506,9 +502,7 @@ def run_c3(args, baseline, world, rank, dev) -> dict:
     if world > 1:
         # one slab per rank holds all its buckets; every rank's layout is
         # known from the seeded plan, so the slabs are padded to the largest
-        plans = [shard.mixed_plan(total, world, r, payload=PAYLOAD)[4] for r in range(world)]
-        cap = max(shard.slab_layout([p[sf].size for sf in sorted(p)], DATA_SYMS, PAYLOAD)[1]
-                  for p in plans)
+        cap = shard.mixed_slab_bytes(total, world, DATA_SYMS, PAYLOAD)
         slabs = [shard.ResultSlab([plan[sf].size for sf in order], DATA_SYMS, PAYLOAD, dev, cap)
                  for _ in range(2)]
     buckets = [Workload(sf, args.bw, int(plan[sf].size), rank, dev, payloads=payloads[plan[sf]],
@@ -538,14 +532,11 @@ def run_c3(args, baseline, world, rank, dev) -> dict:
         if rank == 0:
             # the whole stream, every rank's buckets put back in frame order
             allp = shard.mixed_plan(total, 1, 0, payload=PAYLOAD)[3]
-            got = []
-            for r in range(world):
-                f_r, c_r, _, _, p_r = shard.mixed_plan(total, world, r, payload=PAYLOAD)
-                srt = sorted(p_r)
-                unp = shard.unpack_slab(parts[r], [p_r[sf].size for sf in srt], DATA_SYMS, PAYLOAD)
-                got.append(shard.reassemble(p_r, {sf: u[1] for sf, u in zip(srt, unp)}, c_r, PAYLOAD))
-            got = np.concatenate(got)
-            gathered = {"frames": int(total), "stream_in_order": bool(np.array_equal(got, allp))}
+            gs, got, gm = shard.gather_mixed(parts, total, world, DATA_SYMS, PAYLOAD)
+            m = gm.reshape(-1).view(lphy.META_DTYPE)
+            gathered = {"frames": int(total), "stream_in_order": bool(np.array_equal(got, allp)),
+                        "symbols_exact": bool(np.array_equal(gs, lphy.encode_payloads(allp))),
+                        "records_ok": int(((m["status"] == 0) & (m["sync_word"] == 0x12)).sum())}
         for wl in buckets:
             wl.run(mode_b)  # slot 0 again for the local checks below
     ok = sum(w.check(mode_b)["payloads_recovered"] for w in buckets)
@@ -647,15 +638,40 @@ def rank_env(rank: int, world: int, port: int) -> dict:
             "MASTER_PORT": str(port)}
 
 
+def node_gpu_count(sysfs: str = "/sys/class/kfd/kfd/topology/nodes", env=None) -> int:
+    """GPUs on this node without touching HIP: the KFD topology nodes with
+    SIMDs (CPU nodes have simd_count 0), capped by the visible-device list
+    (HIP_VISIBLE_DEVICES, ROCR_VISIBLE_DEVICES or CUDA_VISIBLE_DEVICES, as
+    the runtime honours them).  0 when the topology is unreadable."""
+    env = os.environ if env is None else env
+    n = 0
+    try:
+        for node in sorted(Path(sysfs).iterdir()):
+            props = {}
+            for line in (node / "properties").read_text().splitlines():
+                parts = line.split()
+                if len(parts) == 2:
+                    props[parts[0]] = parts[1]
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except (OSError, ValueError):
+        return 0
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def launch_ranks(cmd: list, world: int, devices: int | None = None) -> int:
     """Run `cmd` as `world` ranks, one child process per GPU, and return
-    the first failing rank's exit code (0 when all succeed).  Called before
-    anything touches the GPU (torch.cuda.device_count() does not initialise
-    it on ROCm); refuses when the node has fewer devices than ranks.  A
+    the first failing rank's exit code (0 when all succeed).  The parent
+    never touches HIP: it counts the node's GPUs from the KFD topology in
+    sysfs (node_gpu_count) and refuses when there are fewer than ranks.  A
     rank that fails ends the others (their own PIDs)."""
     import subprocess
     if devices is None:
-        devices = world if REHEARSE else torch.cuda.device_count()
+        devices = world if REHEARSE else node_gpu_count()
     if devices < world:
         print(f"bench.py: --gpus {world} needs {world} GPUs, this node has {devices}", file=sys.stderr)
         return 3

@@ -87,7 +87,7 @@ enum lphy_flags {
                                     instead of the fused single launch
                                     (same results; the shapes the fused
                                     kernels do not take run them anyway) */
-    /* Bits 64..512 are comparison / test paths of the test-only build
+    /* Bits 64..1024 are comparison / test paths of the test-only build
      * (lib/test/, csrc/lphy_testing.h); this library rejects them with
      * -EINVAL. */
 };
@@ -118,6 +118,14 @@ int lphy_hip_ctx_share(lphy_hip_ctx** out, const lphy_hip_ctx* base, unsigned os
  * A larger call later grows the staging once.  Returns 0 or -ENOMEM/-EIO. */
 int lphy_hip_ctx_reserve(lphy_hip_ctx* ctx, size_t frames, size_t frame_samples);
 
+/* Smallest batch (frames per lphy_hip_demod_batch call) that takes the
+ * fused single-launch kernels on this context; smaller batches take the
+ * separate symbol-parallel launches, which finish a few frames sooner.
+ * `frames` < 0 restores the measured per-SF crossover (the default); 0 sends
+ * every batch whose shape fits to the fused kernels (throughput callers, the
+ * test suite).  Results are identical either way.  Returns 0 or -EINVAL. */
+int lphy_hip_ctx_set_fused_min_frames(lphy_hip_ctx* ctx, long frames);
+
 /* Symbols written per frame for a frame of `frame_samples` samples. */
 size_t lphy_hip_syms_per_frame(const lphy_hip_ctx* ctx, size_t frame_samples,
                                int mode);
@@ -134,8 +142,10 @@ size_t lphy_hip_syms_per_frame(const lphy_hip_ctx* ctx, size_t frame_samples,
  * SF 9-10; k_wave2s at SF 9 and k_wave at SF 10-12 for osr 1, no window,
  * modes 1/2 with the speculative normalisation or mode 0) for batches of at
  * least a per-SF crossover (256 frames at SF <= 7 ... 384 at SF 10-12,
- * DESIGN.md 4.7; LPHY_FUSED_MIN_FRAMES overrides), the separate
- * symbol-parallel launches below it (a packet at a time).
+ * DESIGN.md 4.7; lphy_hip_ctx_set_fused_min_frames overrides it per
+ * context), the separate symbol-parallel launches below it (a packet at a
+ * time).  The choice depends on the arguments and that setting only (no
+ * environment variables).
  * Memory: the fused launches allocate nothing.  The SF 11-12 separate launches
  * (LPHY_F_UNFUSED, small batches, osr > 1, a window) take per-call speculation records
  * (16 B per frame) from the stream-ordered pool on `stream`, released in
@@ -209,7 +219,9 @@ int lphy_hip_modulate_host(lphy_hip_ctx* ctx, const uint16_t* h_syms,
  * non-temporal stores (LPHY_STREAM_COPY=pread: pread instead; the file
  * size is re-read before each chunk, but as with any mapping, a truncation
  * racing a chunk's copy can raise SIGBUS); the pinned
- * slots and streams stay with the context for its next call.
+ * slots and streams stay with the context for its next call, and calls on
+ * one context are serialised (a second thread's call waits for the first);
+ * use one context per thread (lphy_hip_ctx_share) for concurrent streams.
  * `max_frames` is their capacity in frames and is required
  * (0 gives -EINVAL): reading stops there and the rest of the stream is left
  * unread on `fd` for a later call.  Synchronous.

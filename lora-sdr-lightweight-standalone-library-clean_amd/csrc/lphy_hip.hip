@@ -27,6 +27,7 @@
 
 #include <cstring>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -95,6 +96,9 @@ struct lphy_hip_ctx {
     // made by its first call, kept for the next ones, freed with the context
     void* stream_ext = nullptr;
     void (*stream_ext_free)(void*) = nullptr;
+    // smallest batch the fused kernels take on this context (-1: the measured
+    // per-SF crossover, fused_min_frames; lphy_hip_ctx_set_fused_min_frames)
+    std::atomic<long> fused_min{-1};
     // (per-call scratch of the device entry points - the SF 11-12 speculation
     // records, the producer's phases, the compensation's shift buffer - comes
     // from the stream-ordered allocator on the caller's stream, so concurrent
@@ -158,26 +162,15 @@ inline bool frames_fit(unsigned sf, unsigned osr, int est_units, size_t total) {
     return total + 1 >= 2 * wt;
 }
 
-// Whether the fused SF 9-12 kernels (k_wave2 / k_wave2s, 64 x 64 values per
+// Whether the fused SF 9-12 kernels (k_wave / k_wave2s, 64 x 64 values per
 // wavefront unit) take this batch: osr 1, the two-symbol estimate, no
 // window, the certified rotation, and in modes 1/2 the speculative
 // normalisation.  Hann windows, LPHY_F_EXACT_ROTATION and the pre-scan
 // schedule stay on k_frames (SF 9-10) or the separate launches (SF 11-12).
-// wave_min_sf: the lowest SF they take, k_frames below it;
-// LPHY_WAVE_MIN_SF (9..13) moves the boundary for A/B timing.
-unsigned wave_min_sf() {
-    static const unsigned v = [] {
-        const char* e = getenv("LPHY_WAVE_MIN_SF");
-        const int x = e ? atoi(e) : 0;
-        return (x >= 9 && x <= 13) ? (unsigned)x : 9u;
-    }();
-    return v;
-}
-
 inline bool wave_fit(unsigned sf, unsigned osr, int window, int est_units, size_t total, int mode,
                      const DemodArgs& A) {
-    return sf >= wave_min_sf() && sf <= 12 && osr == 1 && window == LPHY_WINDOW_NONE && est_units == 2 &&
-           total >= 2 && !A.exact_rotation && (mode == LPHY_MODE_DEMODULATE || A.spec);
+    return sf >= 9 && sf <= 12 && osr == 1 && window == LPHY_WINDOW_NONE && est_units == 2 && total >= 2 &&
+           !A.exact_rotation && (mode == LPHY_MODE_DEMODULATE || A.spec);
 }
 
 const SfOps* sf_ops(unsigned sf) {
@@ -209,25 +202,16 @@ int launch_post(unsigned sf, int mode, const DemodArgs& A, const FinalArgs& F, b
 // of the GPU idle and the separate launches (symbol-parallel k_demod) finish
 // first.  Crossovers measured per SF, mode 2 with decode, device time per
 // call (tools/fused_crossover.py, profiles/r4/fused_crossover.json); the
-// per-packet latency of the lora_phy:: API rides on the small end.
-// LPHY_FUSED_MIN_FRAMES overrides (0: always fused when the shape fits).
-size_t fused_min_frames(unsigned sf) {
-    static const long env = [] {
-        const char* e = getenv("LPHY_FUSED_MIN_FRAMES");
-        return e ? atol(e) : -1L;
-    }();
-    if (env >= 0) return (size_t)env;
+// per-packet latency of the lora_phy:: API rides on the small end.  A
+// context's own setting (lphy_hip_ctx_set_fused_min_frames) wins; the test
+// build also reads a process default from LPHY_FUSED_MIN_FRAMES.
+size_t fused_min_frames(const lphy_hip_ctx* c) {
+    const long own = c->fused_min.load(std::memory_order_relaxed);
+    if (own >= 0) return (size_t)own;
+    const long test = lphy_test_fused_min_frames();
+    if (test >= 0) return (size_t)test;
     static const size_t t[13] = {256, 256, 256, 256, 256, 256, 256, 256, 1536, 768, 384, 384, 384};
-    return t[sf <= 12 ? sf : 12];
-}
-
-bool fused_enabled() {
-    static int env = -1;
-    if (env < 0) {
-        const char* e = getenv("LPHY_FUSED");
-        env = (e && e[0] == '0') ? 0 : 1;
-    }
-    return env == 1;
+    return t[c->sf <= 12 ? c->sf : 12];
 }
 
 constexpr size_t kPinnedMax = size_t(32) << 20;
@@ -437,6 +421,12 @@ void lphy_hip_ctx_destroy(lphy_hip_ctx* c) {
     delete c;
 }
 
+int lphy_hip_ctx_set_fused_min_frames(lphy_hip_ctx* c, long frames) {
+    if (!c) return -EINVAL;
+    c->fused_min.store(frames < 0 ? -1L : frames, std::memory_order_relaxed);
+    return 0;
+}
+
 size_t lphy_hip_syms_per_frame(const lphy_hip_ctx* c, size_t frame_samples, int mode) {
     if (!c) return 0;
     const size_t total = frame_samples / ((size_t)c->N * c->osr);
@@ -498,6 +488,7 @@ int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t f
     A.counters = c->d_counters;
     A.spec = (mode != LPHY_MODE_DEMODULATE && !A.no_scratch && !(flags & LPHY_F_SCAN_FIRST)) ? 1 : 0;
     A.debug_recheck = (flags & LPHY_F_DEBUG_RECHECK) ? 1 : 0;
+    A.lock_fail = (flags & LPHY_F_DEBUG_LOCKFAIL) ? 1 : 0;
     const size_t est_syms = mode == LPHY_MODE_DEMODULATE ? 2 : (total < 2 ? total : 2);
     A.est_units = (int)(est_syms * c->osr);
     // 32-bit symbol / sample bookkeeping in the kernels
@@ -513,8 +504,8 @@ int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t f
     // two streams, prologue of chunk c+1 beside the symbol kernel of chunk
     // c: the co-running kernels slowed each other ~2x, 1.1x slower overall.)
     const bool wfit = wave_fit(c->sf, c->osr, c->window, A.est_units, total, mode, A);
-    const bool fused = (all || (stages & both) == both) && !(flags & LPHY_F_UNFUSED) && fused_enabled() &&
-                       frames >= fused_min_frames(c->sf) && (frames_fit(c->sf, c->osr, A.est_units, total) || wfit);
+    const bool fused = (all || (stages & both) == both) && !(flags & LPHY_F_UNFUSED) &&
+                       frames >= fused_min_frames(c) && (frames_fit(c->sf, c->osr, A.est_units, total) || wfit);
     A.wave = fused && (c->sf >= 11 || wfit) ? 1 : 0;
     // SF 11-12 separate launches, modes 1/2: the speculative normalisation
     // of k_frames across workgroups (k_maxabs scans the two estimate

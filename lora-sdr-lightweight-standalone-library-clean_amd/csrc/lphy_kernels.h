@@ -41,6 +41,7 @@
 
 #include "../../include/lphy_hip.h"
 #include "libm_exact.h"
+#include "lphy_testing.h"
 #include "lphy_fft.h"
 
 
@@ -76,7 +77,9 @@ struct DemodArgs {
     // atomic max / min), flags (1 NaN, 2 symbol left open)}; nullptr = off
     uint4* spec_big;
     int debug_recheck;       // LPHY_F_DEBUG_RECHECK: mark estimated frames kStatusRecheck before k_demod
-    int wave;                // the fused SF 9-12 launch (k_wave2 / k_wave2s) ran (it settles its frames itself)
+    int wave;                // the fused SF 9-12 launch (k_wave / k_wave2s) ran (it settles its frames itself)
+    int lock_fail;           // LPHY_F_DEBUG_LOCKFAIL (test build): k_wave2s's exchange-buffer locks fail
+                             // deterministically, so the fail-safe path (exact re-run) is exercised
     // persistent demod workers: symbol stride per step split into whole
     // frames + symbols (host-computed, so the kernel never divides)
     unsigned stride_f, stride_s;
@@ -2857,48 +2860,40 @@ int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symb
 // Fused wave-per-symbol path, SF 9-12: which kernel.
 //   k_wave   (lphy_wave.h): one wave per SIMD, 256-thread workgroups, the
 //            next symbols staged through LDS by DMA while a symbol computes;
-//   k_wave2  (lphy_wave2.h): two waves per SIMD, IQ loaded straight into
-//            registers, LDS exchange buffers shared under locks;
-//   k_wave2s (lphy_wave2.h, SF 9-10): k_wave2 with units spanning frames.
-// Defaults follow the round-4 measurements: k_wave2s at SF 9,
-// k_wave at SF 10-12.  LPHY_WAVE=1 | 2 | 2s picks one (A/B; 2s only at
-// SF 9-10).
-enum class WaveKind { V1, V2, V2S };
-
+//   k_wave2s (lphy_wave2.h, SF 9-10): two waves per SIMD, IQ loaded straight
+//            into registers, LDS exchange buffers shared under locks, units
+//            spanning frames (frames of at least SPW symbols).
+// By the round-4 measurements: k_wave2s at SF 9, k_wave at
+// SF 10-12 and for frames shorter than a unit.  The test build takes
+// LPHY_WAVE=1 | 2s to force one for comparisons (lphy_testing.h).
 template <int SF>
-WaveKind wave_kind() {
-    static int env = -2;
-    if (env == -2) {
-        const char* e = getenv("LPHY_WAVE");
-        env = !e ? -1 : (e[0] == '1' ? 0 : (e[0] == '2' && e[1] == 's' ? 2 : (e[0] == '2' ? 1 : -1)));
+bool use_wave2s(const DemodArgs& A) {
+    if constexpr (WGeo<SF>::SPW < 4) {
+        (void)A;
+        return false;
+    } else {
+        if (A.total_syms < (unsigned long long)WGeo<SF>::SPW) return false;  // k_wave2s's precondition
+        const int forced = lphy_test_wave_kind();  // -1 in the product build
+        if (forced >= 0) return forced == 2;
+        return SF == 9;
     }
-    if (env == 0) return WaveKind::V1;
-    if (env == 1) return WaveKind::V2;
-    if (env == 2 && WGeo<SF>::SPW >= 4) return WaveKind::V2S;
-    return SF == 9 ? WaveKind::V2S : WaveKind::V1;
 }
 
 template <int SF, int MODE>
 int launch_wave_mode(const DemodArgs& A, hipStream_t st) {
     FrameArgs P{};
     P.A = A;
-    const WaveKind kind = wave_kind<SF>();
-    if (kind != WaveKind::V1) {
-        constexpr unsigned WPB = W2Lds<SF, MODE>::WPB;
-        unsigned long long blocks = (unsigned long long)cu_count();
-        const unsigned long long need = (A.frames + WPB - 1) / WPB;
-        if (blocks > need) blocks = need;
-        P.waves = (unsigned)(blocks * WPB);
-        if constexpr (WGeo<SF>::SPW >= 4) {
-            if (kind == WaveKind::V2S) {
-                hipLaunchKernelGGL((k_wave2s<SF, MODE>), dim3((unsigned)blocks), dim3(64 * WPB), 0, st, P);
-                HIP_OK(hipGetLastError());
-                return 0;
-            }
+    if constexpr (WGeo<SF>::SPW >= 4) {
+        if (use_wave2s<SF>(A)) {
+            constexpr unsigned WPB = W2Lds<SF, MODE>::WPB;
+            unsigned long long blocks = (unsigned long long)cu_count();
+            const unsigned long long need = (A.frames + WPB - 1) / WPB;
+            if (blocks > need) blocks = need;
+            P.waves = (unsigned)(blocks * WPB);
+            hipLaunchKernelGGL((k_wave2s<SF, MODE>), dim3((unsigned)blocks), dim3(64 * WPB), 0, st, P);
+            HIP_OK(hipGetLastError());
+            return 0;
         }
-        hipLaunchKernelGGL((k_wave2<SF, MODE>), dim3((unsigned)blocks), dim3(64 * WPB), 0, st, P);
-        HIP_OK(hipGetLastError());
-        return 0;
     }
     unsigned long long blocks = (unsigned long long)cu_count();
     const unsigned long long need = (A.frames + WGeo<SF>::WPB - 1) / WGeo<SF>::WPB;

@@ -266,6 +266,10 @@ struct Slot {
 // context (lphy_hip_ctx_stream_ext) so that repeated calls allocate nothing;
 // regrown when a call needs larger chunks.
 struct StreamState {
+    // held for a whole lphy_hip_demod_stream call: the slots, buffers and
+    // streams below are the call's own while it runs (a second thread's call
+    // on the same context waits; ensure() never releases buffers in use)
+    std::mutex mu;
     Slot sl[NSLOT];
     hipStream_t copy_st = nullptr, comp_st = nullptr;
     size_t chunk_bytes = 0, sym_cap = 0, byte_cap = 0, meta_cap = 0;
@@ -373,6 +377,7 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
         }
     }
     StreamState* S = nullptr;
+    std::unique_lock<std::mutex> call_lock;  // S->mu, from S's lookup to the return
     Slot* sl = nullptr;
     hipStream_t copy_st = nullptr, comp_st = nullptr;
 
@@ -394,6 +399,7 @@ extern "C" int lphy_hip_demod_stream(lphy_hip_ctx* ctx, int fd, size_t frame_sam
         rc = -ENOMEM;
         goto done;
     }
+    call_lock = std::unique_lock<std::mutex>(S->mu);
     if ((rc = S->ensure(chunk_bytes, (per ? per : 1) * chunk_frames, (per / 2 ? per / 2 : 1) * chunk_frames,
                         chunk_frames)) != 0)
         goto done;

@@ -1,14 +1,11 @@
-// lphy_wave2.h — the SF 9-12 fused launch at two waves per SIMD (k_wave2).
-// Included by lphy_kernels.h after lphy_wave.h, whose unit geometry (WGeo:
-// one wavefront per unit of 64 x 64 complex values), transform passes,
-// exchange, keyed top two, estimate fold and schedule (WSched) it reuses.
+// lphy_wave2.h — the SF 9-10 fused launch at two waves per SIMD with units
+// spanning frames (k_wave2s).  Included by lphy_kernels.h after lphy_wave.h,
+// whose unit geometry (WGeo: one wavefront per unit of 64 x 64 complex
+// values), transform passes, exchange, keyed top two and estimate fold it
+// reuses.
 //
-// k_wave (one 256-thread workgroup per CU, one wave per SIMD) kept each
-// unit's IQ in a per-wave 32 KiB LDS buffer filled by LDS-DMA, so the next
-// unit's copy could only start once the current unit's exchange had read
-// the buffer, and with one wave per SIMD nothing covered the waits or the
-// packed-f32 dependency pads (VALU issue 61 % of the wave's
-// cycles, waits 20 %).  Here:
+// k_wave (one 256-thread workgroup per CU, one wave per SIMD) keeps each
+// unit's IQ in a per-wave 32 KiB LDS buffer filled by LDS-DMA.  Here:
 //   * 512-thread workgroups, 8 independent waves per CU (2 per SIMD, at most
 //     256 VGPR + AGPR each): one wave's loads and LDS waits run under its
 //     partner's arithmetic;
@@ -16,14 +13,12 @@
 //     (64 coalesced 8-byte loads per lane: lane (h, l) reads samples
 //     l + LPS m of its symbol's window), no LDS staging copy;
 //   * the 64 x LPS exchange between the passes borrows one of NBUF shared
-//     LDS buffers (3 or 4 per CU, an LDS compare-and-swap lock each) for the
-//     ~130 LDS operations it takes, so 8 waves fit beside the down-chirp;
+//     LDS buffers (4 per CU, an LDS compare-and-swap lock each) for the ~130
+//     LDS operations it takes, so 8 waves fit beside the down-chirp;
 //   * the estimate units fold the two estimate symbols' max-abs from their
-//     own registers (SF 9-11: both symbols are in one unit; SF 12: the first
-//     estimate unit scans symbol 1 before it scales symbol 0), with no
-//     separate two-symbol scan, and units load no window for symbols a frame
-//     does not have (the last unit of a frame at SF 9-10, the estimate
-//     unit's spare halves).
+//     own registers, with no separate two-symbol scan.
+// Round 4 also had k_wave2, the same units one frame at a time: slower than
+// k_wave at every SF and removed in round 5.
 // Results are bit-identical to k_wave: the same arithmetic in the same
 // order on the same values (tests/test_gpu_*: oracle, goldens, k_wave).
 //
@@ -48,14 +43,25 @@ typedef __attribute__((address_space(3))) unsigned lds_u32;
 // from `start` on by an LDS compare-and-swap (acquire), the wave learns it
 // by readfirstlane; with none free the wave sleeps and sweeps again.  A
 // holder never waits for anything but its own LDS operations, so every
-// wait ends.
+// wait ends; still, the sweeps are capped (2^20, ~0.1 s, far beyond any
+// holder's ~1 us) so that a lost lock can never hang the GPU, and at the cap
+// the wave gets -1: it then uses no buffer, and its caller leaves the unit
+// to the exact re-run (a symbol: kSymRecheck; an estimate: the frame to
+// kStatusFixup), so the outputs stay bit-exact.
+// `salt` >= 0 (test build, LPHY_F_DEBUG_LOCKFAIL): one sweep only, and every
+// third salt fails outright, so the tests reach the fail-safe path.
 template <int NBUF>
-__device__ __forceinline__ int wbuf_acquire(lds_u32* locks, int start) {
-    // (a safety cap: after ~2^20 sweeps - far beyond any holder's ~1 us -
-    // the wave proceeds with its first choice rather than spin forever; the
-    // exchange may then be wrong, which the parity tests would show, but
-    // the GPU never hangs on a lost lock)
-    for (unsigned spin = 0; spin < (1u << 20); ++spin) {
+__device__ __forceinline__ int wbuf_acquire(lds_u32* locks, int start, int salt) {
+    unsigned cap = 1u << 20;
+#ifdef LPHY_TEST_PATHS
+    if (salt >= 0) {
+        if (salt % 3 == 0) return -1;
+        cap = 1;
+    }
+#else
+    (void)salt;
+#endif
+    for (unsigned spin = 0; spin < cap; ++spin) {
         int got = -1;
         if ((threadIdx.x & 63) == 0) {
 #pragma unroll
@@ -74,7 +80,7 @@ __device__ __forceinline__ int wbuf_acquire(lds_u32* locks, int start) {
         if (got >= 0) return got;
         __builtin_amdgcn_s_sleep(2);
     }
-    return start;
+    return -1;
 }
 // Give the buffer back once this wave's reads of it are done (release: the
 // compiler orders the store after them; the LDS serves one wave's requests
@@ -83,65 +89,36 @@ __device__ __forceinline__ void wbuf_release(lds_u32* locks, int b) {
     if ((threadIdx.x & 63) == 0)
         __hip_atomic_store((unsigned*)&locks[b], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-
-// Max-abs of symbol s of frame f (the [dechirped] samples, as the
-// reference's normalisation scans them, LoRaDemod.cpp:60-78) by the whole
-// wave, NaN when one is not finite; wscan2's arithmetic over one symbol.
-template <int SF, int MODE>
-__device__ __noinline__ float wscan1(KArgs ka, unsigned f, unsigned s, const lds_cf32* ldnl) {
-    const DemodArgs& A = kargs(ka);
-    constexpr int N = 1 << SF;
-    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
-    const cf32* const dnl = (const cf32*)ldnl;
-    const int lane = threadIdx.x & 63;
-    const cf32* fr = A.iq + (unsigned long long)f * A.frame_samples + (unsigned long long)s * N;
-    iq_check(A, f, (long long)s * N + N - 1);
-    float fm = 0.0f;
-    cf32 sum = czero();
-    constexpr int U = 16;
-#pragma unroll 1
-    for (int r = 0; r < N / (64 * U); ++r) {
-        cf32 x[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = fr[(r * U + u) * 64 + lane];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            cf32 a = x[u];
-            if constexpr (DECH) a = cmul(a, dnl[((r * U + u) * 64 + lane) & (N - 1)]);
-            fm = max3_abs(fm, a.x, a.y);
-            sum = sum + a;
-        }
-    }
-    const bool bad = !(sum.x == sum.x && sum.y == sum.y) || !(fm <= 3.40282347e38f);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) fm = fmaxf(fm, __shfl_xor(fm, off, 64));
-    return __ballot(bad) ? __builtin_nanf("") : fm;
+// wbuf_acquire's salt: the unit's own number (lane 0's: wave-uniform, as the
+// acquisition is) under LPHY_F_DEBUG_LOCKFAIL, -1 otherwise
+__device__ __forceinline__ int wlock_salt(const DemodArgs& A, unsigned unit) {
+    return A.lock_fail ? (int)((unsigned)__builtin_amdgcn_readfirstlane((int)unit) & 0x3fffffffu) : -1;
 }
 
 struct WEst {
-    UnitResult ur;  // the lane's half (SF 9-11) or the unit's symbol (SF 12)
-    float mx;       // the two estimate symbols' max-abs (when computed here)
+    UnitResult ur;  // the lane's half
+    float mx;       // the frame's two estimate symbols' max-abs (when computed here)
 };
 
-// An estimate unit (KISS's arithmetic, bit for bit: LoRaDemod.cpp:80-136,
-// phy.cpp:81-148): SF 9-11 symbols 0 and 1 in halves 0 and 1, SF 12 symbol
-// j.  With `find_mx` (modes 1/2, the frame's first estimate unit) the unit
-// also folds the two estimate symbols' max-abs from its own samples - SF 12:
-// symbol 1 by wscan1 first - and normalises with it; otherwise with `mx`.
+// The settle re-run of a frame's estimate unit (KISS's arithmetic, bit for
+// bit: LoRaDemod.cpp:80-136, phy.cpp:81-148): symbols 0 and 1 in halves 0
+// and 1 (the other halves idle), normalised with the frame's true max-abs
+// `mx`.  Without an exchange buffer (wbuf_acquire's cap) the unit reports
+// NaN, which sends the frame to the exact re-run.
 template <int SF, int MODE>
 __device__ __noinline__ WEst west2(KArgs ka, lds_cf32* lpool, lds_u32* locks, const lds_cf32* ldnl, unsigned f,
-                                   unsigned j, float mx, bool find_mx) {
+                                   float mx) {
     using W = WGeo<SF>;
     using L = W2Lds<SF, MODE>;
     constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
+    static_assert(SPW >= 2, "both estimate symbols in one unit");
     constexpr bool M0 = (MODE & 3) == LPHY_MODE_DEMODULATE;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     const DemodArgs& A = kargs(ka);
     const cf32* const dnl = (const cf32*)ldnl;
     const int lane = threadIdx.x & 63, h = lane / LPS, l = lane % LPS;
-    // the half's symbol: SF 12 symbol j; below, halves 0 and 1 (the others idle)
-    const bool mine = SPW == 1 || h < 2;
-    const unsigned s = SPW == 1 ? j : (unsigned)(h < 2 ? h : 0);
+    const bool mine = h < 2;
+    const unsigned s = (unsigned)(h < 2 ? h : 0);
     cf32 v[64];
     const cf32* src = A.iq + (unsigned long long)f * A.frame_samples + (unsigned long long)s * N + l;
     iq_check(A, f, (long long)s * N + l + LPS * 63);
@@ -156,26 +133,6 @@ __device__ __noinline__ WEst west2(KArgs ka, lds_cf32* lpool, lds_u32* locks, co
 #pragma unroll
         for (int e = 0; e < 64; ++e) v[e] = cmul(v[e], dnl[l + LPS * e]);
     }
-    if constexpr (!M0) {
-        if (find_mx) {
-            float fm = 0.0f;
-            cf32 sum = czero();
-#pragma unroll
-            for (int e = 0; e < 64; ++e) {
-                fm = max3_abs(fm, v[e].x, v[e].y);
-                sum = sum + v[e];
-            }
-            const bool bad = !(sum.x == sum.x && sum.y == sum.y) || !(fm <= 3.40282347e38f);
-            // over the two estimate symbols' lanes (all 64 at SF 11-12)
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) fm = fmaxf(fm, __shfl_xor(fm, off, 64));
-            mx = __ballot(bad) ? __builtin_nanf("") : fm;
-            if constexpr (SPW == 1) {
-                const float m1 = wscan1<SF, MODE>(ka, f, 1u, ldnl);
-                mx = (mx == mx && m1 == m1) ? fmaxf(mx, m1) : __builtin_nanf("");
-            }
-        }
-    }
     lphy_frame_meta nm{};
     nm.scale = 1.0f;
     if constexpr (!M0) nm = norm_meta_hot(mx, true, A.no_scratch);
@@ -188,16 +145,18 @@ __device__ __noinline__ WEst west2(KArgs ka, lds_cf32* lpool, lds_u32* locks, co
     }
     const WTw<SF> T{};  // unused by the exact pass
     wpass1<SF, false>(v, ctw(A.tw));
-    const int b = wbuf_acquire<L::NBUF>(locks, (threadIdx.x >> 6) & (L::NBUF - 1));
-    cf32* const buf = (cf32*)(lpool + b * W::BUF);
-    wexchange<SF>(v, buf, h, l);
-    // pass 2's per-lane twiddles from an LDS copy of the KISS table
-    wait_lgkm0();  // the exchange reads are done
-    wdma_table<SF>(A.tw, buf, lane);
-    wait_vm0();
-    wpass2<SF, false>(v, T, buf, l);
-    wait_lgkm0();
-    wbuf_release(locks, b);
+    const int b = wbuf_acquire<L::NBUF>(locks, (threadIdx.x >> 6) & (L::NBUF - 1), wlock_salt(A, f + 1));
+    if (b >= 0) {
+        cf32* const buf = (cf32*)(lpool + b * W::BUF);
+        wexchange<SF>(v, buf, h, l);
+        // pass 2's per-lane twiddles from an LDS copy of the KISS table
+        wait_lgkm0();  // the exchange reads are done
+        wdma_table<SF>(A.tw, buf, lane);
+        wait_vm0();
+        wpass2<SF, false>(v, T, buf, l);
+        wait_lgkm0();
+        wbuf_release(locks, b);
+    }
     float sumsq = 0.0f;
 #pragma unroll
     for (int e = 0; e < 64; ++e) {
@@ -207,13 +166,13 @@ __device__ __noinline__ WEst west2(KArgs ka, lds_cf32* lpool, lds_u32* locks, co
     const unsigned long long nb = __ballot(!(sumsq == sumsq));
     WEst r;
     r.ur = wunit_result<SF>(v, h, l, lane);
-    r.ur.nan = (LPS == 64 ? nb : ((nb >> (LPS * h)) & ((1ull << (LPS & 63)) - 1))) != 0 ? 1 : 0;
+    r.ur.nan = (b < 0 || ((nb >> (LPS * h)) & ((1ull << (LPS & 63)) - 1)) != 0) ? 1 : 0;
     if (!live) r.ur = UnitResult{0, 0, 0.0f, 0.0f, 0};
     r.mx = mx;
     return r;
 }
 
-// The pair's two results (SF 9-11: halves 0 and 1; SF 12: the two units).
+// The pair's two results (halves 0 and 1).
 __device__ __forceinline__ UnitResult wur_from(const UnitResult& u, int src) {
     UnitResult r;
     r.idx = __shfl(u.idx, src, 64);
@@ -236,7 +195,7 @@ __device__ __noinline__ void wclose2(KArgs ka, lds_cf32* lpool, lds_u32* locks, 
                                      float rate, float scale, int t_off, float mx01, float m, float r, bool nan,
                                      bool open) {
     using W = WGeo<SF>;
-    constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
+    constexpr int N = W::N, LPS = W::LPS;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     const DemodArgs& A = kargs(ka);
     const cf32* const dnl = (const cf32*)ldnl;
@@ -254,20 +213,10 @@ __device__ __noinline__ void wclose2(KArgs ka, lds_cf32* lpool, lds_u32* locks, 
         return;
     }
     if (me.scale == mg.scale && me.normalised == mg.normalised) return;
-    // settle: the estimate units with the frame's true max-abs (norm_meta_hot
+    // settle: the estimate unit with the frame's true max-abs (norm_meta_hot
     // of it gives me.scale)
-    UnitResult ua{0, 0, 0.0f, 0.0f, 0}, ub = ua;
-#pragma unroll 1
-    for (int j = 0; j < W::NE; ++j) {
-        const WEst e = west2<SF, MODE>(ka, lpool, locks, ldnl, f, (unsigned)j, mt, false);
-        if constexpr (SPW == 1) {
-            if (j == 0) ua = e.ur;
-            else ub = e.ur;
-        } else {
-            ua = wur_from(e.ur, 0);
-            ub = wur_from(e.ur, LPS);
-        }
-    }
+    const WEst est = west2<SF, MODE>(ka, lpool, locks, ldnl, f, mt);
+    const UnitResult ua = wur_from(est.ur, 0), ub = wur_from(est.ur, LPS);
     lphy_frame_meta e = me;
     EstFold fold;
     if (ua.valid) fold.add(ua.idx, ua.findex, 0, ua.phase);
@@ -287,259 +236,11 @@ __device__ __noinline__ void wclose2(KArgs ka, lds_cf32* lpool, lds_u32* locks, 
     }
 }
 
-template <int SF, int MODE>
-__global__ __launch_bounds__(512) void k_wave2(FrameArgs P) {
-    using W = WGeo<SF>;
-    using L = W2Lds<SF, MODE>;
-    constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
-    constexpr bool M0 = (MODE & 3) == LPHY_MODE_DEMODULATE;
-    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
-    const DemodArgs& A = P.A;
-    const KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
-    // the down-chirp at LDS offset 0 (its wrapped index is the byte address
-    // itself), the exchange buffers after it, their locks last
-    __shared__ cf32 lds_all[L::DNC + L::NBUF * W::BUF];
-    __shared__ unsigned locks_s[L::NBUF];
-    cf32* const dnl = lds_all;
-    lds_cf32* const pool = (lds_cf32*)(lds_all + L::DNC);
-    lds_u32* const locks = (lds_u32*)locks_s;
-
-    const int tid = threadIdx.x;
-    if constexpr (L::DN) {
-        for (int i = tid; i < N; i += 512) dnl[i] = A.down[i];
-    }
-    if (tid < L::NBUF) locks_s[tid] = 0u;
-    __syncthreads();  // the only workgroup barrier: waves are independent below
-
-    const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int h = lane / LPS, l = lane % LPS;
-    const unsigned nframes = (unsigned)A.frames;
-    const unsigned S = (unsigned)A.total_syms;
-    const unsigned Wn = P.waves;
-    const unsigned w = blockIdx.x * L::WPB + wv;
-    if (w >= nframes) return;
-    WSched<SF> sch;
-    sch.nk = (nframes - 1 - w) / Wn + 1;
-    sch.ND = (S + SPW - 1) / SPW;
-    sch.p = sch.ND >= 2 ? sch.ND - 2 : 0;
-    const bool spec = !M0 && A.spec != 0;
-    // the wave's first choice of exchange buffer (spreads the waves)
-    const int bstart = wv & (L::NBUF - 1);
-
-    WFrame rec0{0.0f, 1.0f, 0.0f, 0, 0}, rec1 = rec0;
-    auto rec = [&](unsigned k) -> WFrame { return (k & 1) ? rec1 : rec0; };
-    auto set_rec = [&](unsigned k, const WFrame& r) {
-        if (k & 1) rec1 = r;
-        else rec0 = r;
-    };
-    auto fglob = [&](unsigned k) { return w + k * Wn; };
-
-    cf32 Qr[8], Pr[8];
-    unsigned rot_frame = 0xffffffffu;
-    constexpr float kBig = 3.0e38f;
-    float sp_mx = 0.0f, sp_r = kBig;
-    unsigned sp_fl = 0u;
-    UnitResult ur0{0, 0, 0.0f, 0.0f, 0};  // SF 12: the first estimate unit's result
-
-    for (WCursor cu = sch.first(); sch.kind(cu) != kWDead;) {
-        const WCursor nx = sch.next(cu);
-        const unsigned k = sch.frame(cu), f = fglob(k);
-        if (sch.kind(cu) == kWSym) {
-            const WFrame R = rec(k);
-            const unsigned s = SPW * cu.j + (unsigned)h;
-            const bool live = s < S;
-            lphy_frame_meta m{};
-            m.rate = R.rate;
-            m.scale = R.scale;
-            m.t_off = R.t_off;
-            m.status = R.ok ? 0 : -1;
-            m.have_sync = 1;
-            const SymCtx c = sym_ctx(A, f, live ? s : 0u, live, N, m);
-            // the unit's IQ, straight into the registers (no window for a
-            // symbol the frame does not have)
-            cf32 v[64];
-            {
-                const cf32* src = A.iq + (unsigned long long)f * A.frame_samples + c.base + (unsigned)l;
-                if (live) {
-                    iq_check(A, f, (long long)c.base + l + LPS * 63);
-#pragma unroll
-                    for (int e = 0; e < 64; ++e) v[e] = src[LPS * e];
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 64; ++e) v[e] = czero();
-                }
-            }
-            if (k != rot_frame) {
-                rot_frame = k;
-                const WRot rt = wrot<SF, MODE>(R.rate, R.scale);
-#pragma unroll
-                for (int b = 0; b < 8; ++b) Qr[b] = rt.q[b];
-#pragma unroll
-                for (int a = 0; a < 8; ++a)
-                    Pr[a] = cf32{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(rt.p.x), a)),
-                                 __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rt.p.y), a))};
-            }
-            // staging in place: [exact dechirp at the window's own chirp
-            // indices,] max-abs fold, certified rotation
-            float amax = 0.0f;
-            const unsigned d0 = ((c.base + (unsigned)l) & (unsigned)(N - 1)) << 3;
-            // in chunks of 8 samples, chunk q + 1's down-chirp reads issued
-            // before chunk q's arithmetic (sched barriers keep the order and
-            // the registers: 16 in flight, not 128)
-            cf32 dq[2][8];
-            auto ld_chunk = [&](int q, cf32 (&ds)[8]) __attribute__((always_inline)) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const int e = 8 * q + i;
-                    if constexpr (DECH) ds[i] = lds_ld(dnl, (int)((d0 + (unsigned)((LPS * e) << 3)) & (unsigned)(8 * N - 1)));
-                    if constexpr (M0) ds[i] = dnl[l + LPS * e];
-                }
-            };
-            ld_chunk(0, dq[0]);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                if (q + 1 < 8) ld_chunk(q + 1, dq[(q + 1) & 1]);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const int e = 8 * q + i;
-                    cf32 p = v[e];
-                    if constexpr (DECH) p = cmul(p, dq[q & 1][i]);
-                    amax = max3_abs(amax, p.x, p.y);
-                    if constexpr (M0) p = cmul(p, dq[q & 1][i]);
-                    v[e] = cmul_fma(cmul_fma(p, Qr[i]), Pr[q]);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            wpass1<SF, true>(v, ctw(A.tw));
-            // pass 2's per-lane twiddles (9 loads, cached), issued before the
-            // exchange so they land during it; not kept across units (VGPRs)
-            // (the lane indices made opaque: the exchange's lane addresses and
-            // these loads are then recomputed / reissued each unit, a few VALU
-            // and 9 cached loads, rather than hoisted out of the loop, where
-            // the compiler spills them and reloads each from scratch)
-            int hx = h, lx = l;
-            asm volatile("" : "+v"(hx), "+v"(lx));
-            WTw<SF> T;
-            T.load(A.tw, lx);
-            const int b = wbuf_acquire<L::NBUF>(locks, bstart);
-            wexchange<SF>(v, (cf32*)(pool + b * W::BUF), hx, lx);
-            wait_lgkm0();  // the exchange reads are done
-            wbuf_release(locks, b);
-            wpass2<SF, true>(v, T, A.tw, l);
-            // keyed top two over the half's bins l + LPS e (see k_wave)
-            unsigned k1 = 0u, k2 = 0u;
-#pragma unroll
-            for (int e = 0; e < 64; e += 2) {
-                const float ma = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
-                const float mb = __builtin_fmaf(v[e + 1].x, v[e + 1].x, v[e + 1].y * v[e + 1].y);
-                top2_pair(k1, k2, (__float_as_uint(ma) & ~63u) | (unsigned)e,
-                          (__float_as_uint(mb) & ~63u) | (unsigned)(e + 1));
-            }
-            unsigned K1, K2;
-            wave_top2_merge<LPS>(k1, k2, h, K1, K2);
-            const unsigned long long bm = __ballot(k1 == K1);
-            const unsigned long long hm = LPS == 64 ? bm : ((bm >> (LPS * h)) & ((1ull << (LPS & 63)) - 1));
-            ArgMax2 b2;
-            b2.v = __uint_as_float(K1 & ~63u);
-            b2.v2 = __uint_as_float(K2 | 63u);
-            b2.i = (__ffsll((long long)hm) - 1) + LPS * (int)(K1 & 63u);
-            float am = 1.0f;  // modes 1/2: normalised frame (see fast_certified)
-            if constexpr (M0) {
-#pragma unroll
-                for (int off = 1; off < LPS; off <<= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
-                am = amax;
-            }
-            const float cb1 = cert_bound<SF>(c.rate, c.start, 1.0f, kWaveExtra);
-            const float cgap = cert_gap(b2);
-            const bool cert = cgap > 4.0f * (cb1 * am) && (float)N * 1.41421366f * am * 1.0001f < 1e18f &&
-                              am >= 1e-20f && b2.v >= 1e-30f;
-            const bool redo = c.ok && (!cert || A.debug_recheck);  // (DEBUG_RECHECK: tests)
-            if (live && l == 0) {
-                const uint16_t out = redo ? kSymRecheck : (uint16_t)b2.i;
-                if (c.have_sync && c.s < 2) store_symbol(A, c, c.ok ? out : (uint16_t)0);
-                else if (c.ok) store_symbol(A, c, out);
-                if (redo) A.meta[c.f].status = kStatusRecheck;
-            }
-            if (spec && c.ok) {
-                sp_mx = fmaxf(sp_mx, amax);
-                const cf32 q = v[0] * v[0];
-                const float q2 = q.x + q.y;
-                if (!(q2 == q2)) sp_fl |= 1u;  // a NaN sample reaches every bin
-                if (l == 0) {
-                    if (redo) sp_fl |= 2u;
-                    else sp_r = fminf(sp_r, cgap * __builtin_amdgcn_rcpf(cb1) * (1.0f - 4.0f * kU));
-                }
-            }
-            // the frame's last symbol unit closes it (speculative normalisation)
-            if (spec && cu.phase == 3 && cu.j + 1 == sch.ND) {
-                float mm = sp_mx, rr = sp_r;
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) {
-                    mm = fmaxf(mm, __shfl_xor(mm, off, 64));
-                    rr = fminf(rr, __shfl_xor(rr, off, 64));
-                }
-                const bool nan = __ballot(sp_fl & 1u) != 0, open = __ballot(sp_fl & 2u) != 0;
-                sp_mx = 0.0f;
-                sp_r = kBig;
-                sp_fl = 0u;
-                if (R.ok)
-                    wclose2<SF, MODE>(ka, pool, locks, (const lds_cf32*)dnl, f, R.rate, R.scale, R.t_off, R.mx, mm,
-                                      rr, nan, open);
-            }
-        } else {
-            // estimate unit(s): SF 12 symbol j, below symbols 0 and 1 in halves 0 and 1
-            const WFrame R0 = rec(k);
-            const bool first = cu.j == 0;
-            const WEst est = west2<SF, MODE>(ka, pool, locks, (const lds_cf32*)dnl, f, cu.j, R0.mx, first);
-            const UnitResult ur = est.ur;
-            bool fold_now = true;
-            UnitResult ua = ur, ub = ur;
-            if constexpr (SPW == 1) {
-                if (first) {
-                    ur0 = ur;
-                    fold_now = false;
-                } else {
-                    ua = ur0;
-                }
-            } else {
-                ua = wur_from(ur, 0);
-                ub = wur_from(ur, LPS);
-            }
-            WFrame r = R0;
-            if (first) r.mx = est.mx;
-            if (fold_now) {
-                lphy_frame_meta m{};
-                m.scale = 1.0f;
-                m.have_sync = 1;
-                if constexpr (!M0) m = norm_meta_hot(r.mx, true, A.no_scratch);
-                if (m.status == 0) {
-                    EstFold fold;
-                    if (ua.valid) fold.add(ua.idx, ua.findex, 0, ua.phase);
-                    else fold.add(0, 0.0f, 0, 0.0f);
-                    if (ub.valid) fold.add(ub.idx, ub.findex, 0, ub.phase);
-                    else fold.add(0, 0.0f, 0, 0.0f);
-                    fold.finish(m, 2, N, 1);
-                    if (ua.nan || ub.nan) m.status = kStatusFixup;
-                }
-                bound_check(f, (long long)A.frames);
-                if (lane == 0) meta_put_est(&A.meta[f], m);
-                r.rate = m.rate;
-                r.scale = m.scale;
-                r.t_off = m.t_off;
-                r.ok = m.status == 0 ? 1 : 0;
-            }
-            set_rec(k, r);
-        }
-        cu = nx;
-    }
-}
-
 // ---------------------------------------------------------------------------
-// k_wave2s: the same units spanning frames (SF 9-10: 8 / 4 symbols per unit).
-// k_wave2 gives every frame whole units of its own: at SF 9 a frame's 66
-// symbols take 9 units, the last with 2 live halves of 8, and its estimate
-// unit uses 2 halves of 8 - 10 units for 8.5 units of work.  Here a wave's
+// k_wave2s: units spanning frames (SF 9-10: 8 / 4 symbols per unit).
+// Whole units per frame (k_wave) give a frame's 66 symbols at SF 9 9 units,
+// the last with 2 live halves of 8, and its estimate unit uses 2 halves of
+// 8 - 10 units for 8.5 units of work.  Here a wave's
 // frames w, w + W, ... form one stream of symbols (frame k's symbol s at
 // position k S + s) cut into units of SPW consecutive symbols, whatever
 // frames they belong to, and one estimate unit takes the two estimate
@@ -550,6 +251,12 @@ __global__ __launch_bounds__(512) void k_wave2(FrameArgs P) {
 // certificate ratio and flags, which each unit's halves fold in with LDS
 // atomics); the unit holding a frame's last symbol closes it (wclose2).
 // Each lane rotates with its own frame's tables.
+// Precondition (host, launch_wave_mode): frames of at least SPW symbols
+// (S >= SPW).  Then a unit of SPW consecutive stream positions holds at most
+// one frame end (ends are S apart), so it closes at most one frame, a lane's
+// position advances past at most one frame end per unit, and a unit spans at
+// most two frames, which the ring holds with the EPU frames of the estimate
+// unit ahead.  Shorter frames take k_wave.
 // ---------------------------------------------------------------------------
 struct WRec {  // 32 B
     float rate, scale, mx;  // estimate: rotation rate, normalisation, estimate symbols' max-abs
@@ -630,15 +337,19 @@ __device__ __noinline__ WEst west2s(KArgs ka, lds_cf32* lpool, lds_u32* locks, c
     }
     const WTw<SF> T{};  // unused by the exact pass
     wpass1<SF, false>(v, ctw(A.tw));
-    const int b = wbuf_acquire<L::NBUF>(locks, (threadIdx.x >> 6) & (L::NBUF - 1));
-    cf32* const buf = (cf32*)(lpool + b * W::BUF);
-    wexchange<SF>(v, buf, h, l);
-    wait_lgkm0();
-    wdma_table<SF>(A.tw, buf, lane);
-    wait_vm0();
-    wpass2<SF, false>(v, T, buf, l);
-    wait_lgkm0();
-    wbuf_release(locks, b);
+    // (no exchange buffer at wbuf_acquire's cap: the unit reports NaN, which
+    // sends its frames to the exact re-run)
+    const int b = wbuf_acquire<L::NBUF>(locks, (threadIdx.x >> 6) & (L::NBUF - 1), wlock_salt(A, fg + 2));
+    if (b >= 0) {
+        cf32* const buf = (cf32*)(lpool + b * W::BUF);
+        wexchange<SF>(v, buf, h, l);
+        wait_lgkm0();
+        wdma_table<SF>(A.tw, buf, lane);
+        wait_vm0();
+        wpass2<SF, false>(v, T, buf, l);
+        wait_lgkm0();
+        wbuf_release(locks, b);
+    }
     float sumsq = 0.0f;
 #pragma unroll
     for (int e = 0; e < 64; ++e) {
@@ -648,7 +359,7 @@ __device__ __noinline__ WEst west2s(KArgs ka, lds_cf32* lpool, lds_u32* locks, c
     const unsigned long long nb = __ballot(!(sumsq == sumsq));
     WEst r;
     r.ur = wunit_result<SF>(v, h, l, lane);
-    r.ur.nan = ((nb >> (LPS * h)) & ((1ull << (LPS & 63)) - 1)) != 0 ? 1 : 0;
+    r.ur.nan = (b < 0 || ((nb >> (LPS * h)) & ((1ull << (LPS & 63)) - 1)) != 0) ? 1 : 0;
     if (!live) r.ur = UnitResult{0, 0, 0.0f, 0.0f, 0};
     r.mx = mx;
     return r;
@@ -827,10 +538,18 @@ __global__ __launch_bounds__(512) void k_wave2s(FrameArgs P) {
         asm volatile("" : "+v"(hx), "+v"(lx));
         WTw<SF> T;
         T.load(A.tw, lx);
-        const int b = wbuf_acquire<L::NBUF>(locks, bstart);
-        wexchange<SF>(v, (cf32*)(pool + b * W::BUF), hx, lx);
-        wait_lgkm0();
-        wbuf_release(locks, b);
+        // (no exchange buffer at wbuf_acquire's cap: the unit's symbols go to
+        // the exact re-run, `lost`)
+        const int b = wbuf_acquire<L::NBUF>(locks, bstart, wlock_salt(A, u));
+        const bool lost = b < 0;
+        if (!lost) {
+            wexchange<SF>(v, (cf32*)(pool + b * W::BUF), hx, lx);
+            wait_lgkm0();
+            wbuf_release(locks, b);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 64; ++e) v[e] = czero();
+        }
         wpass2<SF, true>(v, T, A.tw, l);
         unsigned k1 = 0u, k2 = 0u;
 #pragma unroll
@@ -858,7 +577,7 @@ __global__ __launch_bounds__(512) void k_wave2s(FrameArgs P) {
         const float cgap = cert_gap(b2);
         const bool cert = cgap > 4.0f * (cb1 * am) && (float)N * 1.41421366f * am * 1.0001f < 1e18f &&
                           am >= 1e-20f && b2.v >= 1e-30f;
-        const bool redo = c.ok && (!cert || A.debug_recheck);
+        const bool redo = c.ok && (!cert || A.debug_recheck || lost);
         if (live && l == 0) {
             const uint16_t out = redo ? kSymRecheck : (uint16_t)b2.i;
             if (c.have_sync && c.s < 2) store_symbol(A, c, c.ok ? out : (uint16_t)0);

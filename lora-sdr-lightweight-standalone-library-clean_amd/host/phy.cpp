@@ -152,10 +152,37 @@ lphy_hip_ctx* decode_ctx(int* err) { return thread_ctx(7, 125000, 1, err); }
 
 // lora_workspace -> its context (the reference struct has no room for it).
 // Lookups take a shared lock only; init() replaces the entry.
+// The reference has no free function for lora_workspace, so an application
+// that heap-allocates a workspace per session would otherwise leave a
+// context (stream, staging, pinned mirror) behind for every address it ever
+// passed to init().  So at most kMaxWsContexts workspaces get a context of
+// their own; the workspaces beyond them are not remembered and share one
+// context per (sf, bw, osr, window) (shared_ctx: calls on it are serialised
+// by the context's mutex, so they are correct, just not concurrent).  Both
+// the map and the number of contexts stay bounded.
+constexpr size_t kMaxWsContexts = 64;
 std::shared_mutex ws_mu;
 std::unordered_map<const lora_workspace*, lphy_hip_ctx*> ws_map;
 
 int window_flag(window_type k, const void* buf);
+
+// The shared context of a configuration (made once, never released).
+lphy_hip_ctx* shared_ctx(unsigned sf, unsigned bw_hz, unsigned osr, int window, int* err) {
+    static std::mutex mu;
+    static std::map<std::tuple<unsigned, unsigned, unsigned, int>, lphy_hip_ctx*> m;
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_tuple(sf, bw_hz, osr, window);
+    auto it = m.find(key);
+    if (it != m.end()) return it->second;
+    lphy_hip_ctx* c = own_ctx(sf, bw_hz, osr, window, kReserveSymbols * (size_t(1) << sf) * osr, err);
+    if (c) m.emplace(key, c);
+    return c;
+}
+
+bool ws_has_room(const lora_workspace* ws) {
+    std::shared_lock<std::shared_mutex> lk(ws_mu);
+    return ws_map.count(ws) != 0 || ws_map.size() < kMaxWsContexts;
+}
 
 lphy_hip_ctx* ws_ctx(const lora_workspace* ws, unsigned sf, unsigned osr, int* err) {
     {
@@ -163,16 +190,24 @@ lphy_hip_ctx* ws_ctx(const lora_workspace* ws, unsigned sf, unsigned osr, int* e
         auto it = ws_map.find(ws);
         if (it != ws_map.end()) return it->second;
     }
+    const unsigned bw = static_cast<unsigned>(ws->bw);
+    const int win = window_flag(ws->window_kind, ws->window);
+    if (!ws_has_room(ws)) return shared_ctx(sf, bw, osr, win, err);
     // a workspace init() did not set up here (e.g. a copy): make its context now
-    lphy_hip_ctx* c = own_ctx(sf, static_cast<unsigned>(ws->bw), osr, window_flag(ws->window_kind, ws->window),
-                              kReserveSymbols * (size_t(1) << sf) * osr, err);
+    lphy_hip_ctx* c = own_ctx(sf, bw, osr, win, kReserveSymbols * (size_t(1) << sf) * osr, err);
     if (!c) return nullptr;
     std::unique_lock<std::shared_mutex> lk(ws_mu);
-    auto r = ws_map.emplace(ws, c);
-    if (!r.second) {  // another thread got there first
+    auto it = ws_map.find(ws);
+    if (it != ws_map.end()) {  // another thread got there first
         release_ctx(c);
-        return r.first->second;
+        return it->second;
     }
+    if (ws_map.size() >= kMaxWsContexts) {  // the last place went meanwhile
+        release_ctx(c);
+        lk.unlock();
+        return shared_ctx(sf, bw, osr, win, err);
+    }
+    ws_map.emplace(ws, c);
     return c;
 }
 
@@ -254,20 +289,27 @@ int init(lora_workspace* ws, const lora_params* cfg) {  // phy.cpp:27-52
     if (ws->window) fill_window(ws->window, (size_t)N, ws->window_kind);
     // the workspace's GPU context and staging, so later calls allocate
     // nothing (the reference allocates nothing after init, API_SPEC.md:9-14)
+    // (beyond kMaxWsContexts workspaces: the configuration's shared context,
+    // made here so that calls still allocate nothing)
     int err = 0;
-    lphy_hip_ctx* c = own_ctx(cfg->sf, static_cast<unsigned>(ws->bw), ws->osr,
-                              window_flag(ws->window_kind, ws->window),
-                              kReserveSymbols * size_t(N) * ws->osr, &err);
+    const unsigned bw = static_cast<unsigned>(ws->bw);
+    const int win = window_flag(ws->window_kind, ws->window);
+    lphy_hip_ctx* c = ws_has_room(ws) ? own_ctx(cfg->sf, bw, ws->osr, win, kReserveSymbols * size_t(N) * ws->osr, &err)
+                                      : nullptr;
     if (c) {
         std::unique_lock<std::shared_mutex> lk(ws_mu);
         auto it = ws_map.find(ws);
         if (it != ws_map.end()) {
             release_ctx(it->second);  // re-init: the new configuration wins
             it->second = c;
-        } else {
+        } else if (ws_map.size() < kMaxWsContexts) {
             ws_map.emplace(ws, c);
+        } else {
+            release_ctx(c);
+            c = nullptr;
         }
     }
+    if (!c) (void)shared_ctx(cfg->sf, bw, ws->osr, win, &err);
     (void)decode_ctx(&err);  // this thread's decoder context
     return 0;
 }

@@ -45,8 +45,14 @@ F_UNFUSED = 32  # separate prologue / symbol launches (lphy_hip.h)
 F_EXACT_ROTATION = 64  # every symbol with the reference's per-sample rotation
 F_SCAN_FIRST = 256  # modes 1/2: whole-frame max-abs pre-scan (no speculation)
 F_DEBUG_RECHECK = 512  # every symbol / estimated frame left to the exact re-run
+F_DEBUG_LOCKFAIL = 1024  # k_wave2s: exchange-buffer locks fail (the fail-safe re-run path)
 WINDOW_NONE = 0
 WINDOW_HANN = 1
+# Smallest batch new Demodulators send to the fused kernels
+# (lphy_hip_ctx_set_fused_min_frames); None keeps the library's measured
+# per-SF crossover.  The test suite sets 0 (tests/conftest.py) so that its
+# small batches run the fused kernels.
+FUSED_MIN_FRAMES = None
 
 
 class FrameMeta(C.Structure):
@@ -72,6 +78,7 @@ _sz = C.c_size_t
 
 EXPORTS = (
     "lphy_hip_ctx_create", "lphy_hip_ctx_destroy", "lphy_hip_ctx_share", "lphy_hip_ctx_reserve",
+    "lphy_hip_ctx_set_fused_min_frames",
     "lphy_hip_syms_per_frame", "lphy_hip_recheck_count", "lphy_hip_bounds_violations",
     "lphy_hip_demod_batch", "lphy_hip_decode_batch", "lphy_hip_estimate_batch",
     "lphy_hip_compensate", "lphy_hip_modulate_batch", "lphy_hip_demod_host",
@@ -129,6 +136,7 @@ def load(path: Path | None = None) -> C.CDLL:
     L.lphy_hip_ctx_destroy.restype = None
     L.lphy_hip_ctx_share.argtypes = [C.POINTER(_vp), _vp, C.c_uint]
     L.lphy_hip_ctx_reserve.argtypes = [_vp, _sz, _sz]
+    L.lphy_hip_ctx_set_fused_min_frames.argtypes = [_vp, C.c_long]
     L.lphy_hip_bounds_violations.argtypes = [_vp, C.POINTER(C.c_ulonglong), C.c_int]
     L.lphy_hip_syms_per_frame.argtypes = [_vp, _sz, C.c_int]
     L.lphy_hip_syms_per_frame.restype = _sz
@@ -207,6 +215,14 @@ class Demodulator:
         _chk(self.lib.lphy_hip_ctx_create(C.byref(h), device, sf, bw_hz, osr, window),
              "lphy_hip_ctx_create")
         self.ctx = h
+        if FUSED_MIN_FRAMES is not None:
+            self.set_fused_min_frames(FUSED_MIN_FRAMES)
+
+    def set_fused_min_frames(self, frames: int) -> None:
+        """Smallest batch that takes the fused kernels on this context
+        (< 0: the library's measured per-SF crossover)."""
+        _chk(self.lib.lphy_hip_ctx_set_fused_min_frames(self.ctx, int(frames)),
+             "lphy_hip_ctx_set_fused_min_frames")
 
     def close(self):
         if self.ctx:

@@ -128,14 +128,46 @@ def mixed_plan(total: int, world: int, rank: int, seed: int = 0xC3, payload: int
     return first, count, mine, pays[first:first + count], {k: v for k, v in buckets.items() if v.size}
 
 
-def reassemble(buckets: dict, parts: dict, count: int, payload: int = 32):
-    """Inverse of the SF bucketing: `parts[sf]` holds the decoded payloads
-    of bucket sf (frames in bucket order, `payload` bytes each, numpy or
-    torch); returns the range's payloads in frame order (numpy)."""
+def reassemble(buckets: dict, parts: dict, count: int, payload: int = 32, dtype=None):
+    """Inverse of the SF bucketing: `parts[sf]` holds bucket sf's rows
+    (frames in bucket order, `payload` elements each - decoded payload
+    bytes, u16 symbols or 32-byte records; numpy or torch); returns the
+    range's rows in frame order (numpy, dtype of the parts or `dtype`)."""
     import numpy as np
-    out = np.zeros((count, payload), np.uint8)
+    out = None
     for sf, idx in buckets.items():
         p = parts[sf]
         p = p.cpu().numpy() if hasattr(p, "cpu") else np.asarray(p)
+        if out is None:
+            out = np.zeros((count, payload), dtype or p.dtype)
         out[idx] = p.reshape(-1, payload)[: idx.size]
-    return out
+    return out if out is not None else np.zeros((count, payload), dtype or np.uint8)
+
+
+def mixed_slab_bytes(total: int, world: int, syms_per_frame: int, payload: int, **plan_kw) -> int:
+    """C3 (mixed SF): the size every rank's result slab is padded to - the
+    largest rank's layout of one part per SF bucket - computed by every rank
+    from the seeded plan, so no size exchange precedes the gather.  plan_kw:
+    mixed_plan's seed / sf_lo / sf_hi (its payload is `payload`)."""
+    best = 0
+    for r in range(world):
+        plan = mixed_plan(total, world, r, payload=payload, **plan_kw)[4]
+        best = max(best, slab_layout([plan[sf].size for sf in sorted(plan)], syms_per_frame, payload)[1])
+    return best
+
+
+def gather_mixed(parts, total: int, world: int, syms_per_frame: int, payload: int, **plan_kw):
+    """Rank 0 after the C3 gather: every rank's slab (one part per SF bucket,
+    buckets in SF order) unpacked and put back in stream order.  Returns
+    (symbols [total, spf] u16, payloads [total, payload] u8, records
+    [total, 32] u8) of the whole stream."""
+    import numpy as np
+    syms, pays, recs = [], [], []
+    for r in range(world):
+        _, c_r, _, _, plan = mixed_plan(total, world, r, payload=payload, **plan_kw)
+        order = sorted(plan)
+        unp = unpack_slab(parts[r], [plan[sf].size for sf in order], syms_per_frame, payload)
+        syms.append(reassemble(plan, {sf: u[0] for sf, u in zip(order, unp)}, c_r, syms_per_frame, np.uint16))
+        pays.append(reassemble(plan, {sf: u[1] for sf, u in zip(order, unp)}, c_r, payload, np.uint8))
+        recs.append(reassemble(plan, {sf: u[2] for sf, u in zip(order, unp)}, c_r, META_BYTES, np.uint8))
+    return np.concatenate(syms), np.concatenate(pays), np.concatenate(recs)

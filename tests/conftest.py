@@ -11,10 +11,14 @@ for p in (str(ROOT / "tests" / "golden"), str(ROOT / "tests"), str(PKG), str(ROO
         sys.path.insert(0, p)
 
 # The suite's small batches exercise the fused kernels: the library would
-# give a batch below fused_min_frames (lphy_hip.hip) to the separate
-# launches, which the tests reach with LPHY_F_UNFUSED and the lora_phy::
-# probes (tests/test_gpu_cxx_api.py, run with the library's defaults).
-os.environ.setdefault("LPHY_FUSED_MIN_FRAMES", "0")
+# give a batch below its fused_min_frames crossover (lphy_hip.hip) to the
+# separate launches, which the tests reach with LPHY_F_UNFUSED and the
+# lora_phy:: probes (tests/test_gpu_cxx_api.py, run with the library's
+# defaults).  Every Demodulator the tests make gets
+# lphy_hip_ctx_set_fused_min_frames(0).
+import lphy as _lphy  # noqa: E402  (the module only; the library loads on first use)
+
+_lphy.FUSED_MIN_FRAMES = 0
 
 
 def pytest_configure(config):

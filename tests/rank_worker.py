@@ -28,9 +28,9 @@ SF, PLEN = 7, 8
 SPF = 2 * PLEN
 
 
-def frame_results(o, iq):
+def frame_results(o, iq, sf=SF):
     """Oracle stand-in for one frame: symbols, payload, frame record."""
-    r, syms, sync, met = o.lora_demodulate(o.dechirp(iq, SF), SF)
+    r, syms, sync, met = o.lora_demodulate(o.dechirp(iq, sf), sf)
     rec = np.zeros(1, lphy.META_DTYPE)
     rec["cfo"], rec["time_offset"], rec["sync_word"] = met[0], met[1], sync
     rec["have_sync"] = 1
@@ -76,5 +76,57 @@ def main(out_path: str, total: int) -> None:
         dist.destroy_process_group()
 
 
+def main_c3(out_path: str, total: int) -> None:
+    """bench.py run_c3's N > 1 path: the seeded mixed-SF stream
+    (shard.mixed_plan, SF 7-9 here to keep the oracle quick) cut into
+    cost-balanced contiguous ranges, each rank's frames bucketed by SF, one
+    slab per rank with a [symbols | payloads | records] part per bucket,
+    padded to the largest rank's layout (shard.mixed_slab_bytes), ONE gather
+    to rank 0, which puts every rank's buckets back in stream order
+    (shard.gather_mixed) and checks each frame against the oracle run on the
+    whole stream."""
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    kw = dict(sf_lo=7, sf_hi=9)
+    try:
+        o = Oracle()
+        first, count, sfs, pays, plan = shard.mixed_plan(total, world, rank, payload=PLEN, **kw)
+        order = sorted(plan)
+        cap = shard.mixed_slab_bytes(total, world, SPF, PLEN, **kw)
+        slab = shard.ResultSlab([plan[sf].size for sf in order], SPF, PLEN, torch.device("cpu"), cap)
+        for i, sf in enumerate(order):
+            sv, pv, mv = slab.views(i)
+            for j, fi in enumerate(plan[sf]):
+                iq = o.modulate(o.encode(pays[fi].tobytes()), sf)
+                s, p, m = frame_results(o, iq, sf)
+                sv[j * SPF:(j + 1) * SPF] = torch.from_numpy(s.view(np.int16).copy())
+                pv[j * PLEN:(j + 1) * PLEN] = torch.from_numpy(p.copy())
+                mv[j * 32:(j + 1) * 32] = torch.from_numpy(m.copy())
+        parts, work = shard.gather_slab(slab.buf, async_op=True)
+        work.wait()
+        if rank == 0:
+            gs, gp, gm = shard.gather_mixed(parts, total, world, SPF, PLEN, **kw)
+            _, _, all_sfs, all_pays, _ = shard.mixed_plan(total, 1, 0, payload=PLEN, **kw)
+            ok, bad = 0, []
+            for f in range(total):
+                iq = o.modulate(o.encode(all_pays[f].tobytes()), int(all_sfs[f]))
+                s, p, m = frame_results(o, iq, int(all_sfs[f]))
+                if (np.array_equal(gs[f], s) and np.array_equal(gp[f], p) and np.array_equal(gp[f], all_pays[f])
+                        and np.array_equal(gm[f], m)):
+                    ok += 1
+                else:
+                    bad.append(f)
+            counts = [shard.mixed_plan(total, world, r, payload=PLEN, **kw)[1] for r in range(world)]
+            buckets = [len(shard.mixed_plan(total, world, r, payload=PLEN, **kw)[4]) for r in range(world)]
+            Path(out_path).write_text(json.dumps({"world": world, "frames": total, "ok": ok, "bad": bad,
+                                                  "counts": counts, "buckets": buckets,
+                                                  "all_ok": ok == total and not bad}))
+    finally:
+        dist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]))
+    if len(sys.argv) > 3 and sys.argv[3] == "c3":
+        main_c3(sys.argv[1], int(sys.argv[2]))
+    else:
+        main(sys.argv[1], int(sys.argv[2]))

@@ -76,3 +76,100 @@ def test_near_ties_straddling_the_certificate(oracle, lphy, sf, nf, mode, hann):
     # the sweep reaches margins far below the bound: some symbols must have
     # gone to the exact re-run, and far above it: not all of them
     assert 0 < n_exact < nf * 66, f"{n_exact} exact re-runs of {nf * 66} symbols"
+
+
+def _const_ratio_frame(oracle, sf, ratio, seed, data_gain=1.0):
+    """One frame whose every data symbol is two tones (a, b) with amplitude
+    ratio `ratio` (b larger on odd symbols, smaller on even ones), under a
+    small CFO and delay; the data symbols scaled by `data_gain` against the
+    sync symbols (data_gain < 1: weak symbols after the frame's max-abs
+    normalisation, whose f16 components reach the subnormal range)."""
+    rng = np.random.default_rng(seed)
+    N = 1 << sf
+    S = 64
+    a = rng.integers(0, N, S).astype(np.uint16)
+    b = ((a.astype(np.int64) + rng.integers(2, N - 1, S)) % N).astype(np.uint16)
+    xa = oracle.modulate(a, sf).astype(np.complex128)
+    xb = oracle.modulate(b, sf).astype(np.complex128)
+    g = np.ones(xa.size)
+    for s in range(S):
+        g[(s + 2) * N:(s + 3) * N] = ratio if s % 2 else 1.0 / ratio
+    x = xa + xb * g
+    x[2 * N:] *= data_gain
+    t = np.arange(x.size)
+    x = x * np.exp(2j * np.pi * rng.uniform(-0.2, 0.2) / N * t)
+    x = np.roll(x, int(rng.integers(-N // 8, N // 8 + 1)))
+    return x.astype(np.complex64)
+
+
+@pytest.mark.parametrize("sf", [7, 8])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_matrix_core_threshold_straddled(oracle, lphy, sf, mode):
+    """SF 7-8 modes 1/2 (the C1 bench path): k_frames' symbol tiles run the
+    transform in f16 on the matrix cores (lphy_mfma.h) and the certificate
+    charges kMfmaExtra = 3 * 2^14 u of A for it, a lead of ~3.3 % of |X| for
+    these two-tone symbols.  One frame per call, every
+    data symbol of a frame at the same amplitude ratio r, r - 1 swept
+    geometrically from 2^-11 to 2^-1: frames well below the threshold must
+    re-run every data symbol exactly, frames above it certify every one, and
+    near-tie symbols (r - 1 < 1/4) are counted on both sides of it.  Every
+    output bit equals the oracle's."""
+    N = 1 << sf
+    ks = 2.0 ** np.linspace(-11, -1, 31)
+    d = lphy.Demodulator(sf)
+    rows = []
+    for i, k in enumerate(ks):
+        x = _const_ratio_frame(oracle, sf, 1.0 + k, seed=4000 + 97 * sf + 11 * mode + i)
+        if mode == 1:  # lora_demodulate takes dechirped samples
+            x = oracle.dechirp(x, sf)
+        d.recheck_count(reset=True)
+        syms, _, meta = d.demod_host(x[None, :], 1, x.size, mode, lphy.F_DECODE)
+        n_exact = d.recheck_count(reset=True)
+        src = x if mode == 1 else oracle.dechirp(x, sf)
+        r, osyms, osync, omet = oracle.lora_demodulate(src, sf)
+        ctx = f"sf {sf} mode {mode} r-1 {k:.3g}"
+        assert meta["status"][0] == 0, ctx
+        np.testing.assert_array_equal(syms[0], osyms, err_msg=ctx)
+        assert meta["sync_word"][0] == osync, ctx
+        assert _bits(meta["cfo"][0]) == _bits(omet[0]), ctx
+        assert _bits(meta["time_offset"][0]) == _bits(omet[1]), ctx
+        assert 0 <= n_exact <= 64, ctx
+        rows.append((k, n_exact))
+    near = [(k, n) for k, n in rows if k < 0.25]
+    certified = sum(64 - n for _, n in near)
+    rerun = sum(n for _, n in near)
+    assert certified > 0 and rerun > 0, rows
+    # below the threshold every symbol is re-run, above it none: the largest
+    # ratio with a re-run lies below the smallest with none re-run... and the
+    # switch happens inside the near-tie band, at a few per cent
+    all_rerun = [k for k, n in rows if n == 64]
+    none_rerun = [k for k, n in rows if n == 0]
+    assert all_rerun and none_rerun, rows
+    assert max(all_rerun) < min(none_rerun) < 0.25, rows
+    assert 0.005 < max(all_rerun), rows
+
+
+@pytest.mark.parametrize("sf", [7, 8])
+def test_matrix_core_weak_symbols(oracle, lphy, sf):
+    """Weak data symbols under loud sync symbols: after the
+    frame's normalisation their f16 components are small or subnormal.  The
+    certificate bounds the f16 error against A with amax = 1, the
+    normalisation's bound, not the symbol's own amplitude, so an absolute
+    f16 error of up to 2^-14 per component (flush to zero included) stays
+    inside kMfmaExtra's slack; a weak near-tie is re-run.  Every output bit
+    equals the oracle's across data gains 2^-2 .. 2^-16."""
+    d = lphy.Demodulator(sf)
+    counts = []
+    for i, gexp in enumerate([2, 4, 6, 8, 12, 16]):
+        x = _const_ratio_frame(oracle, sf, 1.3, seed=5000 + sf + i, data_gain=2.0 ** -gexp)
+        d.recheck_count(reset=True)
+        syms, _, meta = d.demod_host(x[None, :], 1, x.size, 2, lphy.F_DECODE)
+        counts.append(d.recheck_count(reset=True))
+        r, osyms, osync, omet = oracle.lora_demodulate(oracle.dechirp(x, sf), sf)
+        ctx = f"sf {sf} gain 2^-{gexp}"
+        assert meta["status"][0] == 0, ctx
+        np.testing.assert_array_equal(syms[0], osyms, err_msg=ctx)
+        assert _bits(meta["cfo"][0]) == _bits(omet[0]), ctx
+        assert _bits(meta["time_offset"][0]) == _bits(omet[1]), ctx
+    # loud data certify, the weakest re-run every symbol
+    assert counts[0] < 64 and counts[-1] == 64, counts

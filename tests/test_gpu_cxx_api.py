@@ -19,12 +19,26 @@ REF_PROBE = ROOT / "oracle" / "_ref" / "lora_phy_api_probe_ref"
 
 
 def prod_env(**kw):
-    """The probes run the drop-in with the library's own launch choices (the
-    suite's conftest forces the fused kernels for small batches; a packet
-    at a time takes the separate launches by default, fused_min_frames)."""
-    env = {k: v for k, v in os.environ.items() if k != "LPHY_FUSED_MIN_FRAMES"}
+    """The probes run the drop-in with the library's own launch choices (a
+    packet at a time takes the separate launches by default,
+    fused_min_frames)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("LPHY_FUSED_MIN_FRAMES", "LD_LIBRARY_PATH")}
     env.update(kw)
     return env
+
+
+def fused_env():
+    """The same drop-in with every call on the fused kernels: the test build
+    of liblphy_hip.so (lib/test/, found first through LD_LIBRARY_PATH by
+    liblora_phy_amd.so) reads LPHY_FUSED_MIN_FRAMES; the product library
+    takes no launch choice from the environment."""
+    return prod_env(LD_LIBRARY_PATH=str(PKG / "lib" / "test"), LPHY_FUSED_MIN_FRAMES="0")
+
+
+def loaded_hip_lib(exe, env) -> str:
+    """The liblphy_hip.so the dynamic loader picks for `exe` under `env`."""
+    out = subprocess.run(["ldd", str(exe)], capture_output=True, text=True, env=env, check=True).stdout
+    return next(l.split("=>")[1].split("(")[0].strip() for l in out.splitlines() if "liblphy_hip.so" in l)
 
 
 def test_cxx_api_transcript_matches_reference(tmp_path):
@@ -39,7 +53,9 @@ def test_cxx_api_transcript_matches_reference(tmp_path):
     assert ref.returncode == 0, ref.stderr
     b = ref.stdout.splitlines()
     # default launch choices, then the fused kernels forced for every call
-    for env in (prod_env(), prod_env(LPHY_FUSED_MIN_FRAMES="0")):
+    assert loaded_hip_lib(exe, prod_env()) == str(PKG / "lib" / "liblphy_hip.so")
+    assert loaded_hip_lib(exe, fused_env()) == str(PKG / "lib" / "test" / "liblphy_hip.so")
+    for env in (prod_env(), fused_env()):
         ours = subprocess.run([str(exe), golden], capture_output=True, text=True, timeout=300, env=env)
         assert ours.returncode == 0, ours.stderr
         a = ours.stdout.splitlines()

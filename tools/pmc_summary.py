@@ -8,6 +8,7 @@ import csv
 import json
 import re
 import sys
+import time
 from collections import defaultdict
 from pathlib import Path
 
@@ -32,7 +33,10 @@ def main():
     d, tag, frames, sf = Path(sys.argv[1]), sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
     acc, n = load(d)
     mode = int(sys.argv[6]) if len(sys.argv) > 6 else 2
-    out = {"tag": tag, "frames": frames, "sf": sf, "mode": mode, "source": str(d), "kernels": {}}
+    # "written": bench.py's measured_traffic takes the newest summary of a
+    # configuration by this stamp
+    out = {"tag": tag, "frames": frames, "sf": sf, "mode": mode, "source": str(d),
+           "written": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()), "kernels": {}}
     for k, c in acc.items():
         if not k.startswith("k_"):
             continue
