@@ -711,6 +711,19 @@ int lphy_hip_recheck_count(lphy_hip_ctx* c, unsigned long long* out, int reset) 
     return 0;
 }
 
+#ifdef LPHY_TEST_PATHS
+// Test build only (csrc/lphy_testing.h): the context's device counter `idx`
+// (1: symbols the wave kernels certified by Parseval).  Synchronises.
+int lphy_hip_test_counter(lphy_hip_ctx* c, int idx, unsigned long long* out, int reset) {
+    if (!c || !out || idx < 0 || idx > 8) return -EINVAL;
+    HIP_OK(hipSetDevice(c->device));
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(out, c->d_counters + idx, sizeof(*out), hipMemcpyDeviceToHost));
+    if (reset) HIP_OK(hipMemset(c->d_counters + idx, 0, sizeof(*out)));
+    return 0;
+}
+#endif
+
 int lphy_hip_bounds_violations(lphy_hip_ctx* c, unsigned long long* out, int reset) {
     if (!c || !out) return -EINVAL;
 #ifdef LPHY_DEBUG_BOUNDS

@@ -2873,6 +2873,9 @@ bool use_wave2s(const DemodArgs& A) {
         return false;
     } else {
         if (A.total_syms < (unsigned long long)WGeo<SF>::SPW) return false;  // k_wave2s's precondition
+#ifdef LPHY_AB_WAVE_V1  // A/B timing builds only (tools/ubench/variants.py)
+        return false;
+#endif
         const int forced = lphy_test_wave_kind();  // -1 in the product build
         if (forced >= 0) return forced == 2;
         return SF == 9;

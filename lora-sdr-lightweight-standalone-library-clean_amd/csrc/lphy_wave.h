@@ -653,18 +653,209 @@ __device__ __forceinline__ UnitResult wunit_result(const cf32 (&v)[64], int h, i
     return r;
 }
 
+// ---------------------------------------------------------------------------
+// Parseval certificate (round 5): a symbol unit proven without its FFT.
+//
+// The fast path above transforms every symbol and certifies the winner
+// against the runner-up.  A clean symbol - one tone after the dechirp and the
+// rotation - carries nearly all of its energy in one bin, and then the winner
+// can be proven from that one bin alone: by Parseval, sum_j |Y_j|^2 =
+// N sum_n |y_n|^2 = N E for the exact DFT Y of the staged samples y, so every
+// other bin obeys |Y_j| <= sqrt(N E - |Y_k|^2).  With B the certificate's
+// bound on | |X_ref_j| - |Y_j| | (the rotation's and KISS's roundings, as
+// cert_bound charges them; our own FFT's roundings are not incurred here),
+// KISS's argmax is k once
+//     |Y_k| - sqrt(N E - |Y_k|^2) > 2 B
+// (strict: k beats every other bin, so the detector's first-maximum rule,
+// LoRaDetector.hpp:46-58, picks it); the kernels ask for 4 B like the
+// runner-up certificate.  Per half (symbol) of a unit:
+//   * a candidate k: the lag-1 autocorrelation across lanes (DPP row_shl:1,
+//     samples 0 .. 8 LPS - 1) gives k coarsely, the lag-LPS one inside each
+//     lane (samples i, i + LPS: arg = 2 pi k / 64) gives k mod 64; a wrong
+//     candidate only fails the test;
+//   * Y_k = sum_l W^{k l} sum_a W_8^{k a} sum_b y[l + LPS (8 a + b)] W_64^{k b}
+//     (W_64 / W_8 powers: the correctly rounded 64th roots, read from a
+//     register table by ds_bpermute; W^{k l}: the KISS table entry), and E,
+//     both with per-lane partial sums and a tree over the symbol's lanes;
+//   * the samples are taken before the frame's rotation, which is folded
+//     into the twiddles (pv_lane_sums): the staging then skips the two
+//     rotation products per sample, and only a failed unit applies them;
+//   * |dY_k| <= kPvErr u A (A = N sqrt2 amax >= sum |y_n|): the folded
+//     twiddle products (<= 3 u each, two), fused products and 8-term partial
+//     sums (<= 16 u each, two stages), the KISS entry (<= 7.3 u) and its
+//     product (3 u), the tree (<= 6 u): < 58 u; E's relative error (8-term
+//     partial sums, the tree, scale^2) < 26 u (charged 32 u);
+//   * lead = Ylo - sqrt(max(0, N E (1 + 32 u) - Ylo^2)) (1 + 4 u) with
+//     Ylo = sqrt(|Y_k|^2) (1 - 4 u) - kPvErr u A (v_sqrt within 2 u, the
+//     square's rounding within 2 u), certified when lead > 4 B.
+// A unit whose every live symbol passes skips pass 1, the exchange, pass 2
+// and the top two (~3x fewer VALU instructions at SF 12); otherwise it runs
+// them as before.  After a failed unit the frame's remaining units go
+// straight to the transform (noisy frames pay one attempt per frame).  The
+// speculative normalisation's lead ratio of a Parseval-certified symbol is
+// lead / B: a lower bound of the exact winner's lead over every other bin,
+// as the runner-up certificate's is.
+// ---------------------------------------------------------------------------
+constexpr float kPvErr = 64.0f;
+
+// Test build: symbols certified by Parseval, summed in counters[1]
+// (lphy_hip_test_counter; tests/test_gpu_parseval.py).
+__device__ __forceinline__ void pv_count(const DemodArgs& A, bool mine) {
+#ifdef LPHY_TEST_PATHS
+    const unsigned long long m = __ballot(mine);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&A.counters[1], (unsigned long long)__popcll(m));
+#else
+    (void)A;
+    (void)mine;
+#endif
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+// Sum over the LPS lanes of each symbol (every lane gets its symbol's sum).
+template <int LPS>
+__device__ __forceinline__ float half_sum(float x) {
+    static_assert(LPS == 8 || LPS == 16 || LPS == 32 || LPS == 64, "8 to 64 lanes per symbol");
+    x = x + dpp_f32<0xB1>(x);   // quad_perm [1,0,3,2]
+    x = x + dpp_f32<0x4E>(x);   // quad_perm [2,3,0,1]
+    x = x + dpp_f32<0x141>(x);  // row_half_mirror: the 8-lane sum
+    if constexpr (LPS >= 16) x = x + dpp_f32<0x140>(x);  // row_mirror: 16
+    if constexpr (LPS >= 32) x = x + __shfl_xor(x, 16, 64);
+    if constexpr (LPS >= 64) x = x + __shfl_xor(x, 32, 64);
+    return x;
+}
+// root64(idx) for a per-lane idx from the register table rr = root64(lane)
+__device__ __forceinline__ cf32 pv_root(cf32 rr, int idx) {
+    return cf32{__int_as_float(__builtin_amdgcn_ds_bpermute((idx & 63) << 2, __float_as_int(rr.x))),
+                __int_as_float(__builtin_amdgcn_ds_bpermute((idx & 63) << 2, __float_as_int(rr.y)))};
+}
+// acc + y * w (complex), two fused packed ops
+__device__ __forceinline__ cf32 cmac(cf32 acc, cf32 y, cf32 w) {
+    cf32 t, r;
+    // t = (acc.x + y.x w.x, acc.y + y.x w.y)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(t) : "v"(y), "v"(w), "v"(acc));
+    // r = (t.x - y.y w.y, t.y + y.y w.x)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r) : "v"(y), "v"(w), "v"(t));
+    return r;
+}
+
+// acc + (y.x^2, y.y^2), one packed fma
+__device__ __forceinline__ cf32 pk_fma_sq(cf32 acc, cf32 y) {
+    cf32 r;
+    asm("v_pk_fma_f32 %0, %1, %1, %2" : "=v"(r) : "v"(y), "v"(acc));
+    return r;
+}
+
+// The candidate bin of each symbol of the unit (every lane of the symbol
+// gets it).  v[e]: sample l + LPS e of the lane's symbol before the frame's
+// rotation e^{j rate i} (which shifts every lag-d autocorrelation's phase by
+// rate d).
+template <int SF>
+__device__ __forceinline__ int pv_candidate(const cf32 (&v)[64], int l, float rate) {
+    constexpr int N = 1 << SF, LPS = WGeo<SF>::LPS;
+    constexpr float kInv2Pi = 0.159154943f;
+    // lag 1: sample i + 1 sits in lane l + 1 of the same row (DPP row_shl:1;
+    // a row's last lane, and a symbol's last lane, have no partner)
+    float zr = 0.0f, zi = 0.0f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float nx = dpp_f32<0x101>(v[e].x), ny = dpp_f32<0x101>(v[e].y);
+        zr = fmaf(v[e].x, nx, zr);
+        zr = fmaf(v[e].y, ny, zr);
+        zi = fmaf(v[e].x, ny, zi);
+        zi = fmaf(-v[e].y, nx, zi);
+    }
+    if ((l & 15) == 15 || (l % LPS) == LPS - 1) zr = zi = 0.0f;
+    // lag LPS inside the lane: arg = 2 pi k / 64
+    float wr = 0.0f, wi = 0.0f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        wr = fmaf(v[e].x, v[e + 1].x, wr);
+        wr = fmaf(v[e].y, v[e + 1].y, wr);
+        wi = fmaf(v[e].x, v[e + 1].y, wi);
+        wi = fmaf(-v[e].y, v[e + 1].x, wi);
+    }
+    zr = half_sum<LPS>(zr);
+    zi = half_sum<LPS>(zi);
+    wr = half_sum<LPS>(wr);
+    wi = half_sum<LPS>(wi);
+    const int kc = (int)rintf((atan2f(zi, zr) + rate) * (kInv2Pi * (float)N));
+    const int k64 = (int)rintf((atan2f(wi, wr) + rate * (float)LPS) * (kInv2Pi * 64.0f));
+    int d = (k64 - kc) & 63;
+    d = d >= 32 ? d - 64 : d;
+    return (kc + d) & (N - 1);
+}
+
+// The lane's share of Y_k before its factor W^{k l} (the caller applies it:
+// the table entry's load is issued early) and the lane's share of sum |p|^2.
+// v[e] = p: the sample before the rotation, which is folded into the
+// twiddles: y_i W^{k i} = p_i (Qr[b] W_64^{k b}) (Pr[a] W_8^{k a}) W^{k l}
+// for i = l + LPS (8 a + b) (Qr carries the normalisation's scale; the
+// caller multiplies E by scale^2).
+template <int SF>
+__device__ __forceinline__ void pv_lane_sums(const cf32 (&v)[64], int k, cf32 rr, const cf32 (&Qr)[8],
+                                             const cf32 (&Pr)[8], cf32& yk, float& e) {
+    cf32 q[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) q[b] = b == 0 ? Qr[0] : cmul_fma(pv_root(rr, k * b), Qr[b]);
+    cf32 acc = czero();
+    cf32 e2 = czero();  // (sum re^2, sum im^2), 8-term partial sums
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+        cf32 in = cmul_fma(v[8 * a], q[0]);
+        cf32 ep = v[8 * a] * v[8 * a];
+#pragma unroll
+        for (int b = 1; b < 8; ++b) {
+            in = cmac(in, v[8 * a + b], q[b]);
+            ep = pk_fma_sq(ep, v[8 * a + b]);
+        }
+        e2 = e2 + ep;
+        const cf32 t = a == 0 ? Pr[0] : cmul_fma(pv_root(rr, 8 * k * a), Pr[a]);
+        acc = a == 0 ? cmul_fma(in, t) : cmac(acc, in, t);
+    }
+    yk = acc;
+    e = e2.x + e2.y;
+}
+
+// The certificate's lead of a symbol from its lanes' shares (summed here).
+template <int SF>
+__device__ __forceinline__ float pv_lead(cf32 yk, float e, float scale2, float am) {
+    constexpr int N = 1 << SF, LPS = WGeo<SF>::LPS;
+    const float yr = half_sum<LPS>(yk.x), yi = half_sum<LPS>(yk.y);
+    const float E = half_sum<LPS>(e) * scale2;  // sum |y|^2 = scale^2 sum |p|^2
+    const float A = (float)N * 1.41421366f * am * 1.0001f;
+    const float y2 = __builtin_fmaf(yr, yr, yi * yi);
+    const float ylo = __builtin_amdgcn_sqrtf(y2) * (1.0f - 4.0f * kU) - kPvErr * kU * A;
+    const float rest = fmaxf(0.0f, (float)N * E * (1.0f + 32.0f * kU) - ylo * ylo * (1.0f - 4.0f * kU));
+    const float lead = ylo - __builtin_amdgcn_sqrtf(rest) * (1.0f + 4.0f * kU);
+    // finite, normal and in range (a NaN fails every comparison)
+    return (y2 >= 1e-30f && y2 < 1e30f && E < 1e30f && ylo > 0.0f) ? lead : -1.0f;
+}
+
 // The rare parts of k_wave live in functions of their own (not inlined):
 // their registers then never compete with the symbol units' 64-value
 // transform, and the few calls per frame cost a spill of the loop state.
 
-// An estimate unit from the wave's buffer (symbol h of the pair at SF 11):
-// KISS's exact transform and the detector outputs; .nan when a bin is NaN
-// (the frame then goes to the exact re-run, as in k_frames).
+// An estimate unit from the wave's buffer (SF 12: one estimate symbol; SF
+// 9-11: symbols 0 and 1 in halves 0 and 1): KISS's exact transform and the
+// detector outputs; .nan when a bin is NaN (the frame then goes to the exact
+// re-run, as in k_frames).  Modes 1/2 normalise with the max-abs `mx`, or
+// with find_mx (SF 9-11, both estimate symbols in the unit) with the two
+// estimate symbols' max-abs folded here from the unit's own samples, as the
+// reference's normalisation scans them (LoRaDemod.cpp:60-78; NaN when one is
+// not finite, as wscan2 returns): the frame's blocking two-symbol scan is
+// then not needed.  Returns the max-abs used.
+struct WEstU {
+    UnitResult ur;
+    float mx;
+};
 template <int SF, int MODE>
-__device__ __noinline__ UnitResult west_unit(KArgs ka, lds_cf32* lbuf, const lds_cf32* ldnl, float scale,
-                                             bool live) {
+__device__ __noinline__ WEstU west_unit(KArgs ka, lds_cf32* lbuf, const lds_cf32* ldnl, float mx, bool find_mx) {
     using W = WGeo<SF>;
-    constexpr int N = W::N, LPS = W::LPS;
+    constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
     constexpr bool M0 = (MODE & 3) == LPHY_MODE_DEMODULATE;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     const DemodArgs& A = kargs(ka);
@@ -678,7 +869,33 @@ __device__ __noinline__ UnitResult west_unit(KArgs ka, lds_cf32* lbuf, const lds
         if ((e & 7) == 0) cfence();
         cf32 x = lds_ld(buf, rb + ((LPS * e) << 3));
         if constexpr (DECH) x = cmul(x, dnl[l + LPS * e]);
-        if constexpr (!M0) x = cscale(x, scale);
+        v[e] = x;
+    }
+    if constexpr (!M0 && SPW > 1) {
+        if (find_mx) {
+            float fm = 0.0f;
+            cf32 sum = czero();
+            if (h < 2) {
+#pragma unroll
+                for (int e = 0; e < 64; ++e) {
+                    fm = max3_abs(fm, v[e].x, v[e].y);
+                    sum = sum + v[e];
+                }
+            }
+            const bool bad = !(sum.x == sum.x && sum.y == sum.y) || !(fm <= 3.40282347e38f);
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) fm = fmaxf(fm, __shfl_xor(fm, off, 64));
+            mx = __ballot(bad) ? __builtin_nanf("") : fm;
+        }
+    }
+    lphy_frame_meta nm{};
+    nm.scale = 1.0f;
+    if constexpr (!M0) nm = norm_meta_hot(mx, true, A.no_scratch);
+    const bool live = nm.status == 0;
+#pragma unroll
+    for (int e = 0; e < 64; ++e) {
+        cf32 x = v[e];
+        if constexpr (!M0) x = cscale(x, nm.scale);
         v[e] = live ? x : czero();
     }
     const WTw<SF> T{};  // unused by the exact pass
@@ -697,10 +914,12 @@ __device__ __noinline__ UnitResult west_unit(KArgs ka, lds_cf32* lbuf, const lds
         sumsq += sq.x + sq.y;
     }
     const unsigned long long nb = __ballot(!(sumsq == sumsq));
-    UnitResult ur = wunit_result<SF>(v, h, l, lane);
-    ur.nan = (LPS == 64 ? nb : ((nb >> (LPS * h)) & ((1ull << (LPS & 63)) - 1))) != 0 ? 1 : 0;
-    if (!live) ur = UnitResult{0, 0, 0.0f, 0.0f, 0};
-    return ur;
+    WEstU r;
+    r.ur = wunit_result<SF>(v, h, l, lane);
+    r.ur.nan = (LPS == 64 ? nb : ((nb >> (LPS * h)) & ((1ull << (LPS & 63)) - 1))) != 0 ? 1 : 0;
+    if (!live) r.ur = UnitResult{0, 0, 0.0f, 0.0f, 0};
+    r.mx = mx;
+    return r;
 }
 
 // The frame's rotation tables: q[b] = [scale] e^{j rate (l + LPS b)} for the
@@ -771,7 +990,7 @@ __device__ __noinline__ void wclose(KArgs ka, lds_cf32* lbuf, const lds_cf32* ld
     for (int j = 0; j < W::NE; ++j) {
         wdma<SF>(A, buf, WDma{f, (unsigned)j, 0, 1, 1}, lane);
         wait_vm0();
-        const UnitResult ur = west_unit<SF, MODE>(ka, lbuf, ldnl, me.scale, true);
+        const UnitResult ur = west_unit<SF, MODE>(ka, lbuf, ldnl, mt, false).ur;
         if constexpr (SPW == 1) {
             if (j == 0) ua = ur;
             else ub = ur;
@@ -939,6 +1158,10 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     // per lane, Pr[a] = e^{j rate 8 LPS a} wave-uniform (sample i = l + LPS (8a + b))
     cf32 Qr[8], Pr[8];
     unsigned rot_frame = 0xffffffffu;
+    // Parseval certificate: the 64th roots as a register table (lane j holds
+    // root64(j)); tried while no unit of the frame has failed it
+    const cf32 rr = root64(lane);
+    bool pv_on = true;
     // speculative normalisation of the frame in demodulation (lane state)
     constexpr float kBig = 3.0e38f;
     float sp_mx = 0.0f, sp_r = kBig;
@@ -947,7 +1170,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
 
     WCursor cu = sch.first();
     WPH_DECL
-    if constexpr (!M0) {
+    if constexpr (!M0 && SPW == 1) {  // (SF 9-11: the estimate unit scans its own samples)
         const float m = wscan2<SF, MODE>(ka, fglob(0), dnl, lane);
         WFrame r = rec0;
         r.mx = m;
@@ -967,6 +1190,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             const WFrame R = rec(k);
             if (k != rot_frame) {
                 rot_frame = k;
+                pv_on = true;
                 const WRot rt = wrot<SF, MODE>(R.rate, R.scale);
 #pragma unroll
                 for (int b = 0; b < 8; ++b) Qr[b] = rt.q[b];
@@ -1026,54 +1250,13 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                     amax = max3_abs(amax, p.x, p.y);
                     if constexpr (M0) p = cmul(p, dq[q % SB][i]);
                     // (a unit whose symbol is not demodulated transforms whatever
-                    // its window holds; nothing of it is stored)
-                    v[e] = cmul_fma(cmul_fma(p, Qr[i]), Pr[q]);
+                    // its window holds; nothing of it is stored; the rotation
+                    // is applied below, or folded into the Parseval sums)
+                    v[e] = p;
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
             WPH(1);
-            wpass1<SF, true>(v, ctw(A.tw));
-            WPH(2);
-#ifndef LPHY_ABLATE_W_EXCH  // timing experiments only
-            wexchange<SF>(v, buf, h, l);
-#endif
-#ifdef LPHY_W_LATE_DMA
-            // pass 2's first stage consumes the exchange reads as they land;
-            // then the buffer is free for the next unit's IQ
-            wpass2_s2<SF, true>(v, T, A.tw, l);
-            wait_lgkm0();
-            dma_unit(nx);
-            WPH(3);
-            wpass2_s10<SF, true>(v, T, A.tw, l);
-#else
-            wait_lgkm0();  // the exchange reads are done: the buffer is free
-#ifndef LPHY_ABLATE_W_DMA  // timing experiments only
-            dma_unit(nx);  // the next unit's IQ lands during pass 2
-#endif
-            WPH(3);
-            wpass2<SF, true>(v, T, A.tw, l);
-#endif
-            WPH(4);
-            // keyed top two over the half's bins l + LPS e (key: |X|^2 bits,
-            // low 6 bits the element; see team_argmax2_keyed_first)
-            unsigned k1 = 0u, k2 = 0u;
-#pragma unroll
-            for (int e = 0; e < 64; e += 2) {
-                // |X|^2 = fma(x, x, fl(y y)): within 2 u, inside cert_gap's 8 u;
-                // scalar f32 ops (no packed-f32 dependency pad)
-                const float ma = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
-                const float mb = __builtin_fmaf(v[e + 1].x, v[e + 1].x, v[e + 1].y * v[e + 1].y);
-                top2_pair(k1, k2, (__float_as_uint(ma) & ~63u) | (unsigned)e,
-                          (__float_as_uint(mb) & ~63u) | (unsigned)(e + 1));
-            }
-            unsigned K1, K2;
-            wave_top2_merge<LPS>(k1, k2, h, K1, K2);
-            const unsigned long long bm = __ballot(k1 == K1);
-            const unsigned long long hm = LPS == 64 ? bm : ((bm >> (LPS * h)) & ((1ull << (LPS & 63)) - 1));
-            ArgMax2 b2;
-            b2.v = __uint_as_float(K1 & ~63u);
-            b2.v2 = __uint_as_float(K2 | 63u);
-            b2.i = (__ffsll((long long)hm) - 1) + LPS * (int)(K1 & 63u);
             float am = 1.0f;  // modes 1/2: normalised frame (see fast_certified)
             if constexpr (M0) {
 #pragma unroll
@@ -1081,12 +1264,88 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                 am = amax;
             }
             const float cb1 = cert_bound<SF>(c.rate, c.start, 1.0f, kWaveExtra);
-            const float cgap = cert_gap(b2);
-            const bool cert = cgap > 4.0f * (cb1 * am) && (float)N * 1.41421366f * am * 1.0001f < 1e18f &&
-                              am >= 1e-20f && b2.v >= 1e-30f;
-            const bool redo = c.ok && (!cert || A.debug_recheck);  // (DEBUG_RECHECK: tests)
+            int sym = 0;         // the symbol's bin (certified) ...
+            float cgap = -1.0f;  // ... and its certified lead (-1: not certified)
+            bool pv = false;     // the whole unit certified by Parseval
+            if (pv_on && !A.debug_recheck) {
+                // Parseval certificate (above): the candidate, its DFT bin
+                // and the energy; the buffer is free after the staging, so
+                // the next unit's IQ is on its way meanwhile
+                const int kc = pv_candidate<SF>(v, l, c.rate);
+                const cf32 wkl = A.tw[(unsigned)(kc * l) & (unsigned)(N - 1)];
+                wait_lgkm0();
+                dma_unit(nx);
+                cf32 ykl;
+                float el;
+                pv_lane_sums<SF>(v, kc, rr, Qr, Pr, ykl, el);
+                const float lead = pv_lead<SF>(cmul_fma(ykl, wkl), el, M0 ? 1.0f : c.scale * c.scale, am);
+                const bool ok = lead > 4.0f * (cb1 * am) && (float)N * 1.41421366f * am * 1.0001f < 1e18f &&
+                                am >= 1e-20f;
+                pv = __ballot(live && c.ok && !ok) == 0;
+                if (pv) {
+                    pv_count(A, live && c.ok && l == 0);
+                    sym = kc;
+                    cgap = lead;
+                } else {
+                    pv_on = false;  // the frame's other units: the transform
+                    wait_vm0();     // the early DMA has landed before the exchange reuses the buffer
+                }
+            }
+            WPH(2);
+            if (!pv) {
+                // the certified rotation (staging left the samples unrotated)
+#pragma unroll
+                for (int e = 0; e < 64; ++e) v[e] = cmul_fma(cmul_fma(v[e], Qr[e & 7]), Pr[e >> 3]);
+                wpass1<SF, true>(v, ctw(A.tw));
+#ifndef LPHY_ABLATE_W_EXCH  // timing experiments only
+                wexchange<SF>(v, buf, h, l);
+#endif
+#ifdef LPHY_W_LATE_DMA
+                // pass 2's first stage consumes the exchange reads as they land;
+                // then the buffer is free for the next unit's IQ
+                wpass2_s2<SF, true>(v, T, A.tw, l);
+                wait_lgkm0();
+                dma_unit(nx);
+                WPH(3);
+                wpass2_s10<SF, true>(v, T, A.tw, l);
+#else
+                wait_lgkm0();  // the exchange reads are done: the buffer is free
+#ifndef LPHY_ABLATE_W_DMA  // timing experiments only
+                dma_unit(nx);  // the next unit's IQ lands during pass 2
+#endif
+                WPH(3);
+                wpass2<SF, true>(v, T, A.tw, l);
+#endif
+                WPH(4);
+                // keyed top two over the half's bins l + LPS e (key: |X|^2 bits,
+                // low 6 bits the element; see team_argmax2_keyed_first)
+                unsigned k1 = 0u, k2 = 0u;
+#pragma unroll
+                for (int e = 0; e < 64; e += 2) {
+                    // |X|^2 = fma(x, x, fl(y y)): within 2 u, inside cert_gap's 8 u;
+                    // scalar f32 ops (no packed-f32 dependency pad)
+                    const float ma = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
+                    const float mb = __builtin_fmaf(v[e + 1].x, v[e + 1].x, v[e + 1].y * v[e + 1].y);
+                    top2_pair(k1, k2, (__float_as_uint(ma) & ~63u) | (unsigned)e,
+                              (__float_as_uint(mb) & ~63u) | (unsigned)(e + 1));
+                }
+                unsigned K1, K2;
+                wave_top2_merge<LPS>(k1, k2, h, K1, K2);
+                const unsigned long long bm = __ballot(k1 == K1);
+                const unsigned long long hm = LPS == 64 ? bm : ((bm >> (LPS * h)) & ((1ull << (LPS & 63)) - 1));
+                ArgMax2 b2;
+                b2.v = __uint_as_float(K1 & ~63u);
+                b2.v2 = __uint_as_float(K2 | 63u);
+                b2.i = (__ffsll((long long)hm) - 1) + LPS * (int)(K1 & 63u);
+                const float g = cert_gap(b2);
+                const bool cert = g > 4.0f * (cb1 * am) && (float)N * 1.41421366f * am * 1.0001f < 1e18f &&
+                                  am >= 1e-20f && b2.v >= 1e-30f;
+                sym = b2.i;
+                cgap = cert && !A.debug_recheck ? g : -1.0f;  // (DEBUG_RECHECK: tests)
+            }
+            const bool redo = c.ok && !(cgap >= 0.0f);
             if (live && l == 0) {
-                const uint16_t out = redo ? kSymRecheck : (uint16_t)b2.i;
+                const uint16_t out = redo ? kSymRecheck : (uint16_t)sym;
                 if (c.have_sync && c.s < 2) store_symbol(A, c, c.ok ? out : (uint16_t)0);
                 else if (c.ok) store_symbol(A, c, out);
                 if (redo) A.meta[c.f].status = kStatusRecheck;
@@ -1120,13 +1379,15 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
         } else {
             // estimate unit(s): KISS's arithmetic, bit for bit (LoRaDemod.cpp:80-136,
             // phy.cpp:81-148); SF 12 symbol j, SF 11 symbol h of the pair
-            const WFrame R0 = rec(k);
+            // (SF 9-11: the unit folds the two estimate symbols' max-abs itself)
+            WFrame R0 = rec(k);
+            const WEstU eu = west_unit<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, R0.mx, SPW > 1);
+            const UnitResult ur = eu.ur;
+            R0.mx = eu.mx;
             lphy_frame_meta nm{};
             nm.scale = 1.0f;
             nm.have_sync = 1;
             if constexpr (!M0) nm = norm_meta_hot(R0.mx, true, A.no_scratch);
-            const bool live = nm.status == 0;
-            const UnitResult ur = west_unit<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, nm.scale, live);
             bool fold_now = true;
             UnitResult ua = ur, ub = ur;
             if constexpr (SPW == 1) {
@@ -1172,7 +1433,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
         }
         // the two-symbol scan of the frame whose estimate comes next
         // (WPH slot 7 from here to the next unit: the scan and the cursor)
-        if constexpr (!M0) {
+        if constexpr (!M0 && SPW == 1) {
             if (sch.kind(nx) == kWEst && nx.j == 0 && nx.phase == 2) {
                 const unsigned kn = sch.frame(nx);
                 WFrame r = rec(kn);

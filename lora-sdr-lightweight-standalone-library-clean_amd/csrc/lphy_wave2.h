@@ -430,6 +430,8 @@ __global__ __launch_bounds__(512) void k_wave2s(FrameArgs P) {
 
     cf32 Qr[8], Pr[8];
     unsigned rot_k = 0xffffffffu;  // the lane's frame its tables are for
+    const cf32 rroot = root64(lane);  // Parseval certificate's register table
+    bool pv_on = true;
     // the lane's stream position for the next symbol unit: frame kh, symbol sh
     unsigned kh = 0, sh = (unsigned)h;
     unsigned est = 0;  // frames whose estimate is folded
@@ -498,6 +500,7 @@ __global__ __launch_bounds__(512) void k_wave2s(FrameArgs P) {
             }
         }
         if (__ballot(live && kh != rot_k)) {
+            pv_on = true;  // a new frame: try the Parseval certificate again
             const WRot rt = wrot_lane<SF, MODE>(R.rate, R.scale);
 #pragma unroll
             for (int b = 0; b < 8; ++b) Qr[b] = rt.q[b];
@@ -529,44 +532,10 @@ __global__ __launch_bounds__(512) void k_wave2s(FrameArgs P) {
                 if constexpr (DECH) p = cmul(p, dq[q & 1][i]);
                 amax = max3_abs(amax, p.x, p.y);
                 if constexpr (M0) p = cmul(p, dq[q & 1][i]);
-                v[e] = cmul_fma(cmul_fma(p, Qr[i]), Pr[q]);
+                v[e] = p;  // the rotation: below, or folded into the Parseval sums
             }
             __builtin_amdgcn_sched_barrier(0);
         }
-        wpass1<SF, true>(v, ctw(A.tw));
-        int hx = h, lx = l;
-        asm volatile("" : "+v"(hx), "+v"(lx));
-        WTw<SF> T;
-        T.load(A.tw, lx);
-        // (no exchange buffer at wbuf_acquire's cap: the unit's symbols go to
-        // the exact re-run, `lost`)
-        const int b = wbuf_acquire<L::NBUF>(locks, bstart, wlock_salt(A, u));
-        const bool lost = b < 0;
-        if (!lost) {
-            wexchange<SF>(v, (cf32*)(pool + b * W::BUF), hx, lx);
-            wait_lgkm0();
-            wbuf_release(locks, b);
-        } else {
-#pragma unroll
-            for (int e = 0; e < 64; ++e) v[e] = czero();
-        }
-        wpass2<SF, true>(v, T, A.tw, l);
-        unsigned k1 = 0u, k2 = 0u;
-#pragma unroll
-        for (int e = 0; e < 64; e += 2) {
-            const float ma = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
-            const float mb = __builtin_fmaf(v[e + 1].x, v[e + 1].x, v[e + 1].y * v[e + 1].y);
-            top2_pair(k1, k2, (__float_as_uint(ma) & ~63u) | (unsigned)e,
-                      (__float_as_uint(mb) & ~63u) | (unsigned)(e + 1));
-        }
-        unsigned K1, K2;
-        wave_top2_merge<LPS>(k1, k2, h, K1, K2);
-        const unsigned long long bm = __ballot(k1 == K1);
-        const unsigned long long hm = (bm >> (LPS * h)) & ((1ull << (LPS & 63)) - 1);
-        ArgMax2 b2;
-        b2.v = __uint_as_float(K1 & ~63u);
-        b2.v2 = __uint_as_float(K2 | 63u);
-        b2.i = (__ffsll((long long)hm) - 1) + LPS * (int)(K1 & 63u);
         float am = 1.0f;
         if constexpr (M0) {
 #pragma unroll
@@ -574,12 +543,73 @@ __global__ __launch_bounds__(512) void k_wave2s(FrameArgs P) {
             am = amax;
         }
         const float cb1 = cert_bound<SF>(c.rate, c.start, 1.0f, kWaveExtra);
-        const float cgap = cert_gap(b2);
-        const bool cert = cgap > 4.0f * (cb1 * am) && (float)N * 1.41421366f * am * 1.0001f < 1e18f &&
-                          am >= 1e-20f && b2.v >= 1e-30f;
-        const bool redo = c.ok && (!cert || A.debug_recheck || lost);
+        int sym = 0;         // the symbol's bin (certified) ...
+        float cgap = -1.0f;  // ... and its certified lead (-1: not certified)
+        bool pv = false;     // the whole unit certified by Parseval (lphy_wave.h)
+        if (pv_on && !A.debug_recheck) {
+            const int kc = pv_candidate<SF>(v, l, c.rate);
+            const cf32 wkl = A.tw[(unsigned)(kc * l) & (unsigned)(N - 1)];
+            cf32 ykl;
+            float el;
+            pv_lane_sums<SF>(v, kc, rroot, Qr, Pr, ykl, el);
+            const float lead = pv_lead<SF>(cmul_fma(ykl, wkl), el, M0 ? 1.0f : c.scale * c.scale, am);
+            const bool ok = lead > 4.0f * (cb1 * am) && (float)N * 1.41421366f * am * 1.0001f < 1e18f &&
+                            am >= 1e-20f;
+            pv = __ballot(live && c.ok && !ok) == 0;
+            if (pv) {
+                pv_count(A, live && c.ok && l == 0);
+                sym = kc;
+                cgap = lead;
+            } else {
+                pv_on = false;  // until a unit enters a new frame: the transform
+            }
+        }
+        if (!pv) {
+#pragma unroll
+            for (int e = 0; e < 64; ++e) v[e] = cmul_fma(cmul_fma(v[e], Qr[e & 7]), Pr[e >> 3]);
+            wpass1<SF, true>(v, ctw(A.tw));
+            int hx = h, lx = l;
+            asm volatile("" : "+v"(hx), "+v"(lx));
+            WTw<SF> T;
+            T.load(A.tw, lx);
+            // (no exchange buffer at wbuf_acquire's cap: the unit's symbols go to
+            // the exact re-run, `lost`)
+            const int b = wbuf_acquire<L::NBUF>(locks, bstart, wlock_salt(A, u));
+            const bool lost = b < 0;
+            if (!lost) {
+                wexchange<SF>(v, (cf32*)(pool + b * W::BUF), hx, lx);
+                wait_lgkm0();
+                wbuf_release(locks, b);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 64; ++e) v[e] = czero();
+            }
+            wpass2<SF, true>(v, T, A.tw, l);
+            unsigned k1 = 0u, k2 = 0u;
+#pragma unroll
+            for (int e = 0; e < 64; e += 2) {
+                const float ma = __builtin_fmaf(v[e].x, v[e].x, v[e].y * v[e].y);
+                const float mb = __builtin_fmaf(v[e + 1].x, v[e + 1].x, v[e + 1].y * v[e + 1].y);
+                top2_pair(k1, k2, (__float_as_uint(ma) & ~63u) | (unsigned)e,
+                          (__float_as_uint(mb) & ~63u) | (unsigned)(e + 1));
+            }
+            unsigned K1, K2;
+            wave_top2_merge<LPS>(k1, k2, h, K1, K2);
+            const unsigned long long bm = __ballot(k1 == K1);
+            const unsigned long long hm = (bm >> (LPS * h)) & ((1ull << (LPS & 63)) - 1);
+            ArgMax2 b2;
+            b2.v = __uint_as_float(K1 & ~63u);
+            b2.v2 = __uint_as_float(K2 | 63u);
+            b2.i = (__ffsll((long long)hm) - 1) + LPS * (int)(K1 & 63u);
+            const float g = cert_gap(b2);
+            const bool cert = g > 4.0f * (cb1 * am) && (float)N * 1.41421366f * am * 1.0001f < 1e18f &&
+                              am >= 1e-20f && b2.v >= 1e-30f;
+            sym = b2.i;
+            cgap = cert && !A.debug_recheck && !lost ? g : -1.0f;
+        }
+        const bool redo = c.ok && !(cgap >= 0.0f);
         if (live && l == 0) {
-            const uint16_t out = redo ? kSymRecheck : (uint16_t)b2.i;
+            const uint16_t out = redo ? kSymRecheck : (uint16_t)sym;
             if (c.have_sync && c.s < 2) store_symbol(A, c, c.ok ? out : (uint16_t)0);
             else if (c.ok) store_symbol(A, c, out);
             if (redo) A.meta[c.f].status = kStatusRecheck;

@@ -352,6 +352,15 @@ class Demodulator:
     def reserve(self, frames: int, frame_samples: int) -> None:
         _chk(self.lib.lphy_hip_ctx_reserve(self.ctx, frames, frame_samples), "lphy_hip_ctx_reserve")
 
+    def parseval_count(self, reset: bool = True) -> int:
+        """Test build only: symbols the wave kernels (SF 9-12) certified by
+        the Parseval certificate, without their FFT (device sync)."""
+        fn = self.lib.lphy_hip_test_counter
+        fn.argtypes = [_vp, C.c_int, C.POINTER(C.c_ulonglong), C.c_int]
+        n = C.c_ulonglong(0)
+        _chk(fn(self.ctx, 1, C.byref(n), int(reset)), "lphy_hip_test_counter")
+        return int(n.value)
+
     def recheck_count(self, reset: bool = True) -> int:
         """Symbols the fused kernel re-ran with the exact rotation (device sync)."""
         n = C.c_ulonglong(0)

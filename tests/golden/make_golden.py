@@ -14,9 +14,10 @@ from /root/reference's own sources (oracle/Makefile).  Writes:
                                 the reference's bit_exact_test input format
                                 (bit_exact_test.cpp:62-105: u32 count, then per
                                 record u8 0, u32 sf/bw_khz/cr_idx/flags/len,
-                                payload, u32 n, f64 IQ) for the BW125 profiles
-                                of tests/profiles.yaml, which the reference
-                                could not run because the file was missing.
+                                payload, u32 n, f64 IQ) for every profile of
+                                tests/profiles.yaml, which the reference could
+                                not run because the file was missing (BW250/500:
+                                expected bytes = the reference's own decode).
 
 Usage: python tests/golden/make_golden.py   (from the repo root)
 """
@@ -207,12 +208,22 @@ def main() -> None:
     (HERE / "manifest.json").write_text(json.dumps(manifest, indent=1, sort_keys=False))
     np.savez_compressed(HERE / "golden_v1.npz", **arrays)
 
-    # modulation_tests.bin in the reference's own format, BW125 profiles
+    # modulation_tests.bin in the reference's own format, every profile of
+    # tests/profiles.yaml.  BW125: the ramp payload, which the reference
+    # recovers.  BW250/500: the reference's lora_modulate at that bandwidth
+    # does not round-trip through its own dechirp + lora_demodulate (SURVEY
+    # §0.8: e2e fails those four profiles), so the record's expected bytes
+    # are what the reference's chain decodes (bit_exact_test.cpp:143-166),
+    # i.e. the reference's own output for the stored samples.
     recs = []
-    for sf, cr in [(7, 1), (7, 3), (8, 1)]:
+    for sf, bw, cr in [(7, 125000, 1), (7, 125000, 3), (8, 125000, 1), (9, 250000, 4), (10, 250000, 3),
+                       (11, 500000, 1), (12, 500000, 1)]:
         payload = bytes.fromhex(ramp32())
-        iq = ref.modulate(ref.encode(payload, sf), sf)
-        body = struct.pack("<B5I", 0, sf, 125, cr, 0, len(payload)) + payload
+        iq = ref.modulate(ref.encode(payload, sf), sf, bw_hz=bw)
+        if bw != 125000:
+            r, syms, _, _ = ref.lora_demodulate(ref.dechirp(iq, sf, bw_hz=bw), sf)
+            payload = ref.decode(syms)[1][: len(syms) // 2].tobytes()
+        body = struct.pack("<B5I", 0, sf, bw // 1000, cr, 0, len(payload)) + payload
         body += struct.pack("<I", iq.size) + np.stack([iq.real, iq.imag], 1).astype("<f8").tobytes()
         recs.append(body)
     (HERE / "modulation_tests.bin").write_bytes(struct.pack("<I", len(recs)) + b"".join(recs))

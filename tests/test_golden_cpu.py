@@ -90,11 +90,18 @@ def test_checksum_known_answer(oracle):
 
 def test_modulation_tests_bin_records(oracle):
     """vectors/golden/modulation_tests.bin in the reference's record format
-    (SURVEY §4): every record's IQ demodulates back to its payload."""
+    (SURVEY §4), one record per profile of the reference's tests/profiles.yaml:
+    each record's IQ is the oracle's lora_modulate of the ramp payload at the
+    profile's SF / bandwidth, and its expected bytes are what the dechirp +
+    lora_demodulate + lora_decode chain gives (BW125: the payload itself;
+    BW250/500, where the reference's chain does not round-trip, SURVEY §0.8:
+    its own decode, bit_exact_test.cpp:143-166)."""
     blob = (G.HERE / "modulation_tests.bin").read_bytes()
     (count,) = struct.unpack_from("<I", blob, 0)
     off, n = 4, 0
     hdr = struct.Struct("<B5I")
+    ramp = bytes(i & 0xFF for i in range(32))
+    seen = []
     for _ in range(count):
         kind, sf, bw_khz, cr, _res, plen = hdr.unpack_from(blob, off)
         off += hdr.size
@@ -105,12 +112,14 @@ def test_modulation_tests_bin_records(oracle):
         ri = np.frombuffer(blob[off:off + 16 * nsamp], "<f8").reshape(nsamp, 2)
         off += 16 * nsamp
         iq = (ri[:, 0] + 1j * ri[:, 1]).astype(np.complex64)
-        assert kind == 0 and bw_khz == 125
+        assert kind == 0
         np.testing.assert_array_equal(iq.view(np.uint64),
-                                      oracle.modulate(oracle.encode(payload), sf).view(np.uint64))
-        r, syms, sync, _ = oracle.lora_demodulate(oracle.dechirp(iq, sf), sf)
+                                      oracle.modulate(oracle.encode(ramp), sf, bw_hz=1000 * bw_khz).view(np.uint64))
+        r, syms, sync, _ = oracle.lora_demodulate(oracle.dechirp(iq, sf, bw_hz=1000 * bw_khz), sf)
         k, pay = oracle.lora_decode(syms)
-        assert pay.tobytes() == payload and sync == 0x12
+        assert pay.tobytes() == payload
+        assert (payload == ramp) == (bw_khz == 125)
+        seen.append((sf, bw_khz, cr))
         n += 1
     assert off == len(blob)
-    assert n == 3
+    assert seen == [(7, 125, 1), (7, 125, 3), (8, 125, 1), (9, 250, 4), (10, 250, 3), (11, 500, 1), (12, 500, 1)]

@@ -1,0 +1,225 @@
+"""The Parseval certificate of the SF 9-12 wave kernels (csrc/lphy_wave.h,
+k_wave and k_wave2s): a symbol unit whose every symbol carries most of its
+energy in one bin is proven from that bin and the symbol's energy alone,
+without its FFT (|Y_k| - sqrt(N E - |Y_k|^2) > 4 B); any other unit runs the
+transform and the runner-up certificate, and whatever neither proves is
+re-run exactly (k_post).  These tests pin each branch:
+
+* a straddle: one frame per call, every data symbol two pure tones with a
+  constant amplitude ratio r, r - 1 swept geometrically across the bound
+  (for two tones both certificates have the same lead N (a - b)): frames
+  above it are certified by Parseval entirely, frames below re-run every
+  data symbol exactly;
+* three tones (a main tone and two side tones of 0.8 of its amplitude):
+  less than half the energy in the winner, so Parseval cannot prove it,
+  while the runner-up certificate can: the transform path takes over and
+  nothing is re-run;
+* AWGN frames across SNRs (every path mixed).
+Every output bit is compared with the oracle (LoRaDemod.cpp:50-197,
+phy.cpp:182-243).  The Parseval count is the test build's counter
+(lphy_hip_test_counter), the re-runs lphy_hip_recheck_count."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(x):
+    return np.asarray(x, np.float32).view(np.uint32)
+
+
+def _tones_frame(oracle, sf, gains, seed, cfo=0.2, roll=True):
+    """One frame whose every data symbol is len(gains) tones (distinct
+    random bins) with relative amplitudes `gains` (a callable of the symbol
+    index giving the list), under a small CFO and delay."""
+    rng = np.random.default_rng(seed)
+    N = 1 << sf
+    S = 64
+    base = rng.integers(0, N, S)
+    x = None
+    g0 = gains(0)
+    for t in range(len(g0)):
+        # side tone t in its own part of the spectrum (never on another tone)
+        off = 0 if t == 0 else int(rng.integers((2 * t - 1) * N // 8, 2 * t * N // 8 + 1))
+        syms = ((base + off) % N).astype(np.uint16)
+        xt = oracle.modulate(syms, sf).astype(np.complex128)
+        g = np.ones(xt.size)
+        for s in range(S):
+            g[(s + 2) * N:(s + 3) * N] = gains(s)[t]
+        if t > 0:
+            g[:2 * N] = 0.0  # the sync symbols: one tone
+        x = xt * g if x is None else x + xt * g
+    n = np.arange(x.size)
+    x = x * np.exp(2j * np.pi * rng.uniform(-cfo, cfo) / N * n)
+    if roll:
+        x = np.roll(x, int(rng.integers(-N // 8, N // 8 + 1)))
+    return x.astype(np.complex64)
+
+
+def _check_one(oracle, sf, x, mode, syms, meta, ctx):
+    if mode == 0:
+        r, osyms, osync, omet = oracle.demodulate(x, sf)
+    else:
+        src = x if mode == 1 else oracle.dechirp(x, sf)
+        r, osyms, osync, omet = oracle.lora_demodulate(src, sf)
+    assert meta["status"][0] == 0, ctx
+    np.testing.assert_array_equal(syms[0], osyms, err_msg=ctx)
+    assert meta["sync_word"][0] == osync, ctx
+    assert _bits(meta["cfo"][0]) == _bits(omet[0]), ctx
+    assert _bits(meta["time_offset"][0]) == _bits(omet[1]), ctx
+
+
+def _pure_tone_frame(sf, amps, gains, seed, nsym=64):
+    """Mode-1 input (dechirped samples) built directly: two sync symbols of
+    one tone each, then data symbols of len(amps) pure integer tones at
+    distinct random bins, tone t of symbol s with amplitude amps[t] *
+    gains(s)[t].  No wrap-around phase step (a modulated chirp's dechirp
+    has one, which leaks energy out of the peak and breaks an amplitude
+    tie), so the peaks are the amplitudes times N."""
+    rng = np.random.default_rng(seed)
+    N = 1 << sf
+    n = np.arange(N)
+    tone = lambda k: np.exp(2j * np.pi * k * n / N)
+    # both sync symbols at bin 0: the estimate (LoRaDemod.cpp:80-136) then
+    # finds cfo 0 and time offset 0, so the data tones stay on integer bins
+    # (a fractional rotation would leak each tone into the others' bins and
+    # break a tie by far more than the sweeps' ratios)
+    out = [tone(0), tone(0)]
+    for s in range(nsym):
+        bins = rng.choice(N, len(amps), replace=False)
+        g = gains(s)
+        out.append(sum(amps[t] * g[t] * tone(int(bins[t])) for t in range(len(amps))))
+    return np.concatenate(out).astype(np.complex64)
+
+
+@pytest.mark.parametrize("sf", [9, 10, 11, 12])
+def test_runner_up_threshold_straddled(oracle, lphy, sf):
+    """One frame per call (mode 1), every data symbol two pure tones at a
+    constant amplitude ratio r.  Two comparable tones give the Parseval
+    certificate no candidate (their lag autocorrelations average the two
+    frequencies) and no lead beyond the runner-up's, so these symbols go to
+    the transform: above the runner-up bound every symbol is certified,
+    below it every data symbol is re-run exactly; the switch lies where
+    |X_a| - |X_b| = N (r - 1) / 2 meets 4 B."""
+    d = lphy.Demodulator(sf, test_build=True)
+    ks = 2.0 ** np.linspace(-22, -8, 29)
+    rows = []
+    for i, k in enumerate(ks):
+        x = _pure_tone_frame(sf, [0.5, 0.5], lambda s, k=k: [1.0, (1.0 + k) if s % 2 else 1.0 / (1.0 + k)],
+                             seed=7000 + 31 * sf + i)
+        d.recheck_count(reset=True)
+        d.parseval_count(reset=True)
+        syms, _, meta = d.demod_host(x[None, :], 1, x.size, 1, lphy.F_DECODE)
+        n_exact, n_pv = d.recheck_count(reset=True), d.parseval_count(reset=True)
+        _check_one(oracle, sf, x, 1, syms, meta, f"sf {sf} r-1 {k:.3g}")
+        rows.append((k, n_exact, n_pv))
+    assert d.bounds_violations() == 0
+    msg = "\n".join(f"r-1 {k:.3g}: exact {n} parseval {p}" for k, n, p in rows)
+    certified = [k for k, n, p in rows if n == 0]
+    rerun = [k for k, n, p in rows if n == 64]
+    assert certified and rerun, msg
+    assert max(rerun) < min(certified) < 2.0 ** -9, msg
+    assert all(p <= 2 for _, _, p in rows), msg  # Parseval: the one-tone sync symbols at most
+
+
+def _flat_side_frame(sf, delta, seed, nsym=64):
+    """Mode-1 input: sync symbols at bin 0, then data symbols of a main tone
+    (amplitude 1/2, random bin k) plus equal power at every other bin with
+    random phases, that power summing to a fraction 1 - delta of the main
+    tone's.  A flat side spectrum leaves the candidate's lag
+    autocorrelations pointing at k exactly (the other bins' roots of unity
+    sum to minus k's), so the Parseval lead |Y_k| - sqrt(N E - |Y_k|^2) =
+    N (1 - sqrt(1 - delta)) / 2 decides alone."""
+    rng = np.random.default_rng(seed)
+    N = 1 << sf
+    n = np.arange(N)
+    out = [np.ones(N), np.ones(N)]
+    c = 0.5 * np.sqrt((1.0 - delta) / (N - 1))
+    for s in range(nsym):
+        k = int(rng.integers(0, N))
+        Y = c * N * np.exp(2j * np.pi * rng.random(N))
+        Y[k] = 0.5 * N
+        out.append(np.fft.ifft(Y))
+    return np.concatenate(out).astype(np.complex64)
+
+
+@pytest.mark.parametrize("sf", [9, 10, 11, 12])
+def test_parseval_threshold_straddled(oracle, lphy, sf):
+    """One frame per call (mode 1), every data symbol a main tone holding a
+    fraction 1 / (2 - delta) of the energy, the rest spread flat over the
+    other bins (_flat_side_frame), delta swept geometrically.  Parseval's
+    lead ~ N delta / 4 crosses its bound inside the sweep, while the
+    runner-up certificate's lead stays ~ N / 2: above Parseval's bound every
+    symbol is certified by Parseval, below it by the transform, and nothing
+    is re-run."""
+    d = lphy.Demodulator(sf, test_build=True)
+    deltas = 2.0 ** np.linspace(-24, -4, 41)
+    rows = []
+    for i, dl in enumerate(deltas):
+        x = _flat_side_frame(sf, dl, seed=9000 + 31 * sf + i)
+        d.recheck_count(reset=True)
+        d.parseval_count(reset=True)
+        syms, _, meta = d.demod_host(x[None, :], 1, x.size, 1, lphy.F_DECODE)
+        n_exact, n_pv = d.recheck_count(reset=True), d.parseval_count(reset=True)
+        _check_one(oracle, sf, x, 1, syms, meta, f"sf {sf} delta {dl:.3g}")
+        rows.append((dl, n_exact, n_pv))
+    assert d.bounds_violations() == 0
+    msg = "\n".join(f"delta {k:.3g}: exact {n} parseval {p}" for k, n, p in rows)
+    assert all(n == 0 for _, n, _ in rows), msg
+    proven = [k for k, n, p in rows if p == 66]
+    transform = [k for k, n, p in rows if p <= 2]
+    assert proven and transform, msg
+    assert max(transform) < min(proven) < 2.0 ** -6, msg
+
+
+@pytest.mark.parametrize("sf", [9, 10, 11, 12])
+def test_three_tones_take_the_transform(oracle, lphy, sf):
+    d = lphy.Demodulator(sf, test_build=True)
+    for i in range(3):
+        x = _tones_frame(oracle, sf, lambda s: [1.0, 0.8, 0.8], seed=8000 + sf * 7 + i)
+        d.recheck_count(reset=True)
+        d.parseval_count(reset=True)
+        syms, _, meta = d.demod_host(x[None, :], 1, x.size, 2, lphy.F_DECODE)
+        n_exact, n_pv = d.recheck_count(reset=True), d.parseval_count(reset=True)
+        _check_one(oracle, sf, x, 2, syms, meta, f"sf {sf} frame {i}")
+        # Parseval proves the one-tone sync symbols at most (SF 12: its
+        # units hold one symbol each); the data symbols: the transform
+        assert n_pv <= 2 and n_exact == 0, (n_pv, n_exact)
+
+
+@pytest.mark.parametrize("sf,nf", [(9, 800), (10, 400), (11, 200), (12, 100)])
+@pytest.mark.parametrize("mode", [0, 2])
+def test_awgn_mixed_paths(oracle, lphy, sf, nf, mode):
+    """AWGN from 30 dB down to -10 dB per-sample SNR over the batch's frames
+    (one SNR per frame): high-SNR frames take Parseval, low ones the
+    transform (after one attempt per frame), near-ties the exact re-run."""
+    N = 1 << sf
+    rng = np.random.default_rng(900 + sf)
+    base = oracle.modulate(oracle.encode(bytes(range(32))), sf).astype(np.complex128)
+    n = np.arange(base.size)
+    snrs = np.linspace(30, -10, nf)
+    iq = np.zeros((nf, base.size), np.complex64)
+    for f in range(nf):
+        sig = np.sqrt(10 ** (-snrs[f] / 10) / 2)
+        x = base * np.exp(2j * np.pi * rng.uniform(-0.3, 0.3) / N * n)
+        x = x + sig * (rng.standard_normal(x.size) + 1j * rng.standard_normal(x.size))
+        iq[f] = x.astype(np.complex64)
+    dt = lphy.Demodulator(sf, test_build=True)
+    dt.parseval_count(reset=True)
+    got = dt.demod_host(iq, nf, iq.shape[1], mode, lphy.F_DECODE)
+    n_pv = dt.parseval_count(reset=True)
+    # the separate launches (no Parseval) as the whole-batch reference
+    ref = lphy.Demodulator(sf).demod_host(iq, nf, iq.shape[1], mode, lphy.F_DECODE | lphy.F_UNFUSED)
+    np.testing.assert_array_equal(got[0], ref[0])
+    np.testing.assert_array_equal(got[1], ref[1])
+    np.testing.assert_array_equal(got[2].view(np.uint8), ref[2].view(np.uint8))
+    assert 0 < n_pv < nf * 66, n_pv
+    for f in range(0, nf, max(1, nf // 25)):
+        if mode == 0:
+            r, osyms, osync, omet = oracle.demodulate(iq[f], sf)
+        else:
+            r, osyms, osync, omet = oracle.lora_demodulate(oracle.dechirp(iq[f], sf), sf)
+        ctx = f"sf {sf} mode {mode} frame {f} snr {snrs[f]:.1f}"
+        assert got[2]["status"][f] == 0, ctx
+        np.testing.assert_array_equal(got[0][f], osyms, err_msg=ctx)
+        assert _bits(got[2]["cfo"][f]) == _bits(omet[0]), ctx
