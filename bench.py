@@ -427,7 +427,7 @@ def write_perf_csv(path: str, run_id: str, rows: list) -> None:
 
 def frames_fused(sf: int) -> bool:
     """Whether the bench frame shape takes a fused launch: every SF (k_frames
-    up to SF 8, k_wave2s at SF 9, k_wave at 10-12; lphy_hip.hip frames_fit /
+    up to SF 8, k_wave at SF 9-12; lphy_hip.hip frames_fit /
     wave_fit: the bench's batches are far above the fused crossover)."""
     return True
 
@@ -435,10 +435,10 @@ def frames_fused(sf: int) -> bool:
 def fused_kernel(sf: int) -> str:
     """Name of the fused launch's kernel, as the PMC summaries key it, by the
     library's own rule for the bench's frames (66 symbols, osr 1, no window;
-    lphy_hip.hip wave_fit, lphy_kernels.h use_wave2s)."""
+    lphy_hip.hip wave_fit)."""
     if sf <= 8:
         return f"k_frames<{sf}>"
-    return f"k_wave2s<{sf}>" if sf == 9 else f"k_wave<{sf}>"
+    return f"k_wave<{sf}>"
 
 
 def measured_traffic(kernel: str, frames: int):

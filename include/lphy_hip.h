@@ -139,7 +139,7 @@ size_t lphy_hip_syms_per_frame(const lphy_hip_ctx* ctx, size_t frame_samples,
  * frame_samples < 2^31 (32-bit symbol bookkeeping in the kernels): larger
  * batches give -ERANGE; split them across calls.
  * Launch choice: the fused launches (k_frames up to SF 8 and for windowed
- * SF 9-10; k_wave2s at SF 9 and k_wave at SF 10-12 for osr 1, no window,
+ * SF 9-10; k_wave at SF 9-12 for osr 1, no window,
  * modes 1/2 with the speculative normalisation or mode 0) for batches of at
  * least a per-SF crossover (256 frames at SF <= 7 ... 384 at SF 10-12,
  * DESIGN.md 4.7; lphy_hip_ctx_set_fused_min_frames overrides it per

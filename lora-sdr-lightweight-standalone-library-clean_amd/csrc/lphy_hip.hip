@@ -162,7 +162,7 @@ inline bool frames_fit(unsigned sf, unsigned osr, int est_units, size_t total) {
     return total + 1 >= 2 * wt;
 }
 
-// Whether the fused SF 9-12 kernels (k_wave / k_wave2s, 64 x 64 values per
+// Whether the fused SF 9-12 kernel (k_wave, 64 x 64 values per
 // wavefront unit) take this batch: osr 1, the two-symbol estimate, no
 // window, the certified rotation, and in modes 1/2 the speculative
 // normalisation.  Hann windows, LPHY_F_EXACT_ROTATION and the pre-scan
@@ -488,7 +488,6 @@ int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t f
     A.counters = c->d_counters;
     A.spec = (mode != LPHY_MODE_DEMODULATE && !A.no_scratch && !(flags & LPHY_F_SCAN_FIRST)) ? 1 : 0;
     A.debug_recheck = (flags & LPHY_F_DEBUG_RECHECK) ? 1 : 0;
-    A.lock_fail = (flags & LPHY_F_DEBUG_LOCKFAIL) ? 1 : 0;
     const size_t est_syms = mode == LPHY_MODE_DEMODULATE ? 2 : (total < 2 ? total : 2);
     A.est_units = (int)(est_syms * c->osr);
     // 32-bit symbol / sample bookkeeping in the kernels

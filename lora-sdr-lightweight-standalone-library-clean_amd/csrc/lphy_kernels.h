@@ -77,9 +77,7 @@ struct DemodArgs {
     // atomic max / min), flags (1 NaN, 2 symbol left open)}; nullptr = off
     uint4* spec_big;
     int debug_recheck;       // LPHY_F_DEBUG_RECHECK: mark estimated frames kStatusRecheck before k_demod
-    int wave;                // the fused SF 9-12 launch (k_wave / k_wave2s) ran (it settles its frames itself)
-    int lock_fail;           // LPHY_F_DEBUG_LOCKFAIL (test build): k_wave2s's exchange-buffer locks fail
-                             // deterministically, so the fail-safe path (exact re-run) is exercised
+    int wave;                // the fused SF 9-12 launch (k_wave) ran (it settles its frames itself)
     // persistent demod workers: symbol stride per step split into whole
     // frames + symbols (host-computed, so the kernel never divides)
     unsigned stride_f, stride_s;
@@ -2453,7 +2451,6 @@ __global__ __launch_bounds__(kTile) void k_post(DemodArgs A, FinalArgs F, int fi
 }
 
 #include "lphy_wave.h"
-#include "lphy_wave2.h"
 
 // ---------------------------------------------------------------------------
 // lora_modulate (LoRaMod.cpp:8-43 + ChirpGenerator.hpp:24-51), bit-exact.
@@ -2857,47 +2854,16 @@ int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symb
     return 0;
 }
 
-// Fused wave-per-symbol path, SF 9-12: which kernel.
-//   k_wave   (lphy_wave.h): one wave per SIMD, 256-thread workgroups, the
-//            next symbols staged through LDS by DMA while a symbol computes;
-//   k_wave2s (lphy_wave2.h, SF 9-10): two waves per SIMD, IQ loaded straight
-//            into registers, LDS exchange buffers shared under locks, units
-//            spanning frames (frames of at least SPW symbols).
-// By the round-4 measurements: k_wave2s at SF 9, k_wave at
-// SF 10-12 and for frames shorter than a unit.  The test build takes
-// LPHY_WAVE=1 | 2s to force one for comparisons (lphy_testing.h).
-template <int SF>
-bool use_wave2s(const DemodArgs& A) {
-    if constexpr (WGeo<SF>::SPW < 4) {
-        (void)A;
-        return false;
-    } else {
-        if (A.total_syms < (unsigned long long)WGeo<SF>::SPW) return false;  // k_wave2s's precondition
-#ifdef LPHY_AB_WAVE_V1  // A/B timing builds only (tools/ubench/variants.py)
-        return false;
-#endif
-        const int forced = lphy_test_wave_kind();  // -1 in the product build
-        if (forced >= 0) return forced == 2;
-        return SF == 9;
-    }
-}
-
+// Fused wave-per-symbol path, SF 9-12: k_wave (lphy_wave.h): one wave per
+// SIMD, 256-thread workgroups, the next unit staged through LDS by DMA while
+// a unit computes.  (Round 4's k_wave2 / k_wave2s, two waves per SIMD with
+// shared exchange buffers, were removed in round 5: with the Parseval
+// certificate and the grouped estimate units k_wave was faster at every SF,
+// DESIGN §4.9.)
 template <int SF, int MODE>
 int launch_wave_mode(const DemodArgs& A, hipStream_t st) {
     FrameArgs P{};
     P.A = A;
-    if constexpr (WGeo<SF>::SPW >= 4) {
-        if (use_wave2s<SF>(A)) {
-            constexpr unsigned WPB = W2Lds<SF, MODE>::WPB;
-            unsigned long long blocks = (unsigned long long)cu_count();
-            const unsigned long long need = (A.frames + WPB - 1) / WPB;
-            if (blocks > need) blocks = need;
-            P.waves = (unsigned)(blocks * WPB);
-            hipLaunchKernelGGL((k_wave2s<SF, MODE>), dim3((unsigned)blocks), dim3(64 * WPB), 0, st, P);
-            HIP_OK(hipGetLastError());
-            return 0;
-        }
-    }
     unsigned long long blocks = (unsigned long long)cu_count();
     const unsigned long long need = (A.frames + WGeo<SF>::WPB - 1) / WGeo<SF>::WPB;
     if (blocks > need) blocks = need;

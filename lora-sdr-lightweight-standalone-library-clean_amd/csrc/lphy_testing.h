@@ -23,32 +23,8 @@ enum lphy_test_flags {
                                    // marked "has open symbols" first; fused
                                    // kernels: every symbol left to k_post's
                                    // exact re-run (tests/test_gpu_concurrency.py)
-    LPHY_F_DEBUG_LOCKFAIL = 1024u, // k_wave2s: every third exchange-buffer
-                                   // acquisition fails and the others try
-                                   // once, so the fail-safe path (the unit left
-                                   // to the exact re-run) runs
-                                   // (tests/test_gpu_wave2s.py)
 };
-constexpr unsigned kTestFlags =
-    LPHY_F_EXACT_ROTATION | 128u | LPHY_F_SCAN_FIRST | LPHY_F_DEBUG_RECHECK | LPHY_F_DEBUG_LOCKFAIL;
-
-// Test build only: LPHY_WAVE=1 forces k_wave, LPHY_WAVE=2s k_wave2s (SF 9-10,
-// frames of at least a unit) on the fused SF 9-10 path, for comparisons of
-// the two kernels.  -1: the library's own choice.
-inline int lphy_test_wave_kind() {
-#ifdef LPHY_TEST_PATHS
-    static const int v = [] {
-        const char* e = std::getenv("LPHY_WAVE");
-        if (!e) return -1;
-        if (e[0] == '1') return 1;
-        if (e[0] == '2' && e[1] == 's') return 2;
-        return -1;
-    }();
-    return v;
-#else
-    return -1;
-#endif
-}
+constexpr unsigned kTestFlags = LPHY_F_EXACT_ROTATION | 128u | LPHY_F_SCAN_FIRST | LPHY_F_DEBUG_RECHECK;
 
 // Test build only: LPHY_FUSED_MIN_FRAMES sets the process default of the
 // smallest batch the fused kernels take (the lora_phy:: probes run once with

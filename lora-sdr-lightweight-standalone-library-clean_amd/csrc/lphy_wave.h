@@ -53,7 +53,10 @@ struct WGeo {
     static constexpr int N = 1 << SF;
     static constexpr int LPS = N / 64;    // lanes per symbol = pass-1 sub-transform length
     static constexpr int SPW = 64 / LPS;  // symbols per unit (1 | 2 | 4 | 8)
-    static constexpr int NE = SPW == 1 ? 2 : 1;  // estimate units per frame
+    static constexpr int NE = SPW == 1 ? 2 : 1;  // estimate units per frame (group)
+    // frames per estimate unit: SF 9-10 put EPU frames' two estimate symbols
+    // in one unit (halves 2j, 2j + 1: frame j), SF 11-12 one frame's
+    static constexpr int EPU = SPW >= 4 ? SPW / 2 : 1;
     static constexpr int L = (SF + 1) / 2;       // KISS stages (radix 4, a last radix 2 for odd SF)
     static constexpr int PPS = N / 128;   // LDS-DMA pieces (1 KiB) per symbol
     static_assert(PPS % 4 == 0, "LDS-DMA in groups of four pieces");
@@ -414,6 +417,7 @@ struct WDma {
     unsigned f, j;
     int t_off;
     int est, on;
+    unsigned fstride, nest;  // estimate units: the group's frames f + j fstride, j < nest (EPU > 1)
 };
 
 // Window start of symbol s under time shift t (LoRaDemod.cpp:144-150, as
@@ -431,24 +435,34 @@ __device__ __forceinline__ unsigned wwin(const DemodArgs& A, unsigned s, int t, 
 }
 
 // LDS-DMA of one unit's windows into the wave's buffer: symbol h of the
-// unit at h SS (dead halves load a valid window).
+// unit at h SS.  Halves without a symbol (an estimate unit's halves past the
+// two estimate symbols, a frame's last unit's halves past its last symbol)
+// load nothing: their lanes compute on whatever the buffer holds, and
+// nothing of them is used (round 4 loaded a valid window for them: at SF 9
+// 48 KiB per frame, 18 % more than the frame's 270 KiB).
 template <int SF>
 __device__ __forceinline__ void wdma(const DemodArgs& A, cf32* buf, const WDma& d, int lane) {
     using W = WGeo<SF>;
     typedef __attribute__((address_space(3))) void lds_void;
     typedef __attribute__((address_space(1))) const void g_void;
     const unsigned S = (unsigned)A.total_syms;
-#pragma unroll
+    // (a loop, not unrolled: the halves' wave-uniform addresses would
+    // otherwise all be live at once and spill SGPRs)
+#pragma unroll 1
     for (int h = 0; h < W::SPW; ++h) {
-        unsigned base;
+        unsigned base, fr = d.f;
         if (d.est) {
-            base = (W::SPW == 1 ? d.j : (h < 2 ? (unsigned)h : 1u)) * (unsigned)W::N;
+            // SF 12: symbol j; below: half h holds symbol h & 1 of the
+            // group's frame h >> 1
+            if (W::SPW > 1 && (unsigned)(h >> 1) >= d.nest) break;
+            base = (W::SPW == 1 ? d.j : (unsigned)(h & 1)) * (unsigned)W::N;
+            fr = d.f + (unsigned)(h >> 1) * d.fstride;
         } else {
-            unsigned sy = (unsigned)W::SPW * d.j + (unsigned)h;
-            if (sy >= S) sy = (unsigned)W::SPW * d.j;
+            const unsigned sy = (unsigned)W::SPW * d.j + (unsigned)h;
+            if (sy >= S) break;  // (wave-uniform: halves in order)
             base = wwin(A, sy, d.t_off, (unsigned)W::N);
         }
-        const cf32* src = A.iq + (unsigned long long)d.f * A.frame_samples + base + 2 * lane;
+        const cf32* src = A.iq + (unsigned long long)fr * A.frame_samples + base + 2 * lane;
         // four 1 KiB pieces per base: the instruction's immediate offset moves
         // the source and the LDS destination alike (tools/ubench/glds_align)
 #pragma unroll
@@ -839,6 +853,18 @@ __device__ __forceinline__ float pv_lead(cf32 yk, float e, float scale2, float a
 // their registers then never compete with the symbol units' 64-value
 // transform, and the few calls per frame cost a spill of the loop state.
 
+// Another half's estimate unit result (lanes of half h: src = first lane of
+// the half wanted).
+__device__ __forceinline__ UnitResult wur_from(const UnitResult& u, int src) {
+    UnitResult r;
+    r.idx = __shfl(u.idx, src, 64);
+    r.valid = __shfl(u.valid, src, 64);
+    r.findex = __shfl(u.findex, src, 64);
+    r.phase = __shfl(u.phase, src, 64);
+    r.nan = __shfl(u.nan, src, 64);
+    return r;
+}
+
 // An estimate unit from the wave's buffer (SF 12: one estimate symbol; SF
 // 9-11: symbols 0 and 1 in halves 0 and 1): KISS's exact transform and the
 // detector outputs; .nan when a bin is NaN (the frame then goes to the exact
@@ -853,7 +879,8 @@ struct WEstU {
     float mx;
 };
 template <int SF, int MODE>
-__device__ __noinline__ WEstU west_unit(KArgs ka, lds_cf32* lbuf, const lds_cf32* ldnl, float mx, bool find_mx) {
+__device__ __noinline__ WEstU west_unit(KArgs ka, lds_cf32* lbuf, const lds_cf32* ldnl, float mx, bool find_mx,
+                                        unsigned nlive) {
     using W = WGeo<SF>;
     constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
     constexpr bool M0 = (MODE & 3) == LPHY_MODE_DEMODULATE;
@@ -871,11 +898,14 @@ __device__ __noinline__ WEstU west_unit(KArgs ka, lds_cf32* lbuf, const lds_cf32
         if constexpr (DECH) x = cmul(x, dnl[l + LPS * e]);
         v[e] = x;
     }
+    // (SF 9-11: halves 2j, 2j + 1 hold frame j's two estimate symbols, j <
+    // nlive; the other halves hold nothing of use)
+    const bool live_frame = SPW == 1 || (unsigned)(h >> 1) < nlive;
     if constexpr (!M0 && SPW > 1) {
         if (find_mx) {
             float fm = 0.0f;
             cf32 sum = czero();
-            if (h < 2) {
+            if (live_frame) {
 #pragma unroll
                 for (int e = 0; e < 64; ++e) {
                     fm = max3_abs(fm, v[e].x, v[e].y);
@@ -883,15 +913,18 @@ __device__ __noinline__ WEstU west_unit(KArgs ka, lds_cf32* lbuf, const lds_cf32
                 }
             }
             const bool bad = !(sum.x == sum.x && sum.y == sum.y) || !(fm <= 3.40282347e38f);
+            // over the frame's two halves (2 LPS lanes)
 #pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) fm = fmaxf(fm, __shfl_xor(fm, off, 64));
-            mx = __ballot(bad) ? __builtin_nanf("") : fm;
+            for (int off = LPS; off >= 1; off >>= 1) fm = fmaxf(fm, __shfl_xor(fm, off, 64));
+            constexpr unsigned long long PM = 2 * LPS >= 64 ? ~0ull : ((1ull << (2 * LPS)) - 1ull);
+            const unsigned pair = (unsigned)(lane / (2 * LPS));
+            mx = ((__ballot(bad) >> (pair * 2 * LPS)) & PM) != 0 ? __builtin_nanf("") : fm;
         }
     }
     lphy_frame_meta nm{};
     nm.scale = 1.0f;
     if constexpr (!M0) nm = norm_meta_hot(mx, true, A.no_scratch);
-    const bool live = nm.status == 0;
+    const bool live = live_frame && nm.status == 0;
 #pragma unroll
     for (int e = 0; e < 64; ++e) {
         cf32 x = v[e];
@@ -988,9 +1021,9 @@ __device__ __noinline__ void wclose(KArgs ka, lds_cf32* lbuf, const lds_cf32* ld
     UnitResult ua{0, 0, 0.0f, 0.0f, 0}, ub = ua;
 #pragma unroll 1
     for (int j = 0; j < W::NE; ++j) {
-        wdma<SF>(A, buf, WDma{f, (unsigned)j, 0, 1, 1}, lane);
+        wdma<SF>(A, buf, WDma{f, (unsigned)j, 0, 1, 1, 0u, 1u}, lane);
         wait_vm0();
-        const UnitResult ur = west_unit<SF, MODE>(ka, lbuf, ldnl, mt, false).ur;
+        const UnitResult ur = west_unit<SF, MODE>(ka, lbuf, ldnl, mt, false, 1u).ur;
         if constexpr (SPW == 1) {
             if (j == 0) ua = ur;
             else ub = ur;
@@ -1052,7 +1085,7 @@ __device__ __noinline__ void wclose(KArgs ka, lds_cf32* lbuf, const lds_cf32* ld
 enum : int { kWDead = 0, kWEst = 1, kWSym = 2 };
 
 struct WCursor {
-    int phase;      // 0: E(0); 1: D(k) before E(k+1); 2: E(k+1); 3: D(k) after; 4: done
+    int phase;      // 0: E(0); 1: D(k) before E(k+1); 2: E(k+1) (frames k+1 .. k+EPU); 3: D(k) after; 4: done
     unsigned k, j;  // frame (wave-local) of the D units; unit index within the phase
 };
 
@@ -1062,7 +1095,12 @@ struct WSched {
     // first unit of a (possibly empty) phase
     __device__ __forceinline__ void settle(WCursor& c) const {
         for (;;) {
-            if (c.phase == 1 && c.j >= p) { c.phase = c.k + 1 < nk ? 2 : 3; c.j = c.phase == 2 ? 0 : p; continue; }
+            // (an estimate unit before the end of D(k) when frame k + 1 starts a group)
+            if (c.phase == 1 && c.j >= p) {
+                c.phase = (c.k + 1 < nk && (c.k + 1) % (unsigned)WGeo<SF>::EPU == 0) ? 2 : 3;
+                c.j = c.phase == 2 ? 0 : p;
+                continue;
+            }
             if (c.phase == 2 && c.j >= (unsigned)WGeo<SF>::NE) { c.phase = 3; c.j = p; continue; }
             if (c.phase == 3 && c.j >= ND) {
                 if (++c.k >= nk) { c.phase = 4; return; }
@@ -1102,6 +1140,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     // one LDS block: the down-chirp at offset 0 (its wrapped index is then
     // the byte address itself), the waves' buffers after it
     __shared__ cf32 lds_all[(DN ? N : 0) + W::WPB * W::BUF];
+    __shared__ WFrame frings[W::WPB][W::EPU > 1 ? 8 : 1];  // (EPU > 1: the frame records)
     cf32* const dnl = lds_all;
     cf32 (*const sbuf)[W::BUF] = reinterpret_cast<cf32 (*)[W::BUF]>(lds_all + (DN ? N : 0));
 
@@ -1130,8 +1169,20 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     WTw<SF> T;
     T.load(A.tw, l);
 
+    // frame records: EPU = 1, two in registers by frame parity (frame k + 1's
+    // is written while frame k's units run); EPU > 1, a per-wave LDS ring
+    // (an estimate unit writes EPU frames' records at once, lane by lane)
     WFrame rec0{0.0f, 1.0f, 0.0f, 0, 0}, rec1 = rec0;
-    auto rec = [&](unsigned k) -> WFrame { return (k & 1) ? rec1 : rec0; };
+    typedef __attribute__((address_space(3))) WFrame lds_frame;
+    lds_frame* const ring = (lds_frame*)frings[wv];
+    auto rec = [&](unsigned k) -> WFrame {
+        if constexpr (W::EPU > 1) {
+            const lds_frame& q = ring[k & 7u];
+            return WFrame{q.rate, q.scale, q.mx, q.t_off, q.ok};
+        } else {
+            return (k & 1) ? rec1 : rec0;
+        }
+    };
     auto set_rec = [&](unsigned k, const WFrame& r) {
         if (k & 1) rec1 = r;
         else rec0 = r;
@@ -1139,14 +1190,16 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     auto fglob = [&](unsigned k) { return w + k * Wn; };
     // the LDS-DMA of unit c: its frame, unit index and the frame's time shift
     auto dma_plan = [&](const WCursor& c) {
-        WDma d{0u, 0u, 0, 0, 0};
+        WDma d{0u, 0u, 0, 0, 0, Wn, 1u};
         const int kd = sch.kind(c);
         if (kd == kWDead) return d;
-        d.f = fglob(sch.frame(c));
+        const unsigned kf = sch.frame(c);
+        d.f = fglob(kf);
         d.j = c.j;
         d.on = 1;
         d.est = kd == kWEst ? 1 : 0;
-        if (kd != kWEst) d.t_off = rec(sch.frame(c)).t_off;
+        d.nest = (sch.nk - kf) < (unsigned)W::EPU ? (sch.nk - kf) : (unsigned)W::EPU;
+        if (kd != kWEst) d.t_off = rec(kf).t_off;
         return d;
     };
     auto dma_unit = [&](const WCursor& c) {
@@ -1378,39 +1431,19 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             WPH(6);
         } else {
             // estimate unit(s): KISS's arithmetic, bit for bit (LoRaDemod.cpp:80-136,
-            // phy.cpp:81-148); SF 12 symbol j, SF 11 symbol h of the pair
+            // phy.cpp:81-148); SF 12 symbol j, SF 11 symbol h of the pair,
+            // SF 9-10 symbol h & 1 of frame k + (h >> 1) of the group
             // (SF 9-11: the unit folds the two estimate symbols' max-abs itself)
-            WFrame R0 = rec(k);
-            const WEstU eu = west_unit<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, R0.mx, SPW > 1);
-            const UnitResult ur = eu.ur;
-            R0.mx = eu.mx;
-            lphy_frame_meta nm{};
-            nm.scale = 1.0f;
-            nm.have_sync = 1;
-            if constexpr (!M0) nm = norm_meta_hot(R0.mx, true, A.no_scratch);
-            bool fold_now = true;
-            UnitResult ua = ur, ub = ur;
-            if constexpr (SPW == 1) {
-                if (cu.j == 0) {
-                    ur0 = ur;
-                    fold_now = false;
-                } else {
-                    ua = ur0;
-                }
-            } else {  // the pair's second estimate unit from the upper half
-                ub.idx = __shfl(ur.idx, LPS, 64);
-                ub.valid = __shfl(ur.valid, LPS, 64);
-                ub.findex = __shfl(ur.findex, LPS, 64);
-                ub.phase = __shfl(ur.phase, LPS, 64);
-                ub.nan = __shfl(ur.nan, LPS, 64);
-                ua.idx = __shfl(ur.idx, 0, 64);
-                ua.valid = __shfl(ur.valid, 0, 64);
-                ua.findex = __shfl(ur.findex, 0, 64);
-                ua.phase = __shfl(ur.phase, 0, 64);
-                ua.nan = __shfl(ur.nan, 0, 64);
-            }
-            if (fold_now) {
-                lphy_frame_meta m = nm;
+            if constexpr (W::EPU > 1) {
+                const unsigned nest = (sch.nk - k) < (unsigned)W::EPU ? (sch.nk - k) : (unsigned)W::EPU;
+                const WEstU eu = west_unit<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, 0.0f, true, nest);
+                // every lane folds its own pair's frame; the pair's first lane stores it
+                const int hb = (h & ~1) * LPS;
+                const UnitResult ua = wur_from(eu.ur, hb), ub = wur_from(eu.ur, hb + LPS);
+                lphy_frame_meta m{};
+                m.scale = 1.0f;
+                m.have_sync = 1;
+                if constexpr (!M0) m = norm_meta_hot(eu.mx, true, A.no_scratch);
                 if (m.status == 0) {
                     EstFold fold;
                     if (ua.valid) fold.add(ua.idx, ua.findex, 0, ua.phase);
@@ -1420,13 +1453,59 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                     fold.finish(m, 2, N, 1);
                     if (ua.nan || ub.nan) m.status = kStatusFixup;
                 }
-                if (lane == 0) meta_put_est(&A.meta[f], m);
-                WFrame r = R0;
-                r.rate = m.rate;
-                r.scale = m.scale;
-                r.t_off = m.t_off;
-                r.ok = m.status == 0 ? 1 : 0;
-                set_rec(k, r);
+                const unsigned kj = k + (unsigned)(h >> 1);
+                if ((h & 1) == 0 && l == 0 && (unsigned)(h >> 1) < nest) {
+                    bound_check(fglob(kj), (long long)A.frames);
+                    meta_put_est(&A.meta[fglob(kj)], m);
+                    lds_frame& q = ring[kj & 7u];
+                    q.rate = m.rate;
+                    q.scale = m.scale;
+                    q.mx = eu.mx;
+                    q.t_off = m.t_off;
+                    q.ok = m.status == 0 ? 1 : 0;
+                }
+            } else {
+                WFrame R0 = rec(k);
+                const WEstU eu =
+                    west_unit<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, R0.mx, SPW > 1, 1u);
+                const UnitResult ur = eu.ur;
+                R0.mx = eu.mx;
+                lphy_frame_meta nm{};
+                nm.scale = 1.0f;
+                nm.have_sync = 1;
+                if constexpr (!M0) nm = norm_meta_hot(R0.mx, true, A.no_scratch);
+                bool fold_now = true;
+                UnitResult ua = ur, ub = ur;
+                if constexpr (SPW == 1) {
+                    if (cu.j == 0) {
+                        ur0 = ur;
+                        fold_now = false;
+                    } else {
+                        ua = ur0;
+                    }
+                } else {  // the pair's second estimate unit from the upper half
+                    ua = wur_from(ur, 0);
+                    ub = wur_from(ur, LPS);
+                }
+                if (fold_now) {
+                    lphy_frame_meta m = nm;
+                    if (m.status == 0) {
+                        EstFold fold;
+                        if (ua.valid) fold.add(ua.idx, ua.findex, 0, ua.phase);
+                        else fold.add(0, 0.0f, 0, 0.0f);
+                        if (ub.valid) fold.add(ub.idx, ub.findex, 0, ub.phase);
+                        else fold.add(0, 0.0f, 0, 0.0f);
+                        fold.finish(m, 2, N, 1);
+                        if (ua.nan || ub.nan) m.status = kStatusFixup;
+                    }
+                    if (lane == 0) meta_put_est(&A.meta[f], m);
+                    WFrame r = R0;
+                    r.rate = m.rate;
+                    r.scale = m.scale;
+                    r.t_off = m.t_off;
+                    r.ok = m.status == 0 ? 1 : 0;
+                    set_rec(k, r);
+                }
             }
             dma_unit(nx);  // after the fold: a symbol unit's window needs the time shift
             WPH(6);

@@ -1,7 +1,7 @@
 """Adversarial near-ties for the certified fast path.
 
 Symbol units of the fused kernels do not run KISS's exact arithmetic: they
-rotate with a per-frame table and (k_wave2) 64th-root twiddles, and prove
+rotate with a per-frame table and (k_wave) 64th-root twiddles, and prove
 the argmax with a certificate (|X_best| - 4B > |X_second|); a symbol the
 certificate cannot prove is re-run exactly (k_post).  If the bound B were
 too small, a near-tie could flip silently.  These frames are built to sit
@@ -14,7 +14,7 @@ oracle's, and lphy_hip_recheck_count must show the exact re-run fired.
 
 Kernels: SF 7-8 k_frames (modes 1/2: symbol tiles on the matrix cores,
 lphy_mfma.h, whose f16 roundings the certificate charges; mode 0 packed
-f32); SF 9 k_wave2s, SF 11-12 k_wave (no window) and, with a Hann window,
+f32); SF 9-12 k_wave (no window) and, with a Hann window,
 k_frames (SF 9) or the separate launches' certified k_demod (SF 11-12)."""
 import numpy as np
 import pytest
@@ -78,56 +78,51 @@ def test_near_ties_straddling_the_certificate(oracle, lphy, sf, nf, mode, hann):
     assert 0 < n_exact < nf * 66, f"{n_exact} exact re-runs of {nf * 66} symbols"
 
 
-def _const_ratio_frame(oracle, sf, ratio, seed, data_gain=1.0):
-    """One frame whose every data symbol is two tones (a, b) with amplitude
-    ratio `ratio` (b larger on odd symbols, smaller on even ones), under a
-    small CFO and delay; the data symbols scaled by `data_gain` against the
-    sync symbols (data_gain < 1: weak symbols after the frame's max-abs
-    normalisation, whose f16 components reach the subnormal range)."""
+def _pure_two_tone_frame(sf, ratio, seed, nsym=64):
+    """Mode-1 input (dechirped samples) built directly: sync symbols at bin
+    0 (the estimate finds cfo 0, time offset 0), then data symbols of two
+    pure integer tones of amplitude 1/2 and ratio / 2 (or 1 / ratio / 2),
+    so the two peaks differ by the ratio alone (a modulated chirp's dechirp
+    has a wrap-around phase step that leaks energy and breaks ties by much
+    more)."""
     rng = np.random.default_rng(seed)
     N = 1 << sf
-    S = 64
-    a = rng.integers(0, N, S).astype(np.uint16)
-    b = ((a.astype(np.int64) + rng.integers(2, N - 1, S)) % N).astype(np.uint16)
-    xa = oracle.modulate(a, sf).astype(np.complex128)
-    xb = oracle.modulate(b, sf).astype(np.complex128)
-    g = np.ones(xa.size)
-    for s in range(S):
-        g[(s + 2) * N:(s + 3) * N] = ratio if s % 2 else 1.0 / ratio
-    x = xa + xb * g
-    x[2 * N:] *= data_gain
-    t = np.arange(x.size)
-    x = x * np.exp(2j * np.pi * rng.uniform(-0.2, 0.2) / N * t)
-    x = np.roll(x, int(rng.integers(-N // 8, N // 8 + 1)))
-    return x.astype(np.complex64)
+    n = np.arange(N)
+    tone = lambda k: np.exp(2j * np.pi * k * n / N)
+    out = [tone(0), tone(0)]
+    for s in range(nsym):
+        a, b = rng.choice(N, 2, replace=False)
+        g = ratio if s % 2 else 1.0 / ratio
+        out.append(0.5 * tone(int(a)) + 0.5 * g * tone(int(b)))
+    return np.concatenate(out).astype(np.complex64)
 
 
 @pytest.mark.parametrize("sf", [7, 8])
-@pytest.mark.parametrize("mode", [1, 2])
-def test_matrix_core_threshold_straddled(oracle, lphy, sf, mode):
+def test_matrix_core_threshold_straddled(oracle, lphy, sf):
     """SF 7-8 modes 1/2 (the C1 bench path): k_frames' symbol tiles run the
     transform in f16 on the matrix cores (lphy_mfma.h) and the certificate
-    charges kMfmaExtra = 3 * 2^14 u of A for it, a lead of ~3.3 % of |X| for
-    these two-tone symbols.  One frame per call, every
-    data symbol of a frame at the same amplitude ratio r, r - 1 swept
-    geometrically from 2^-11 to 2^-1: frames well below the threshold must
-    re-run every data symbol exactly, frames above it certify every one, and
-    near-tie symbols (r - 1 < 1/4) are counted on both sides of it.  Every
-    output bit equals the oracle's."""
+    charges kMfmaExtra = 3 * 2^14 u of A for it: with
+    A = N sqrt2 and two tones of amplitude 1/2, a lead N (r - 1) / 2 must
+    exceed 4 B ~ 0.0166 N, i.e. r - 1 > ~3.3 %.  One frame per call (mode
+    1), every data symbol two pure tones at a constant ratio r, r - 1 swept
+    geometrically from 2^-11 to 2^-2: frames below the threshold re-run
+    every data symbol exactly, frames above it certify every one, the switch
+    lies within a factor 2 of the predicted threshold, and near-tie symbols
+    (r - 1 < 1/4) are counted on both sides.  Every output bit equals the
+    oracle's."""
     N = 1 << sf
-    ks = 2.0 ** np.linspace(-11, -1, 31)
+    L = (sf + 1) // 2
+    thr = 4.0 * 2.0 ** -24 * np.sqrt(2.0) * (24 + 12 * L + 6 + 49152) * 1.001 / 0.5  # r - 1 at the bound
+    ks = 2.0 ** np.linspace(-11, -2, 37)
     d = lphy.Demodulator(sf)
     rows = []
     for i, k in enumerate(ks):
-        x = _const_ratio_frame(oracle, sf, 1.0 + k, seed=4000 + 97 * sf + 11 * mode + i)
-        if mode == 1:  # lora_demodulate takes dechirped samples
-            x = oracle.dechirp(x, sf)
+        x = _pure_two_tone_frame(sf, 1.0 + k, seed=4000 + 97 * sf + i)
         d.recheck_count(reset=True)
-        syms, _, meta = d.demod_host(x[None, :], 1, x.size, mode, lphy.F_DECODE)
+        syms, _, meta = d.demod_host(x[None, :], 1, x.size, 1, lphy.F_DECODE)
         n_exact = d.recheck_count(reset=True)
-        src = x if mode == 1 else oracle.dechirp(x, sf)
-        r, osyms, osync, omet = oracle.lora_demodulate(src, sf)
-        ctx = f"sf {sf} mode {mode} r-1 {k:.3g}"
+        r, osyms, osync, omet = oracle.lora_demodulate(x, sf)
+        ctx = f"sf {sf} r-1 {k:.3g}"
         assert meta["status"][0] == 0, ctx
         np.testing.assert_array_equal(syms[0], osyms, err_msg=ctx)
         assert meta["sync_word"][0] == osync, ctx
@@ -135,18 +130,16 @@ def test_matrix_core_threshold_straddled(oracle, lphy, sf, mode):
         assert _bits(meta["time_offset"][0]) == _bits(omet[1]), ctx
         assert 0 <= n_exact <= 64, ctx
         rows.append((k, n_exact))
+    msg = "\n".join(f"r-1 {k:.4g}: exact {n}" for k, n in rows) + f"\npredicted r-1 {thr:.4g}"
     near = [(k, n) for k, n in rows if k < 0.25]
     certified = sum(64 - n for _, n in near)
     rerun = sum(n for _, n in near)
-    assert certified > 0 and rerun > 0, rows
-    # below the threshold every symbol is re-run, above it none: the largest
-    # ratio with a re-run lies below the smallest with none re-run... and the
-    # switch happens inside the near-tie band, at a few per cent
+    assert certified > 0 and rerun > 0, msg
     all_rerun = [k for k, n in rows if n == 64]
     none_rerun = [k for k, n in rows if n == 0]
-    assert all_rerun and none_rerun, rows
-    assert max(all_rerun) < min(none_rerun) < 0.25, rows
-    assert 0.005 < max(all_rerun), rows
+    assert all_rerun and none_rerun, msg
+    assert max(all_rerun) < min(none_rerun) < 0.25, msg
+    assert thr / 2 < max(all_rerun) and min(none_rerun) < 2 * thr, msg
 
 
 @pytest.mark.parametrize("sf", [7, 8])
@@ -157,15 +150,20 @@ def test_matrix_core_weak_symbols(oracle, lphy, sf):
     normalisation's bound, not the symbol's own amplitude, so an absolute
     f16 error of up to 2^-14 per component (flush to zero included) stays
     inside kMfmaExtra's slack; a weak near-tie is re-run.  Every output bit
-    equals the oracle's across data gains 2^-2 .. 2^-16."""
+    equals the oracle's across data gains 2^-2 .. 2^-16 (mode 1, two pure
+    tones at ratio 1.3, sync symbols of amplitude 2)."""
     d = lphy.Demodulator(sf)
     counts = []
     for i, gexp in enumerate([2, 4, 6, 8, 12, 16]):
-        x = _const_ratio_frame(oracle, sf, 1.3, seed=5000 + sf + i, data_gain=2.0 ** -gexp)
+        x = _pure_two_tone_frame(sf, 1.3, seed=5000 + sf + i).astype(np.complex128)
+        N = 1 << sf
+        x[:2 * N] *= 2.0
+        x[2 * N:] *= 2.0 ** -gexp
+        x = x.astype(np.complex64)
         d.recheck_count(reset=True)
-        syms, _, meta = d.demod_host(x[None, :], 1, x.size, 2, lphy.F_DECODE)
+        syms, _, meta = d.demod_host(x[None, :], 1, x.size, 1, lphy.F_DECODE)
         counts.append(d.recheck_count(reset=True))
-        r, osyms, osync, omet = oracle.lora_demodulate(oracle.dechirp(x, sf), sf)
+        r, osyms, osync, omet = oracle.lora_demodulate(x, sf)
         ctx = f"sf {sf} gain 2^-{gexp}"
         assert meta["status"][0] == 0, ctx
         np.testing.assert_array_equal(syms[0], osyms, err_msg=ctx)

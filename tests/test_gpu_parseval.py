@@ -1,15 +1,19 @@
 """The Parseval certificate of the SF 9-12 wave kernels (csrc/lphy_wave.h,
-k_wave and k_wave2s): a symbol unit whose every symbol carries most of its
+k_wave): a symbol unit whose every symbol carries most of its
 energy in one bin is proven from that bin and the symbol's energy alone,
 without its FFT (|Y_k| - sqrt(N E - |Y_k|^2) > 4 B); any other unit runs the
 transform and the runner-up certificate, and whatever neither proves is
 re-run exactly (k_post).  These tests pin each branch:
 
-* a straddle: one frame per call, every data symbol two pure tones with a
-  constant amplitude ratio r, r - 1 swept geometrically across the bound
-  (for two tones both certificates have the same lead N (a - b)): frames
-  above it are certified by Parseval entirely, frames below re-run every
-  data symbol exactly;
+* the runner-up straddle: one frame per call, every data symbol two pure
+  tones with a constant amplitude ratio r, r - 1 swept geometrically
+  across the runner-up bound (two comparable tones give Parseval no
+  candidate): frames above it are certified by the transform, frames
+  below re-run every data symbol exactly;
+* the Parseval straddle: one clean tone plus a half-symbol tone that adds
+  energy but nothing to the winner's bin, swept so the exact Parseval lead
+  crosses 4 B: frames well above it are proven by Parseval entirely, frames
+  below take the transform;
 * three tones (a main tone and two side tones of 0.8 of its amplitude):
   less than half the energy in the winner, so Parseval cannot prove it,
   while the runner-up certificate can: the transform path takes over and
@@ -122,54 +126,84 @@ def test_runner_up_threshold_straddled(oracle, lphy, sf):
     assert all(p <= 2 for _, _, p in rows), msg  # Parseval: the one-tone sync symbols at most
 
 
-def _flat_side_frame(sf, delta, seed, nsym=64):
-    """Mode-1 input: sync symbols at bin 0, then data symbols of a main tone
-    (amplitude 1/2, random bin k) plus equal power at every other bin with
-    random phases, that power summing to a fraction 1 - delta of the main
-    tone's.  A flat side spectrum leaves the candidate's lag
-    autocorrelations pointing at k exactly (the other bins' roots of unity
-    sum to minus k's), so the Parseval lead |Y_k| - sqrt(N E - |Y_k|^2) =
-    N (1 - sqrt(1 - delta)) / 2 decides alone."""
+KU = 2.0 ** -24
+
+
+def _burst_frame(sf, c, seed, a=0.3, nsym=64):
+    """Mode-1 input: sync symbols at bin 0 (cfo 0, time offset 0), then data
+    symbols of one tone (amplitude a, random bin k) plus, in the symbol's
+    second half only, a tone of amplitude c at a bin j = k + 2m (m != 0).
+    A half-symbol tone at an even distance from k has no projection on bin
+    k, so |Y_k| = N a exactly, while it adds N c^2 / 2 to N E: the Parseval
+    lead is N (a - c / sqrt 2) for every symbol.  The candidate reads the
+    first eighth (lag 1) and quarter (lag LPS) of each symbol, where the
+    tone is clean; the transform's runner-up (~ N c / 2) stays far below
+    N a, so the runner-up certificate holds throughout."""
     rng = np.random.default_rng(seed)
     N = 1 << sf
     n = np.arange(N)
     out = [np.ones(N), np.ones(N)]
-    c = 0.5 * np.sqrt((1.0 - delta) / (N - 1))
     for s in range(nsym):
         k = int(rng.integers(0, N))
-        Y = c * N * np.exp(2j * np.pi * rng.random(N))
-        Y[k] = 0.5 * N
-        out.append(np.fft.ifft(Y))
+        m = int(rng.integers(1, N // 2 - 1))
+        j = (k + 2 * m) % N
+        y = a * np.exp(2j * np.pi * k * n / N)
+        y[N // 2:] += c * np.exp(2j * np.pi * j * n[N // 2:] / N)
+        out.append(y)
     return np.concatenate(out).astype(np.complex64)
+
+
+def _parseval_leads(x, sf):
+    """Per data symbol: the exact Parseval lead of the normalised samples
+    (LoRaDemod.cpp:60-78's max-abs scale; cfo 0, so no rotation) and the
+    runner-up certificate's bound B (cert_bound with kWaveExtra, rate 0)."""
+    N = 1 << sf
+    xd = x.astype(np.complex128)
+    mx = max(np.abs(x.real).max(), np.abs(x.imag).max())
+    scale = 1.0 / np.float32(mx) if mx > 1.0 else 1.0
+    y = xd[2 * N:].reshape(-1, N) * np.float64(np.float32(scale))
+    Y = np.fft.fft(y, axis=1)
+    P = np.abs(Y) ** 2
+    k = P.argmax(axis=1)
+    yk = np.sqrt(P[np.arange(len(k)), k])
+    lead = yk - np.sqrt(np.maximum(N * (np.abs(y) ** 2).sum(axis=1) - yk ** 2, 0.0))
+    L = (sf + 1) // 2
+    A = N * np.sqrt(2.0)
+    B = KU * A * (24 + 12 * L + 64) * 1.001
+    return lead, B, A
 
 
 @pytest.mark.parametrize("sf", [9, 10, 11, 12])
 def test_parseval_threshold_straddled(oracle, lphy, sf):
-    """One frame per call (mode 1), every data symbol a main tone holding a
-    fraction 1 / (2 - delta) of the energy, the rest spread flat over the
-    other bins (_flat_side_frame), delta swept geometrically.  Parseval's
-    lead ~ N delta / 4 crosses its bound inside the sweep, while the
-    runner-up certificate's lead stays ~ N / 2: above Parseval's bound every
-    symbol is certified by Parseval, below it by the transform, and nothing
-    is re-run."""
+    """One frame per call (mode 1), every data symbol a clean tone plus a
+    half-symbol tone that adds energy but nothing to the winner's bin
+    (_burst_frame), swept so the exact Parseval lead N a delta crosses the
+    certificate's 4 B + the Parseval charges: frames whose every symbol leads by a clear margin are proven by
+    Parseval entirely (66 symbols with the sync symbols), frames where some
+    symbol's lead is below 4 B are not (their units take the transform,
+    which certifies them: nothing is re-run).  Every output bit equals the
+    oracle's."""
     d = lphy.Demodulator(sf, test_build=True)
-    deltas = 2.0 ** np.linspace(-24, -4, 41)
+    a = 0.3
     rows = []
-    for i, dl in enumerate(deltas):
-        x = _flat_side_frame(sf, dl, seed=9000 + 31 * sf + i)
+    for i, dl in enumerate(2.0 ** np.linspace(-20, -6, 43)):
+        x = _burst_frame(sf, np.sqrt(2.0) * a * (1.0 - dl), seed=9000 + 31 * sf + i, a=a)
         d.recheck_count(reset=True)
         d.parseval_count(reset=True)
         syms, _, meta = d.demod_host(x[None, :], 1, x.size, 1, lphy.F_DECODE)
         n_exact, n_pv = d.recheck_count(reset=True), d.parseval_count(reset=True)
         _check_one(oracle, sf, x, 1, syms, meta, f"sf {sf} delta {dl:.3g}")
-        rows.append((dl, n_exact, n_pv))
+        lead, B, A = _parseval_leads(x, sf)
+        rows.append((dl, lead.min() / B, n_exact, n_pv))
     assert d.bounds_violations() == 0
-    msg = "\n".join(f"delta {k:.3g}: exact {n} parseval {p}" for k, n, p in rows)
-    assert all(n == 0 for _, n, _ in rows), msg
-    proven = [k for k, n, p in rows if p == 66]
-    transform = [k for k, n, p in rows if p <= 2]
-    assert proven and transform, msg
-    assert max(transform) < min(proven) < 2.0 ** -6, msg
+    msg = "\n".join(f"delta {k:.3g}: min lead {r:.3g} B, exact {n}, parseval {p}" for k, r, n, p in rows)
+    assert all(n == 0 for _, _, n, _ in rows), msg
+    # the charges beyond 4 B: kPvErr u A on |Y_k| and E's 32 u, well inside 8 B
+    proven = [r for _, r, _, p in rows if p == 66]
+    short = [r for _, r, _, p in rows if p < 66]
+    assert proven and short, msg
+    assert all(p == 66 for _, r, _, p in rows if r > 8.0), msg
+    assert all(p < 66 for _, r, _, p in rows if r < 4.0), msg
 
 
 @pytest.mark.parametrize("sf", [9, 10, 11, 12])

@@ -86,9 +86,15 @@ def test_lora_phy_tests_binary(workdir):
     test in turn; the sync_word abort ends it in both builds)."""
     ours = _run(H / "amd" / "lora_phy_tests", workdir)
     ref = _run(H / "ref" / "lora_phy_tests", workdir)
-    assert ours.returncode == ref.returncode, (ours.returncode, ref.returncode, ours.stderr[-2000:])
-    strip = lambda s: [l for l in s.splitlines() if " pps, " not in l]
-    assert strip(ours.stdout) == strip(ref.stdout), ours.stdout[-3000:]
+    # sync_word_test.cpp:27-29 writes 256 samples into 255: undefined
+    # behaviour that glibc reports as "malloc(): corrupted top size" (abort)
+    # under the reference build and that may surface as a segfault instead
+    # under another heap layout; either way the process dies by a signal in
+    # both builds, and the output buffered before it is lost
+    assert ours.returncode < 0 and ref.returncode < 0, (ours.returncode, ref.returncode, ours.stderr[-2000:])
+    # the tests before sync_word report on stderr (unbuffered): the same lines
+    strip = lambda s: [l for l in s.splitlines() if "corrupted" not in l]
+    assert strip(ours.stderr) == strip(ref.stderr), (ours.stderr[-3000:], ref.stderr[-3000:])
 
 
 @pytest.mark.parametrize("payload,sf", [("48656c6c6f", 7), ("48656c6c6f", 9), ("deadbeef00112233", 8),
