@@ -36,9 +36,10 @@
 // Estimate units run KISS's own arithmetic: every twiddle from the table,
 // unfused products, the detector's exact argmax, bit-identical bins.
 //
-// Per wave, frames w, w + W, ... (W waves); per frame one blocking two-symbol
-// max-abs scan (modes 1/2), the estimate units (2 at SF 12, below one unit
-// whose halves 0 and 1 hold symbols 0 and 1), then the symbol units.  The next frame's estimate units run two
+// Per wave, frames w, w + W, ... (W waves); per frame the estimate units (2
+// at SF 12, each folding its symbol's max-abs for the normalisation; SF 11
+// one unit whose halves 0 and 1 hold symbols 0 and 1; SF 9-10 one unit for
+// EPU frames), then the symbol units.  The next frame's estimate units run two
 // symbol units before the current frame's end, so its time shift is known
 // when its first symbol unit's LDS-DMA is issued:
 //   E(0) | D(0)_0..D(0)_{p-1}, E(1), D(0)_p..D(0)_{ND-1} | D(1)_0 ...
@@ -552,59 +553,6 @@ __device__ __forceinline__ void wdma_table(const cf32* tw, cf32* buf, int lane) 
 }
 __device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); } // lgkmcnt(0)
 
-// Max-abs of the frame's two estimate symbols (samples [0, 2N)), the
-// [dechirped] samples as the reference's normalisation scans them
-// (LoRaDemod.cpp:60-78), by the whole wave with all 16-byte loads in
-// flight at once; NaN when a sample is not finite (the frame then goes to
-// the exact re-run).  Same arithmetic as wave_maxabs.
-template <int SF, int MODE>
-__device__ __noinline__ float wscan2(KArgs ka, unsigned f, const cf32* down, int lane) {
-    const DemodArgs& A = kargs(ka);
-    constexpr int N = 1 << SF;
-    constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
-    constexpr int U = N / 64 < 32 ? N / 64 : 32;  // float4 per lane per round
-    constexpr int ROUNDS = N / (64 * U);          // 2N samples = N float4
-    static_assert((128 * U) % N == 0, "chirp index of the unrolled scan");
-    const float4* f4 = reinterpret_cast<const float4*>(A.iq + (unsigned long long)f * A.frame_samples);
-    float fm = 0.0f;
-    cf32 sum = czero();
-    if ((reinterpret_cast<uintptr_t>(f4) & 15) == 0) {
-#pragma unroll
-        for (int rd = 0; rd < ROUNDS; ++rd) {
-            float4 x[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) x[u] = f4[rd * 64 * U + u * 64 + lane];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                cf32 a = cf32{x[u].x, x[u].y}, b = cf32{x[u].z, x[u].w};
-                if constexpr (DECH) {
-                    const unsigned ci = (2u * (unsigned)lane + 128u * (unsigned)u) & (N - 1);
-                    a = cmul(a, down[ci]);
-                    b = cmul(b, down[ci + 1]);
-                }
-                fm = max3_abs(fm, a.x, a.y);
-                fm = max3_abs(fm, b.x, b.y);
-                sum = sum + a;
-                sum = sum + b;
-            }
-        }
-    } else {  // 8-byte aligned frames (odd frame length): one sample per load
-        const cf32* fr = A.iq + (unsigned long long)f * A.frame_samples;
-        for (int i = lane; i < 2 * N; i += 64) {
-            cf32 a = fr[i];
-            if constexpr (DECH) a = cmul(a, down[i & (N - 1)]);
-            fm = max3_abs(fm, a.x, a.y);
-            sum = sum + a;
-        }
-    }
-    // a NaN or inf sample (or an inf - inf) ends in the sum as NaN or in the
-    // maximum as inf: exact re-run (v_max3 lacks the reference's NaN rules)
-    const bool bad = !(sum.x == sum.x && sum.y == sum.y) || !(fm <= 3.40282347e38f);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) fm = fmaxf(fm, __shfl_xor(fm, off, 64));
-    return __ballot(bad) ? __builtin_nanf("") : fm;
-}
-
 // Element e (per-lane index, -1: none) of the lane's registers.
 __device__ __forceinline__ cf32 wpick(const cf32 (&v)[64], int e) {
     cf32 r = czero();
@@ -869,20 +817,20 @@ __device__ __forceinline__ UnitResult wur_from(const UnitResult& u, int src) {
 // 9-11: symbols 0 and 1 in halves 0 and 1): KISS's exact transform and the
 // detector outputs; .nan when a bin is NaN (the frame then goes to the exact
 // re-run, as in k_frames).  Modes 1/2 normalise with the max-abs `mx`, or
-// with find_mx (SF 9-11, both estimate symbols in the unit) with the two
-// estimate symbols' max-abs folded here from the unit's own samples, as the
-// reference's normalisation scans them (LoRaDemod.cpp:60-78; NaN when one is
-// not finite, as wscan2 returns): the frame's blocking two-symbol scan is
-// then not needed.  Returns the max-abs used.
+// with find_mx with the max-abs folded here from the unit's own samples, as
+// the reference's normalisation scans them (LoRaDemod.cpp:60-78; NaN when one
+// is not finite): SF 9-11 both estimate symbols' (both are in the unit), SF
+// 12 this symbol's folded with `mx` (0, or symbol 0's for symbol 1).  No
+// blocking pre-scan of the frame is then needed.  Returns the max-abs used.
 struct WEstU {
     UnitResult ur;
     float mx;
 };
 template <int SF, int MODE>
-__device__ __noinline__ WEstU west_unit(KArgs ka, lds_cf32* lbuf, const lds_cf32* ldnl, float mx, bool find_mx,
+__device__ __forceinline__ WEstU west_unit(KArgs ka, lds_cf32* lbuf, const lds_cf32* ldnl, float mx, bool find_mx,
                                         unsigned nlive) {
     using W = WGeo<SF>;
-    constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
+    constexpr int LPS = W::LPS, SPW = W::SPW;
     constexpr bool M0 = (MODE & 3) == LPHY_MODE_DEMODULATE;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     const DemodArgs& A = kargs(ka);
@@ -901,7 +849,7 @@ __device__ __noinline__ WEstU west_unit(KArgs ka, lds_cf32* lbuf, const lds_cf32
     // (SF 9-11: halves 2j, 2j + 1 hold frame j's two estimate symbols, j <
     // nlive; the other halves hold nothing of use)
     const bool live_frame = SPW == 1 || (unsigned)(h >> 1) < nlive;
-    if constexpr (!M0 && SPW > 1) {
+    if constexpr (!M0) {
         if (find_mx) {
             float fm = 0.0f;
             cf32 sum = czero();
@@ -913,12 +861,15 @@ __device__ __noinline__ WEstU west_unit(KArgs ka, lds_cf32* lbuf, const lds_cf32
                 }
             }
             const bool bad = !(sum.x == sum.x && sum.y == sum.y) || !(fm <= 3.40282347e38f);
-            // over the frame's two halves (2 LPS lanes)
+            // over the frame's two halves (2 LPS lanes; SF 12: the wave)
 #pragma unroll
-            for (int off = LPS; off >= 1; off >>= 1) fm = fmaxf(fm, __shfl_xor(fm, off, 64));
+            for (int off = LPS < 32 ? LPS : 32; off >= 1; off >>= 1) fm = fmaxf(fm, __shfl_xor(fm, off, 64));
             constexpr unsigned long long PM = 2 * LPS >= 64 ? ~0ull : ((1ull << (2 * LPS)) - 1ull);
-            const unsigned pair = (unsigned)(lane / (2 * LPS));
-            mx = ((__ballot(bad) >> (pair * 2 * LPS)) & PM) != 0 ? __builtin_nanf("") : fm;
+            const unsigned pair = SPW == 1 ? 0u : (unsigned)(lane / (2 * LPS));
+            // (SF 12: folded with the max-abs `mx` of the frame's other estimate
+            // symbol, NaN staying NaN)
+            mx = (((__ballot(bad) >> (pair * 2 * LPS)) & PM) != 0 || !(mx == mx)) ? __builtin_nanf("")
+                                                                                  : fmaxf(mx, fm);
         }
     }
     lphy_frame_meta nm{};
@@ -963,7 +914,7 @@ struct WRot {
     cf32 p;
 };
 template <int SF, int MODE>
-__device__ __noinline__ WRot wrot(float rate, float scale) {
+__device__ __forceinline__ WRot wrot(float rate, float scale) {
     constexpr int LPS = WGeo<SF>::LPS;
     const int lane = threadIdx.x & 63, l = lane % LPS;
     WRot r;
@@ -973,7 +924,11 @@ __device__ __noinline__ WRot wrot(float rate, float scale) {
         lphy_libm::sincosf_exact(rate * (float)(l + LPS * b), &sn, &cs);
         cf32 t = cf32{cs, sn};
         if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) t = cscale(t, scale);
-        r.q[b] = t;
+        // (a select per entry: r.q[b] with the loop's run-time b would put
+        // r.q in scratch memory)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (i == b) r.q[i] = t;
     }
     float sn, cs;
     lphy_libm::sincosf_exact(rate * (float)(8 * LPS * (lane & 7)), &sn, &cs);
@@ -995,9 +950,13 @@ __device__ __noinline__ WRot wrot(float rate, float scale) {
 // r the symbols' least certificate ratio), else the frame goes to k_post's
 // exact re-run.
 template <int SF, int MODE>
-__device__ __noinline__ void wclose(KArgs ka, lds_cf32* lbuf, const lds_cf32* ldnl, unsigned f, float rate,
+__device__ __forceinline__ void wclose(KArgs ka, lds_cf32* lbuf, const lds_cf32* ldnl, unsigned f, float rate,
                                     float scale, int t_off, float mx01, float m, float r, bool nan, bool open,
-                                    WDma nd) {
+                                    unsigned nd_f, unsigned nd_j, int nd_t, int nd_est, int nd_on, unsigned nd_fs,
+                                    unsigned nd_nest) {
+    // (the next unit's DMA as scalars: a struct argument would pass through
+    // the stack, i.e. scratch stores per call)
+    const WDma nd{nd_f, nd_j, nd_t, nd_est, nd_on, nd_fs, nd_nest};
     using W = WGeo<SF>;
     constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
@@ -1059,6 +1018,78 @@ __device__ __noinline__ void wclose(KArgs ka, lds_cf32* lbuf, const lds_cf32* ld
     }
     if (nd.on) wdma<SF>(A, buf, nd, lane);
 }
+
+// A frame's symbol outputs, collected in registers and stored 128 at a time
+// (lane t holds entries base + 2t and base + 2t + 1 as a u16 pair), the
+// sync symbols (the frame record's sw0, sw1) at the frame's end.  Stored
+// unit by unit, each 2-byte store (one to eight per unit) left a partly
+// written line that the streaming IQ evicted before its neighbours came:
+// ~32 B of HBM writes per 2-byte symbol (round 4's WRITE_SIZE, 13x the
+// results at SF 12).  Entries are stored only where a unit put one (data
+// symbols of frames whose estimate succeeded; store_symbol's rule).
+template <int SF>
+struct WOut {
+    unsigned acc = 0u, msk = 0u;  // per lane: the pair, its valid bits
+    unsigned sw = 0u, swm = 0u;   // wave-uniform: sw0 | sw1 << 16, valid bits
+    unsigned f = 0xffffffffu;     // frame (global index) ...
+    int base = 0;                 // ... and its data index of lane 0's first entry
+    __device__ __forceinline__ void flush(const DemodArgs& A, int lane) {
+        if (f != 0xffffffffu) {
+            bound_check(f, (long long)A.frames);
+            uint16_t* const row = A.syms + (unsigned long long)f * A.out_per_frame + (unsigned)base;
+            if (msk & 1u) {
+                bound_check(base + 2 * lane, (long long)A.out_per_frame);
+                row[2 * lane] = (uint16_t)acc;
+            }
+            if (msk & 2u) {
+                bound_check(base + 2 * lane + 1, (long long)A.out_per_frame);
+                row[2 * lane + 1] = (uint16_t)(acc >> 16);
+            }
+            if (lane == 0 && swm != 0u) {
+                if (swm == 3u) {
+                    *reinterpret_cast<unsigned*>(&A.meta[f].sw0) = sw;
+                } else {
+                    if (swm & 1u) A.meta[f].sw0 = (uint16_t)sw;
+                    if (swm & 2u) A.meta[f].sw1 = (uint16_t)(sw >> 16);
+                }
+            }
+        }
+        acc = msk = sw = swm = 0u;
+        f = 0xffffffffu;
+    }
+    // a symbol unit of frame fr whose half h holds symbol s0 + h; pk (lane
+    // h LPS): 0x10000 | the output when it is stored, else 0
+    __device__ __forceinline__ void put(const DemodArgs& A, unsigned fr, int s0, unsigned pk, int lane) {
+        constexpr int LPS = WGeo<SF>::LPS, SPW = WGeo<SF>::SPW;
+        const int o0 = s0 - 2;  // data index of half 0 (the frame has its sync symbols)
+        if (fr != f || o0 + SPW > base + 128) {
+            flush(A, lane);
+            f = fr;
+            base = (o0 > 0 ? o0 : 0) & ~63;
+        }
+#pragma unroll
+        for (int h = 0; h < (SPW < 2 ? SPW : 2); ++h) {
+            if (s0 + h < 2) {
+                const unsigned v = (unsigned)__builtin_amdgcn_readlane((int)pk, h * LPS);
+                if (v != 0u) {
+                    const int sh = 16 * (s0 + h);
+                    sw = (sw & ~(0xffffu << sh)) | ((v & 0xffffu) << sh);
+                    swm |= 1u << (s0 + h);
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int hh = base + 2 * lane + q - o0;  // (>= 2 for the sync halves' data index < 0)
+            const bool in = hh >= 0 && hh < SPW;
+            const unsigned v = (unsigned)__shfl((int)pk, in ? hh * LPS : 0, 64);
+            if (in && (v & 0x10000u)) {
+                acc = (acc & ~(0xffffu << (16 * q))) | ((v & 0xffffu) << (16 * q));
+                msk |= 1u << q;
+            }
+        }
+    }
+};
 
 // Timing experiments only (-DLPHY_PROFILE_PHASES, tools/ubench): per-wave
 // clock sums of the unit phases, added to A.counters[1..8] at the end.
@@ -1221,14 +1252,10 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     unsigned sp_fl = 0u;
     UnitResult ur0{0, 0, 0.0f, 0.0f, 0};  // SF 12: the first estimate unit's result
 
+    WOut<SF> wo;  // the frame's symbol outputs until they are stored
+
     WCursor cu = sch.first();
     WPH_DECL
-    if constexpr (!M0 && SPW == 1) {  // (SF 9-11: the estimate unit scans its own samples)
-        const float m = wscan2<SF, MODE>(ka, fglob(0), dnl, lane);
-        WFrame r = rec0;
-        r.mx = m;
-        rec0 = r;
-    }
     dma_unit(cu);
     while (sch.kind(cu) != kWDead) {
         const WCursor nx = sch.next(cu);
@@ -1397,11 +1424,13 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                 cgap = cert && !A.debug_recheck ? g : -1.0f;  // (DEBUG_RECHECK: tests)
             }
             const bool redo = c.ok && !(cgap >= 0.0f);
-            if (live && l == 0) {
+            {
                 const uint16_t out = redo ? kSymRecheck : (uint16_t)sym;
-                if (c.have_sync && c.s < 2) store_symbol(A, c, c.ok ? out : (uint16_t)0);
-                else if (c.ok) store_symbol(A, c, out);
-                if (redo) A.meta[c.f].status = kStatusRecheck;
+                const bool sync_sym = c.s < 2;  // (have_sync: set above)
+                const bool st = live && l == 0 && (sync_sym || c.ok);
+                wo.put(A, f, (int)(SPW * cu.j), st ? (0x10000u | (c.ok ? out : 0u)) : 0u, lane);
+                if (live && l == 0 && redo) A.meta[c.f].status = kStatusRecheck;
+                if (cu.phase == 3 && cu.j + 1 == sch.ND) wo.flush(A, lane);  // the frame's last unit
             }
             if (spec && c.ok) {
                 sp_mx = fmaxf(sp_mx, amax);
@@ -1426,7 +1455,11 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                 sp_mx = 0.0f;
                 sp_r = kBig;
                 sp_fl = 0u;
-                if (R.ok) wclose<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, f, R.rate, R.scale, R.t_off, R.mx, mm, rr, nan, open, dma_plan(nx));
+                if (R.ok) {
+                    const WDma nd = dma_plan(nx);
+                    wclose<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, f, R.rate, R.scale, R.t_off, R.mx, mm,
+                                     rr, nan, open, nd.f, nd.j, nd.t_off, nd.est, nd.on, nd.fstride, nd.nest);
+                }
             }
             WPH(6);
         } else {
@@ -1466,9 +1499,15 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                 }
             } else {
                 WFrame R0 = rec(k);
-                const WEstU eu =
-                    west_unit<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, R0.mx, SPW > 1, 1u);
+                // SF 12: symbol 0's unit normalises with its own max-abs m0 (the
+                // speculation that symbol 1 does not change the frame's scale:
+                // max-abs <= 1, no scaling, for any signal within the reference's
+                // [-1, 1] range), symbol 1's with max(m0, m1); a frame whose
+                // symbol 1 changes the scale runs symbol 0's unit again below
+                const float mx_in = (SPW > 1 || cu.j == 0) ? 0.0f : R0.mx;
+                const WEstU eu = west_unit<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, mx_in, true, 1u);
                 const UnitResult ur = eu.ur;
+                const float m_prev = R0.mx;
                 R0.mx = eu.mx;
                 lphy_frame_meta nm{};
                 nm.scale = 1.0f;
@@ -1480,8 +1519,18 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                     if (cu.j == 0) {
                         ur0 = ur;
                         fold_now = false;
+                        set_rec(k, R0);  // m0, for symbol 1's unit
                     } else {
                         ua = ur0;
+                        if constexpr (!M0) {
+                            const lphy_frame_meta n0 = norm_meta_hot(m_prev, true, A.no_scratch);
+                            if (nm.status == 0 && n0.status == 0 &&
+                                (n0.scale != nm.scale || n0.normalised != nm.normalised)) {
+                                wdma<SF>(A, buf, WDma{f, 0u, 0, 1, 1, 0u, 1u}, lane);
+                                wait_vm0();
+                                ua = west_unit<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, R0.mx, false, 1u).ur;
+                            }
+                        }
                     }
                 } else {  // the pair's second estimate unit from the upper half
                     ua = wur_from(ur, 0);
@@ -1510,18 +1559,10 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             dma_unit(nx);  // after the fold: a symbol unit's window needs the time shift
             WPH(6);
         }
-        // the two-symbol scan of the frame whose estimate comes next
-        // (WPH slot 7 from here to the next unit: the scan and the cursor)
-        if constexpr (!M0 && SPW == 1) {
-            if (sch.kind(nx) == kWEst && nx.j == 0 && nx.phase == 2) {
-                const unsigned kn = sch.frame(nx);
-                WFrame r = rec(kn);
-                r.mx = wscan2<SF, MODE>(ka, fglob(kn), dnl, lane);
-                set_rec(kn, r);
-            }
-        }
+        // (WPH slot 7 from here to the next unit: the cursor)
         cu = nx;
     }
+    wo.flush(A, lane);  // (every frame's last unit has stored it already)
     WPH(7);
     WPH_FLUSH(A)
 }
