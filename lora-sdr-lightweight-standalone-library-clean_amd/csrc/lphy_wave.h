@@ -49,6 +49,11 @@
 // rows padded by LPS entries) + the down-chirp (N entries): the whole
 // 160 KiB of a CU at SF 12, one 256-thread workgroup per CU.
 
+// cache policy of the IQ's LDS-DMA (timing experiments: 2 = nt)
+#ifndef LPHY_IQ_CPOL
+#define LPHY_IQ_CPOL 0
+#endif
+
 template <int SF>
 struct WGeo {
     static constexpr int N = 1 << SF;
@@ -470,10 +475,10 @@ __device__ __forceinline__ void wdma(const DemodArgs& A, cf32* buf, const WDma& 
         for (int r = 0; r < W::PPS; r += 4) {
             g_void* g = (g_void*)(src + 128 * r);
             lds_void* ld = (lds_void*)(buf + h * W::SS + 128 * r);
-            __builtin_amdgcn_global_load_lds(g, ld, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(g, ld, 16, 1024, 0);
-            __builtin_amdgcn_global_load_lds(g, ld, 16, 2048, 0);
-            __builtin_amdgcn_global_load_lds(g, ld, 16, 3072, 0);
+            __builtin_amdgcn_global_load_lds(g, ld, 16, 0, LPHY_IQ_CPOL);
+            __builtin_amdgcn_global_load_lds(g, ld, 16, 1024, LPHY_IQ_CPOL);
+            __builtin_amdgcn_global_load_lds(g, ld, 16, 2048, LPHY_IQ_CPOL);
+            __builtin_amdgcn_global_load_lds(g, ld, 16, 3072, LPHY_IQ_CPOL);
         }
     }
 }
