@@ -595,6 +595,23 @@ __device__ __forceinline__ void iq_check(const DemodArgs& A, unsigned long long 
     bound_check(off, (long long)A.frame_samples);
 }
 
+// k_frames' IQ loads (each sample read once, the estimate symbols twice):
+// non-temporal, so the stream does not evict the partly written output
+// lines and the tables from L2 (as k_wave's IQ DMA, lphy_wave.h
+// LPHY_IQ_CPOL).  Same-box A/B (profiles/r5/ab_iq_nt.txt): SF 8 fused
+// 0.999-1.012 -> 0.977-0.979 ms, SF 7 within noise; C1 WRITE_SIZE 33.0 ->
+// 12.6 MB per launch.  (-DLPHY_IQ_NT=0 for timing experiments only.)
+#ifndef LPHY_IQ_NT
+#define LPHY_IQ_NT 1
+#endif
+__device__ __forceinline__ cf32 ld_iq(const cf32* p) {
+#if LPHY_IQ_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
 __device__ __forceinline__ void store_symbol(const DemodArgs& A, const SymCtx& c, uint16_t idx) {
     bound_check(c.f, (long long)A.frames);
     if (c.have_sync && c.s < 2) {
@@ -1186,7 +1203,7 @@ __device__ __forceinline__ float stage_fast(cf32 (&v)[16], cf32 (&raw)[16], cons
             const int ce = first_pass_index<SF>(e, 0);
             bound_check((c.base & (N - 1)) + fl + ce, 2 * N);
             cf32 p = raw[e];
-            if constexpr (EARLY) raw[e] = nsrc[ce];  // the next tile's sample, as this one is consumed
+            if constexpr (EARLY) raw[e] = ld_iq(nsrc + ce);  // the next tile's sample, as this one is consumed
             if constexpr ((MODE & 3) != LPHY_MODE_DEMODULATE) {
                 if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) p = cmul(p, dl[ce]);
                 p = cscale(p, c.scale);
@@ -1202,7 +1219,7 @@ __device__ __forceinline__ float stage_fast(cf32 (&v)[16], cf32 (&raw)[16], cons
             bound_check((c.base & (N - 1)) + fl + ce, 2 * N);
             bound_check(fl + ce, N);
             cf32 p = raw[e];
-            if constexpr (EARLY) raw[e] = nsrc[ce];
+            if constexpr (EARLY) raw[e] = ld_iq(nsrc + ce);
             if constexpr ((MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE) p = cmul(p, dl[ce]);
             amax = max3_abs(amax, p.x, p.y);
             if constexpr (RLDS) {
@@ -1417,7 +1434,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
 #pragma unroll
         for (int e = 0; e < G::E; ++e) {
             iq_check(A, c.f, (long long)c.base + fl + first_pass_index<SF>(e, 0));
-            raw[e] = src[first_pass_index<SF>(e, 0)];
+            raw[e] = ld_iq(src + first_pass_index<SF>(e, 0));
         }
     }
     // speculative normalisation: the lane's running state for the two frames
@@ -1572,7 +1589,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
 #pragma unroll
                 for (int e = 0; e < G::E; ++e) {
                     iq_check(A, nc.f, (long long)nc.base + fl + first_pass_index<SF>(e, 0));
-                    raw[e] = lsrc[first_pass_index<SF>(e, 0)];
+                    raw[e] = ld_iq(lsrc + first_pass_index<SF>(e, 0));
                 }
             }
         }

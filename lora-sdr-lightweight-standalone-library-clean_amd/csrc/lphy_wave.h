@@ -49,9 +49,15 @@
 // rows padded by LPS entries) + the down-chirp (N entries): the whole
 // 160 KiB of a CU at SF 12, one 256-thread workgroup per CU.
 
-// cache policy of the IQ's LDS-DMA (timing experiments: 2 = nt)
+// cache policy of the IQ's LDS-DMA: nt (2), streaming. Every IQ line is
+// read once (twice for the estimate symbols), so it should not push the
+// twiddle table and the partly written output lines out of L2: same-box
+// A/B (profiles/r5/ab_iq_nt.txt) C2 1.63-1.69 -> 1.57-1.60 ms, FETCH
+// 1.044x -> 1.039x of the algorithmic bytes, WRITE 0.85 -> 0.66 MB (the
+// results exactly); SF 9 -1..2 %; sc1 (16): no change.  (-D for timing
+// experiments only.)
 #ifndef LPHY_IQ_CPOL
-#define LPHY_IQ_CPOL 0
+#define LPHY_IQ_CPOL 2
 #endif
 
 template <int SF>
