@@ -167,9 +167,13 @@ inline bool frames_fit(unsigned sf, unsigned osr, int est_units, size_t total) {
 // window, the certified rotation, and in modes 1/2 the speculative
 // normalisation.  Hann windows, LPHY_F_EXACT_ROTATION and the pre-scan
 // schedule stay on k_frames (SF 9-10) or the separate launches (SF 11-12).
+// smallest SF on k_wave (-D for timing experiments only)
+#ifndef LPHY_WAVE_MIN_SF
+#define LPHY_WAVE_MIN_SF 7
+#endif
 inline bool wave_fit(unsigned sf, unsigned osr, int window, int est_units, size_t total, int mode,
                      const DemodArgs& A) {
-    return sf >= 9 && sf <= 12 && osr == 1 && window == LPHY_WINDOW_NONE && est_units == 2 && total >= 2 &&
+    return sf >= LPHY_WAVE_MIN_SF && sf <= 12 && (sf >= 9 || total >= (size_t)(4096u >> sf)) && osr == 1 && window == LPHY_WINDOW_NONE && est_units == 2 && total >= 2 &&
            !A.exact_rotation && (mode == LPHY_MODE_DEMODULATE || A.spec);
 }
 
@@ -502,7 +506,10 @@ int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t f
     // (Measured alternative: the separate kernels pipelined over chunks on
     // two streams, prologue of chunk c+1 beside the symbol kernel of chunk
     // c: the co-running kernels slowed each other ~2x, 1.1x slower overall.)
-    const bool wfit = wave_fit(c->sf, c->osr, c->window, A.est_units, total, mode, A);
+    // (LPHY_F_FRAMES_KERNEL, test build: k_frames where k_wave would run -
+    // the SF 7-8 matrix-core tests)
+    const bool wfit = wave_fit(c->sf, c->osr, c->window, A.est_units, total, mode, A) &&
+                      !(flags & LPHY_F_FRAMES_KERNEL);
     const bool fused = (all || (stages & both) == both) && !(flags & LPHY_F_UNFUSED) &&
                        frames >= fused_min_frames(c) && (frames_fit(c->sf, c->osr, A.est_units, total) || wfit);
     A.wave = fused && (c->sf >= 11 || wfit) ? 1 : 0;

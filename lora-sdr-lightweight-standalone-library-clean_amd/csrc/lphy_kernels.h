@@ -2877,6 +2877,8 @@ int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symb
 // shared exchange buffers, were removed in round 5: with the Parseval
 // certificate and the grouped estimate units k_wave was faster at every SF,
 // DESIGN §4.9.)
+// SF 7-9 with at least SPW symbols per frame: units spanning frames
+// (WSchedSpan); SF 7-8 take k_wave only then (wave_fit).
 template <int SF, int MODE>
 int launch_wave_mode(const DemodArgs& A, hipStream_t st) {
     FrameArgs P{};
@@ -2885,9 +2887,20 @@ int launch_wave_mode(const DemodArgs& A, hipStream_t st) {
     const unsigned long long need = (A.frames + WGeo<SF>::WPB - 1) / WGeo<SF>::WPB;
     if (blocks > need) blocks = need;
     P.waves = (unsigned)(blocks * WGeo<SF>::WPB);
-    hipLaunchKernelGGL((k_wave<SF, MODE>), dim3((unsigned)blocks), dim3(256), 0, st, P);
-    HIP_OK(hipGetLastError());
-    return 0;
+    if constexpr (WGeo<SF>::SPW >= 8) {
+        if (A.total_syms >= (unsigned long long)WGeo<SF>::SPW) {
+            hipLaunchKernelGGL((k_wave<SF, MODE, true>), dim3((unsigned)blocks), dim3(256), 0, st, P);
+            HIP_OK(hipGetLastError());
+            return 0;
+        }
+    }
+    if constexpr (SF >= 9) {
+        hipLaunchKernelGGL((k_wave<SF, MODE, false>), dim3((unsigned)blocks), dim3(256), 0, st, P);
+        HIP_OK(hipGetLastError());
+        return 0;
+    } else {
+        return -ENOTSUP;  // (wave_fit: S >= SPW below SF 9)
+    }
 }
 
 template <int SF>
@@ -2903,7 +2916,7 @@ int launch_frames_sf(const DemodArgs& A, hipStream_t st) {
         (void)A; (void)st;
         return -ENOTSUP;
     } else {
-        if constexpr (SF >= 9) {  // the wave-per-symbol geometry down to 8 lanes per symbol
+        if constexpr (SF >= 7) {  // the wave-per-symbol geometry down to 2 lanes per symbol
             if (A.wave) {
                 switch (A.mode) {
                     case LPHY_MODE_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_DEMODULATE>(A, st);

@@ -23,8 +23,12 @@ enum lphy_test_flags {
                                    // marked "has open symbols" first; fused
                                    // kernels: every symbol left to k_post's
                                    // exact re-run (tests/test_gpu_concurrency.py)
+    LPHY_F_FRAMES_KERNEL = 1024u,  // SF 7-9: k_frames where k_wave would run
+                                   // (the matrix-core symbol tiles' tests,
+                                   // tests/test_gpu_certificate.py)
 };
-constexpr unsigned kTestFlags = LPHY_F_EXACT_ROTATION | 128u | LPHY_F_SCAN_FIRST | LPHY_F_DEBUG_RECHECK;
+constexpr unsigned kTestFlags =
+    LPHY_F_EXACT_ROTATION | 128u | LPHY_F_SCAN_FIRST | LPHY_F_DEBUG_RECHECK | LPHY_F_FRAMES_KERNEL;
 
 // Test build only: LPHY_FUSED_MIN_FRAMES sets the process default of the
 // smallest batch the fused kernels take (the lora_phy:: probes run once with

@@ -69,9 +69,12 @@ struct WGeo {
     // frames per estimate unit: SF 9-10 put EPU frames' two estimate symbols
     // in one unit (halves 2j, 2j + 1: frame j), SF 11-12 one frame's
     static constexpr int EPU = SPW >= 4 ? SPW / 2 : 1;
+    // frame records in the per-wave LDS ring (EPU > 1): the group in
+    // demodulation and the next one
+    static constexpr int RING = EPU > 1 ? (2 * EPU > 8 ? 2 * EPU : 8) : 1;
     static constexpr int L = (SF + 1) / 2;       // KISS stages (radix 4, a last radix 2 for odd SF)
     static constexpr int PPS = N / 128;   // LDS-DMA pieces (1 KiB) per symbol
-    static_assert(PPS % 4 == 0, "LDS-DMA in groups of four pieces");
+    static_assert(PPS < 4 || PPS % 4 == 0, "LDS-DMA in groups of four pieces (SF 7-8: one, two)");
     // symbol stride in the wave's buffer: below 32 lanes per symbol a row of
     // LPS entries shifts the next symbol's banks (conflict-free exchange
     // reads and staging reads across the symbols of one lane group)
@@ -422,29 +425,21 @@ __device__ __forceinline__ void wexchange(cf32 (&v)[64], cf32* buf, int h, int l
     for (int Bp = 0; Bp < 64; ++Bp) v[Bp] = lds_ld(buf, rb + ((Bp * W::LPS) << 3) + ((l ^ W::sw(Bp)) << 3));
 }
 
-// One unit's LDS-DMA: frame f, unit index j, the frame's time shift; est:
-// the estimate unit (SF 12: symbol j; below: symbols 0 and 1 in halves 0
-// and 1, the other halves load symbol 1 again); on = 0: no unit.
+// One unit's LDS-DMA.  Symbol unit: frame f's symbols s0, s0 + 1, ... (time
+// shift t_off) from half 0 up to the frame's end, then (units spanning
+// frames, SF 7-9) n1 halves of frame f1's symbols 0, 1, ... (shift t1).
+// Estimate unit (est): SF 12 symbol s0 of frame f; below, the EPU frames
+// f + j fstride, j < nest, symbols 0 and 1 in halves 2j, 2j + 1.  on = 0:
+// no unit.
 struct WDma {
-    unsigned f, j;
+    unsigned f, s0;
     int t_off;
     int est, on;
-    unsigned fstride, nest;  // estimate units: the group's frames f + j fstride, j < nest (EPU > 1)
+    unsigned fstride, nest;
+    unsigned f1;
+    int t1;
+    unsigned n1;
 };
-
-// Window start of symbol s under time shift t (LoRaDemod.cpp:144-150, as
-// sym_ctx for osr 1).
-__device__ __forceinline__ unsigned wwin(const DemodArgs& A, unsigned s, int t, unsigned N) {
-    const unsigned count = (unsigned)A.frame_samples;
-    unsigned base = s * N;
-    if (t > 0) {
-        if (base + N <= count && (unsigned)t <= count - N - base) base += (unsigned)t;
-    } else if (t < 0) {
-        const unsigned off = 0u - (unsigned)t;
-        if (off <= base) base -= off;
-    }
-    return base;
-}
 
 // LDS-DMA of one unit's windows into the wave's buffer: symbol h of the
 // unit at h SS.  Halves without a symbol (an estimate unit's halves past the
@@ -458,35 +453,90 @@ __device__ __forceinline__ void wdma(const DemodArgs& A, cf32* buf, const WDma& 
     typedef __attribute__((address_space(3))) void lds_void;
     typedef __attribute__((address_space(1))) const void g_void;
     const unsigned S = (unsigned)A.total_syms;
-    // (a loop, not unrolled: the halves' wave-uniform addresses would
-    // otherwise all be live at once and spill SGPRs)
-#pragma unroll 1
-    for (int h = 0; h < W::SPW; ++h) {
-        unsigned base, fr = d.f;
-        if (d.est) {
-            // SF 12: symbol j; below: half h holds symbol h & 1 of the
-            // group's frame h >> 1
-            if (W::SPW > 1 && (unsigned)(h >> 1) >= d.nest) break;
-            base = (W::SPW == 1 ? d.j : (unsigned)(h & 1)) * (unsigned)W::N;
-            fr = d.f + (unsigned)(h >> 1) * d.fstride;
-        } else {
-            const unsigned sy = (unsigned)W::SPW * d.j + (unsigned)h;
-            if (sy >= S) break;  // (wave-uniform: halves in order)
-            base = wwin(A, sy, d.t_off, (unsigned)W::N);
-        }
-        const cf32* src = A.iq + (unsigned long long)fr * A.frame_samples + base + 2 * lane;
+    // one symbol window (src: this lane's first sample of it) into the
+    // buffer at dst
+    auto piece = [&](const cf32* src, cf32* dst) __attribute__((always_inline)) {
         // four 1 KiB pieces per base: the instruction's immediate offset moves
-        // the source and the LDS destination alike (tools/ubench/glds_align)
+        // the source and the LDS destination alike (tools/ubench/glds_align);
+        // SF 7-8: one or two pieces per symbol
 #pragma unroll
         for (int r = 0; r < W::PPS; r += 4) {
             g_void* g = (g_void*)(src + 128 * r);
-            lds_void* ld = (lds_void*)(buf + h * W::SS + 128 * r);
+            lds_void* ld = (lds_void*)(dst + 128 * r);
             __builtin_amdgcn_global_load_lds(g, ld, 16, 0, LPHY_IQ_CPOL);
-            __builtin_amdgcn_global_load_lds(g, ld, 16, 1024, LPHY_IQ_CPOL);
-            __builtin_amdgcn_global_load_lds(g, ld, 16, 2048, LPHY_IQ_CPOL);
-            __builtin_amdgcn_global_load_lds(g, ld, 16, 3072, LPHY_IQ_CPOL);
+            if constexpr (W::PPS >= 2) __builtin_amdgcn_global_load_lds(g, ld, 16, 1024, LPHY_IQ_CPOL);
+            if constexpr (W::PPS >= 4) {
+                __builtin_amdgcn_global_load_lds(g, ld, 16, 2048, LPHY_IQ_CPOL);
+                __builtin_amdgcn_global_load_lds(g, ld, 16, 3072, LPHY_IQ_CPOL);
+            }
         }
+    };
+    // (loops, not unrolled: the halves' wave-uniform addresses would
+    // otherwise all be live at once and spill SGPRs.  The frame's address and
+    // the time shift's range are hoisted and the windows of a run of shifted
+    // symbols advance by N, so below 8 lanes per symbol, where a unit has 16
+    // or 32 halves, a half costs a few instructions.)
+    if (d.est) {
+        // SF 12: symbol j; below: half h holds symbol h & 1 of the group's
+        // frame h >> 1
+        if constexpr (W::SPW == 1) {
+            piece(A.iq + (unsigned long long)d.f * A.frame_samples + d.s0 * (unsigned)W::N + 2 * lane, buf);
+        } else {
+            const unsigned ne = d.nest < (unsigned)(W::SPW / 2) ? d.nest : (unsigned)(W::SPW / 2);
+#pragma unroll 1
+            for (unsigned jf = 0; jf < ne; ++jf) {
+                const cf32* src = A.iq + (unsigned long long)(d.f + jf * d.fstride) * A.frame_samples + 2 * lane;
+                piece(src, buf + 2 * jf * W::SS);
+                piece(src + W::N, buf + (2 * jf + 1) * W::SS);
+            }
+        }
+        return;
     }
+    const unsigned N = (unsigned)W::N, count = (unsigned)A.frame_samples;
+    if constexpr (W::SPW == 1) {  // SF 12: one window (wwin, LoRaDemod.cpp:144-150)
+        if (d.s0 >= S) return;
+        const int t = d.t_off;
+        unsigned base = d.s0 * N;
+        if (t > 0) {
+            if (base + N <= count && (unsigned)t <= count - N - base) base += (unsigned)t;
+        } else if (t < 0) {
+            const unsigned off = 0u - (unsigned)t;
+            if (off <= base) base -= off;
+        }
+        piece(A.iq + (unsigned long long)d.f * A.frame_samples + base + 2 * lane, buf);
+        return;
+    }
+    // symbols sy0 .. sy0 + nh - 1 of frame f (shift t) into halves h0, h0 + 1, ...
+    auto run = [&](unsigned f, int t, unsigned sy0, unsigned nh, unsigned h0) __attribute__((always_inline)) {
+        const cf32* fsrc = A.iq + (unsigned long long)f * A.frame_samples + 2 * lane;
+        // the shifted symbols (as above): s_lo .. s_hi
+        unsigned s_lo = 0u, s_hi = 0xffffffffu;
+        if (t > 0) {
+            if (count >= N + (unsigned)t) s_hi = (count - N - (unsigned)t) / N;
+            else s_lo = 1u, s_hi = 0u;  // (no shifted window fits)
+        } else if (t < 0) {
+            s_lo = ((0u - (unsigned)t) + N - 1u) / N;
+        }
+        // halves [0, ha) unshifted, [ha, hb) shifted, [hb, nh) unshifted
+        const unsigned ha = s_lo > sy0 ? (s_lo - sy0 < nh ? s_lo - sy0 : nh) : 0u;
+        const unsigned hb0 = s_hi >= sy0 ? (s_hi - sy0 < nh ? s_hi - sy0 + 1u : nh) : 0u;  // (s_hi may be ~0u)
+        const unsigned hb = hb0 > ha ? hb0 : ha;
+        cf32* const b0 = buf + h0 * W::SS;
+        unsigned h = 0;
+#pragma unroll 1
+        for (; h < ha; ++h) piece(fsrc + (sy0 + h) * N, b0 + h * W::SS);
+        {
+            const cf32* src = fsrc + (sy0 + h) * N + t;
+            cf32* dst = b0 + h * W::SS;
+#pragma unroll 1
+            for (; h < hb; ++h, src += N, dst += W::SS) piece(src, dst);
+        }
+#pragma unroll 1
+        for (; h < nh; ++h) piece(fsrc + (sy0 + h) * N, b0 + h * W::SS);
+    };
+    const unsigned nh0 = d.s0 < S ? (S - d.s0 < (unsigned)W::SPW ? S - d.s0 : (unsigned)W::SPW) : 0u;
+    run(d.f, d.t_off, d.s0, nh0, 0u);
+    if (d.n1) run(d.f1, d.t1, 0u, d.n1, nh0);
 }
 
 // Keyed top two (see team_argmax2_keyed_first) merged over each symbol's
@@ -511,9 +561,19 @@ __device__ __forceinline__ void top2_add(unsigned& K1, unsigned& K2, unsigned o1
 }
 template <int LPS>
 __device__ __forceinline__ void wave_top2_merge(unsigned k1, unsigned k2, int h, unsigned& K1, unsigned& K2) {
-    static_assert(LPS == 8 || LPS == 16 || LPS == 32 || LPS == 64, "8 to 64 lanes per symbol");
+    static_assert(LPS >= 2 && LPS <= 64 && (LPS & (LPS - 1)) == 0, "2 to 64 lanes per symbol");
     top2_add(k1, k2, dpp_u32<0xB1>(k1), dpp_u32<0xB1>(k2));    // quad_perm [1,0,3,2]
+    if constexpr (LPS == 2) {
+        K1 = k1;
+        K2 = k2;
+        return;
+    }
     top2_add(k1, k2, dpp_u32<0x4E>(k1), dpp_u32<0x4E>(k2));    // quad_perm [2,3,0,1]
+    if constexpr (LPS == 4) {
+        K1 = k1;
+        K2 = k2;
+        return;
+    }
     top2_add(k1, k2, dpp_u32<0x141>(k1), dpp_u32<0x141>(k2));  // row_half_mirror
     if constexpr (LPS == 8) {  // every lane holds its 8-lane symbol's top two
         K1 = k1;
@@ -557,9 +617,11 @@ __device__ __forceinline__ void wdma_table(const cf32* tw, cf32* buf, int lane) 
         g_void* g = (g_void*)(tw + 128 * r + 2 * lane);
         lds_void* d = (lds_void*)(buf + 128 * r);
         __builtin_amdgcn_global_load_lds(g, d, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(g, d, 16, 1024, 0);
-        __builtin_amdgcn_global_load_lds(g, d, 16, 2048, 0);
-        __builtin_amdgcn_global_load_lds(g, d, 16, 3072, 0);
+        if constexpr (W::PPS >= 2) __builtin_amdgcn_global_load_lds(g, d, 16, 1024, 0);
+        if constexpr (W::PPS >= 4) {
+            __builtin_amdgcn_global_load_lds(g, d, 16, 2048, 0);
+            __builtin_amdgcn_global_load_lds(g, d, 16, 3072, 0);
+        }
     }
 }
 __device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); } // lgkmcnt(0)
@@ -600,17 +662,31 @@ __device__ __forceinline__ UnitResult wunit_result(const cf32 (&v)[64], int h, i
     const int idx = best.i;
     const int il = idx > 0 ? idx - 1 : N - 1, ir = idx < N - 1 ? idx + 1 : 0;
     // the lanes holding bins il, idx, ir pick them; three broadcasts
-    int e = -1;
-    if (l == (il & (W::LPS - 1))) e = il / W::LPS;
-    if (l == (idx & (W::LPS - 1))) e = idx / W::LPS;
-    if (l == (ir & (W::LPS - 1))) e = ir / W::LPS;
-    const cf32 mine = wpick(v, e);
     const int hb = h * W::LPS;
-    auto get = [&](int bin) {
-        const int src = hb + (bin & (W::LPS - 1));
-        return cf32{__shfl(mine.x, src, 64), __shfl(mine.y, src, 64)};
-    };
-    const cf32 lb = get(il), bn = get(idx), rb = get(ir);
+    cf32 lb, bn, rb;
+    if constexpr (W::LPS >= 4) {  // three distinct lanes
+        int e = -1;
+        if (l == (il & (W::LPS - 1))) e = il / W::LPS;
+        if (l == (idx & (W::LPS - 1))) e = idx / W::LPS;
+        if (l == (ir & (W::LPS - 1))) e = ir / W::LPS;
+        const cf32 mine = wpick(v, e);
+        auto get = [&](int bin) {
+            const int src = hb + (bin & (W::LPS - 1));
+            return cf32{__shfl(mine.x, src, 64), __shfl(mine.y, src, 64)};
+        };
+        lb = get(il);
+        bn = get(idx);
+        rb = get(ir);
+    } else {  // SF 7 (2 lanes per symbol): il and ir share a lane
+        auto get = [&](int bin) {
+            const cf32 mine = wpick(v, l == (bin & (W::LPS - 1)) ? bin / W::LPS : -1);
+            const int src = hb + (bin & (W::LPS - 1));
+            return cf32{__shfl(mine.x, src, 64), __shfl(mine.y, src, 64)};
+        };
+        lb = get(il);
+        bn = get(idx);
+        rb = get(ir);
+    }
     (void)lane;
     UnitResult r;
     const float mv = best.v > 0.0f ? best.v : 0.0f;
@@ -690,10 +766,10 @@ __device__ __forceinline__ float dpp_f32(float v) {
 // Sum over the LPS lanes of each symbol (every lane gets its symbol's sum).
 template <int LPS>
 __device__ __forceinline__ float half_sum(float x) {
-    static_assert(LPS == 8 || LPS == 16 || LPS == 32 || LPS == 64, "8 to 64 lanes per symbol");
-    x = x + dpp_f32<0xB1>(x);   // quad_perm [1,0,3,2]
-    x = x + dpp_f32<0x4E>(x);   // quad_perm [2,3,0,1]
-    x = x + dpp_f32<0x141>(x);  // row_half_mirror: the 8-lane sum
+    static_assert(LPS >= 2 && LPS <= 64 && (LPS & (LPS - 1)) == 0, "2 to 64 lanes per symbol");
+    x = x + dpp_f32<0xB1>(x);                             // quad_perm [1,0,3,2]
+    if constexpr (LPS >= 4) x = x + dpp_f32<0x4E>(x);     // quad_perm [2,3,0,1]
+    if constexpr (LPS >= 8) x = x + dpp_f32<0x141>(x);    // row_half_mirror: the 8-lane sum
     if constexpr (LPS >= 16) x = x + dpp_f32<0x140>(x);  // row_mirror: 16
     if constexpr (LPS >= 32) x = x + __shfl_xor(x, 16, 64);
     if constexpr (LPS >= 64) x = x + __shfl_xor(x, 32, 64);
@@ -963,11 +1039,7 @@ __device__ __forceinline__ WRot wrot(float rate, float scale) {
 template <int SF, int MODE>
 __device__ __forceinline__ void wclose(KArgs ka, lds_cf32* lbuf, const lds_cf32* ldnl, unsigned f, float rate,
                                     float scale, int t_off, float mx01, float m, float r, bool nan, bool open,
-                                    unsigned nd_f, unsigned nd_j, int nd_t, int nd_est, int nd_on, unsigned nd_fs,
-                                    unsigned nd_nest) {
-    // (the next unit's DMA as scalars: a struct argument would pass through
-    // the stack, i.e. scratch stores per call)
-    const WDma nd{nd_f, nd_j, nd_t, nd_est, nd_on, nd_fs, nd_nest};
+                                    const WDma& nd) {
     using W = WGeo<SF>;
     constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
@@ -1068,7 +1140,8 @@ struct WOut {
         acc = msk = sw = swm = 0u;
         f = 0xffffffffu;
     }
-    // a symbol unit of frame fr whose half h holds symbol s0 + h; pk (lane
+    // a symbol unit whose half h holds symbol s0 + h of frame fr (s0 < 0:
+    // the halves before -s0 hold another frame's, with pk 0); pk (lane
     // h LPS): 0x10000 | the output when it is stored, else 0
     __device__ __forceinline__ void put(const DemodArgs& A, unsigned fr, int s0, unsigned pk, int lane) {
         constexpr int LPS = WGeo<SF>::LPS, SPW = WGeo<SF>::SPW;
@@ -1079,13 +1152,13 @@ struct WOut {
             base = (o0 > 0 ? o0 : 0) & ~63;
         }
 #pragma unroll
-        for (int h = 0; h < (SPW < 2 ? SPW : 2); ++h) {
-            if (s0 + h < 2) {
-                const unsigned v = (unsigned)__builtin_amdgcn_readlane((int)pk, h * LPS);
+        for (int i = 0; i < 2; ++i) {  // sync symbol i: half i - s0
+            const int hs = i - s0;
+            if (hs >= 0 && hs < SPW) {
+                const unsigned v = (unsigned)__builtin_amdgcn_readlane((int)pk, hs * LPS);
                 if (v != 0u) {
-                    const int sh = 16 * (s0 + h);
-                    sw = (sw & ~(0xffffu << sh)) | ((v & 0xffffu) << sh);
-                    swm |= 1u << (s0 + h);
+                    sw = (sw & ~(0xffffu << (16 * i))) | ((v & 0xffffu) << (16 * i));
+                    swm |= 1u << i;
                 }
             }
         }
@@ -1129,6 +1202,7 @@ enum : int { kWDead = 0, kWEst = 1, kWSym = 2 };
 struct WCursor {
     int phase;      // 0: E(0); 1: D(k) before E(k+1); 2: E(k+1) (frames k+1 .. k+EPU); 3: D(k) after; 4: done
     unsigned k, j;  // frame (wave-local) of the D units; unit index within the phase
+    unsigned k0, s0;  // (units spanning frames: the unit's first frame and symbol)
 };
 
 template <int SF>
@@ -1161,6 +1235,45 @@ struct WSched {
     __device__ __forceinline__ unsigned frame(const WCursor& c) const { return c.phase == 2 ? c.k + 1 : c.k; }
 };
 
+// Units spanning frames (SF 7-9, S >= SPW symbols per frame): the wave's
+// frames are one stream of nk S symbols, symbol unit j holds stream symbols
+// SPW j .. SPW j + SPW - 1 (at most two frames: the end of frame k0 and the
+// start of k0 + 1), so no half idles at a frame's end (SF 7: 66 symbols in
+// 2.06 units instead of 3).  The estimate unit of group g (frames g EPU ..
+// g EPU + EPU - 1) runs two symbol units before the first one that reaches
+// the group, as in WSched.  Cursor: phase 2 estimate unit of group k, phase
+// 1 symbol unit j (first frame k0, first symbol s0), phase 4 done.
+template <int SF>
+struct WSchedSpan {
+    unsigned nk, S, NDT, NG;
+    __device__ __forceinline__ unsigned jE(unsigned g) const {
+        if (g == 0) return 0u;
+        const unsigned jf = (unsigned)(((unsigned long long)g * (unsigned)WGeo<SF>::EPU * S) / (unsigned)WGeo<SF>::SPW);
+        return jf >= 2u ? jf - 2u : 0u;
+    }
+    __device__ __forceinline__ void settle(WCursor& c) const {
+        c.phase = (c.k < NG && c.j >= jE(c.k)) ? 2 : (c.j < NDT ? 1 : 4);
+    }
+    __device__ __forceinline__ WCursor first() const { WCursor c{0, 0, 0, 0, 0}; settle(c); return c; }
+    __device__ __forceinline__ WCursor next(WCursor c) const {
+        if (c.phase == 2) {
+            ++c.k;
+        } else {
+            ++c.j;
+            c.s0 += (unsigned)WGeo<SF>::SPW;
+            if (c.s0 >= S) { c.s0 -= S; ++c.k0; }  // (SPW <= S)
+        }
+        settle(c);
+        return c;
+    }
+    __device__ __forceinline__ int kind(const WCursor& c) const {
+        return c.phase == 4 ? kWDead : c.phase == 2 ? kWEst : kWSym;
+    }
+    __device__ __forceinline__ unsigned frame(const WCursor& c) const {
+        return c.phase == 2 ? c.k * (unsigned)WGeo<SF>::EPU : c.k0;
+    }
+};
+
 // Frame record the symbol units read (wave-uniform), kept per wave-local
 // frame parity: frame k's record is written by its fold, while frame k - 1's
 // symbol units still run.
@@ -1170,10 +1283,11 @@ struct WFrame {
     int ok;                 // estimate folded, status 0
 };
 
-template <int SF, int MODE>
+template <int SF, int MODE, bool SPAN = false>
 __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     using W = WGeo<SF>;
     constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
+    static_assert(!SPAN || (SPW >= 8 && W::EPU >= 3), "units spanning frames: SF 7-9");
     constexpr bool M0 = (MODE & 3) == LPHY_MODE_DEMODULATE;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     constexpr bool DN = (MODE & 3) != LPHY_MODE_LORA_DEMODULATE;  // down-chirp used
@@ -1182,7 +1296,11 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     // one LDS block: the down-chirp at offset 0 (its wrapped index is then
     // the byte address itself), the waves' buffers after it
     __shared__ cf32 lds_all[(DN ? N : 0) + W::WPB * W::BUF];
-    __shared__ WFrame frings[W::WPB][W::EPU > 1 ? 8 : 1];  // (EPU > 1: the frame records)
+    __shared__ WFrame frings[W::WPB][W::RING];  // (EPU > 1: the frame records)
+    // SPAN: the rotation tables of the (at most two) frames of a unit, by
+    // frame parity: [scale] e^{j rate i}, i < 8 LPS, then e^{j rate 8 LPS a}
+    constexpr int RT = 8 * LPS + 8;
+    __shared__ cf32 rtabs[SPAN ? W::WPB : 1][2][SPAN ? RT : 1];
     cf32* const dnl = lds_all;
     cf32 (*const sbuf)[W::BUF] = reinterpret_cast<cf32 (*)[W::BUF]>(lds_all + (DN ? N : 0));
 
@@ -1202,10 +1320,17 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     const unsigned Wn = P.waves;
     const unsigned w = blockIdx.x * W::WPB + wv;
     if (w >= nframes) return;
-    WSched<SF> sch;
-    sch.nk = (nframes - 1 - w) / Wn + 1;
-    sch.ND = (S + SPW - 1) / SPW;
-    sch.p = sch.ND >= 2 ? sch.ND - 2 : 0;
+    typename std::conditional<SPAN, WSchedSpan<SF>, WSched<SF>>::type sch;
+    if constexpr (SPAN) {
+        sch.nk = (nframes - 1 - w) / Wn + 1;
+        sch.S = S;
+        sch.NDT = (sch.nk * S + SPW - 1) / SPW;  // (nk S < 2^32: lphy_hip_demod_batch's limit)
+        sch.NG = (sch.nk + W::EPU - 1) / W::EPU;
+    } else {
+        sch.nk = (nframes - 1 - w) / Wn + 1;
+        sch.ND = (S + SPW - 1) / SPW;
+        sch.p = sch.ND >= 2 ? sch.ND - 2 : 0;
+    }
     const bool spec = !M0 && A.spec != 0;
 
     WTw<SF> T;
@@ -1219,7 +1344,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     lds_frame* const ring = (lds_frame*)frings[wv];
     auto rec = [&](unsigned k) -> WFrame {
         if constexpr (W::EPU > 1) {
-            const lds_frame& q = ring[k & 7u];
+            const lds_frame& q = ring[k & (unsigned)(W::RING - 1)];
             return WFrame{q.rate, q.scale, q.mx, q.t_off, q.ok};
         } else {
             return (k & 1) ? rec1 : rec0;
@@ -1232,16 +1357,27 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     auto fglob = [&](unsigned k) { return w + k * Wn; };
     // the LDS-DMA of unit c: its frame, unit index and the frame's time shift
     auto dma_plan = [&](const WCursor& c) {
-        WDma d{0u, 0u, 0, 0, 0, Wn, 1u};
+        WDma d{0u, 0u, 0, 0, 0, Wn, 1u, 0u, 0, 0u};
         const int kd = sch.kind(c);
         if (kd == kWDead) return d;
         const unsigned kf = sch.frame(c);
         d.f = fglob(kf);
-        d.j = c.j;
+        d.s0 = kd == kWEst || SPAN ? c.j : (unsigned)SPW * c.j;
         d.on = 1;
         d.est = kd == kWEst ? 1 : 0;
         d.nest = (sch.nk - kf) < (unsigned)W::EPU ? (sch.nk - kf) : (unsigned)W::EPU;
         if (kd != kWEst) d.t_off = rec(kf).t_off;
+        if constexpr (SPAN) {
+            if (kd == kWSym) {
+                d.s0 = c.s0;
+                const unsigned n0 = S - c.s0 < (unsigned)SPW ? S - c.s0 : (unsigned)SPW;
+                if (n0 < (unsigned)SPW && kf + 1 < sch.nk) {
+                    d.f1 = fglob(kf + 1);
+                    d.t1 = rec(kf + 1).t_off;
+                    d.n1 = (unsigned)SPW - n0;
+                }
+            }
+        }
         return d;
     };
     auto dma_unit = [&](const WCursor& c) {
@@ -1261,6 +1397,9 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     constexpr float kBig = 3.0e38f;
     float sp_mx = 0.0f, sp_r = kBig;
     unsigned sp_fl = 0u;
+    float sp_mx1 = 0.0f, sp_r1 = kBig;  // (SPAN: the odd frames')
+    unsigned sp_fl1 = 0u;
+    unsigned tab0 = 0xffffffffu, tab1 = 0xffffffffu;  // (SPAN: the frames in rtabs)
     UnitResult ur0{0, 0, 0.0f, 0.0f, 0};  // SF 12: the first estimate unit's result
 
     WOut<SF> wo;  // the frame's symbol outputs until they are stored
@@ -1278,27 +1417,76 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
 #endif
         WPH(0);
         if (sch.kind(cu) == kWSym) {
-            const WFrame R = rec(k);
-            if (k != rot_frame) {
-                rot_frame = k;
-                pv_on = true;
-                const WRot rt = wrot<SF, MODE>(R.rate, R.scale);
+            const WFrame R0 = rec(k);
+            WFrame R = R0;      // this lane's frame record (SPAN: frame k or k + 1)
+            unsigned s, fh = f;  // this lane's symbol and frame (global)
+            bool live;
+            bool second = false;  // SPAN: the lane's half is in frame k + 1
+            unsigned n0 = (unsigned)SPW;
+            bool two = false;
+            if constexpr (SPAN) {
+                n0 = S - cu.s0 < (unsigned)SPW ? S - cu.s0 : (unsigned)SPW;
+                two = n0 < (unsigned)SPW && k + 1 < sch.nk;
+                const WFrame R1 = two ? rec(k + 1) : R0;
+                if (k != rot_frame) {
+                    rot_frame = k;
+                    pv_on = true;
+                }
+                // the rotation tables of frames k and k + 1, built once per
+                // frame (by parity) by the whole wave: the wrot values
+                auto ensure = [&](unsigned kk, const WFrame& Rk) __attribute__((always_inline)) {
+                    if (((kk & 1u) ? tab1 : tab0) == kk) return;
+                    if (kk & 1u) tab1 = kk;
+                    else tab0 = kk;
+                    lds_cf32* tb = (lds_cf32*)rtabs[wv][kk & 1u];
+#pragma unroll 1
+                    for (int i = lane; i < RT; i += 64) {
+                        const bool qp = i < 8 * LPS;
+                        float sn, cs;
+                        lphy_libm::sincosf_exact(Rk.rate * (float)(qp ? i : 8 * LPS * (i - 8 * LPS)), &sn, &cs);
+                        cf32 t = cf32{cs, sn};
+                        if constexpr (!M0) {
+                            if (qp) t = cscale(t, Rk.scale);
+                        }
+                        tb[i] = t;
+                    }
+                };
+                ensure(k, R0);
+                if (two) ensure(k + 1, R1);
+                second = (unsigned)h >= n0;
+                s = second ? (unsigned)h - n0 : cu.s0 + (unsigned)h;
+                live = !second || two;
+                if (second && two) {
+                    R = R1;
+                    fh = fglob(k + 1);
+                }
+                const lds_cf32* tb = (const lds_cf32*)rtabs[wv][(k + (second ? 1u : 0u)) & 1u];
 #pragma unroll
-                for (int b = 0; b < 8; ++b) Qr[b] = rt.q[b];
+                for (int b = 0; b < 8; ++b) Qr[b] = tb[l + LPS * b];
 #pragma unroll
-                for (int a = 0; a < 8; ++a)
-                    Pr[a] = cf32{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(rt.p.x), a)),
-                                 __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rt.p.y), a))};
+                for (int a = 0; a < 8; ++a) Pr[a] = tb[8 * LPS + a];
+            } else {
+                if (k != rot_frame) {
+                    rot_frame = k;
+                    pv_on = true;
+                    const WRot rt = wrot<SF, MODE>(R.rate, R.scale);
+#pragma unroll
+                    for (int b = 0; b < 8; ++b) Qr[b] = rt.q[b];
+#pragma unroll
+                    for (int a = 0; a < 8; ++a)
+                        Pr[a] = cf32{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(rt.p.x), a)),
+                                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rt.p.y), a))};
+                }
+                s = SPW * cu.j + (unsigned)h;
+                live = s < S;
             }
-            const unsigned s = SPW * cu.j + (unsigned)h;
-            const bool live = s < S;
             lphy_frame_meta m{};
             m.rate = R.rate;
             m.scale = R.scale;
             m.t_off = R.t_off;
             m.status = R.ok ? 0 : -1;
             m.have_sync = 1;
-            const SymCtx c = sym_ctx(A, f, live ? s : 0u, live, N, m);
+            const SymCtx c = sym_ctx(A, fh, live ? s : 0u, live, N, m);
             // staging: [exact dechirp,] certified rotation, from the LDS copy
             float amax = 0.0f;
             const int rb = (h * W::SS + l) << 3;
@@ -1439,37 +1627,69 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                 const uint16_t out = redo ? kSymRecheck : (uint16_t)sym;
                 const bool sync_sym = c.s < 2;  // (have_sync: set above)
                 const bool st = live && l == 0 && (sync_sym || c.ok);
-                wo.put(A, f, (int)(SPW * cu.j), st ? (0x10000u | (c.ok ? out : 0u)) : 0u, lane);
+                const unsigned pk = st ? (0x10000u | (c.ok ? out : 0u)) : 0u;
+                if constexpr (SPAN) {
+                    wo.put(A, f, (int)cu.s0, second ? 0u : pk, lane);
+                    if (two) wo.put(A, fglob(k + 1), -(int)n0, second ? pk : 0u, lane);
+                } else {
+                    wo.put(A, f, (int)(SPW * cu.j), pk, lane);
+                }
                 if (live && l == 0 && redo) A.meta[c.f].status = kStatusRecheck;
-                if (cu.phase == 3 && cu.j + 1 == sch.ND) wo.flush(A, lane);  // the frame's last unit
+                if constexpr (!SPAN) {
+                    if (cu.phase == 3 && cu.j + 1 == sch.ND) wo.flush(A, lane);  // the frame's last unit
+                }
             }
             if (spec && c.ok) {
-                sp_mx = fmaxf(sp_mx, amax);
+                // (SPAN: the state of the lane's frame, by parity)
+                const bool p1 = SPAN && (((k + (second ? 1u : 0u)) & 1u) != 0u);
+                float smx = p1 ? sp_mx1 : sp_mx, sr = p1 ? sp_r1 : sp_r;
+                unsigned sfl = p1 ? sp_fl1 : sp_fl;
+                smx = fmaxf(smx, amax);
                 const cf32 q = v[0] * v[0];
                 const float q2 = q.x + q.y;
-                if (!(q2 == q2)) sp_fl |= 1u;  // a NaN sample reaches every bin
+                if (!(q2 == q2)) sfl |= 1u;  // a NaN sample reaches every bin
                 if (l == 0) {
-                    if (redo) sp_fl |= 2u;
-                    else sp_r = fminf(sp_r, cgap * __builtin_amdgcn_rcpf(cb1) * (1.0f - 4.0f * kU));
+                    if (redo) sfl |= 2u;
+                    else sr = fminf(sr, cgap * __builtin_amdgcn_rcpf(cb1) * (1.0f - 4.0f * kU));
+                }
+                if (p1) {
+                    sp_mx1 = smx;
+                    sp_r1 = sr;
+                    sp_fl1 = sfl;
+                } else {
+                    sp_mx = smx;
+                    sp_r = sr;
+                    sp_fl = sfl;
                 }
             }
             WPH(5);
             // the frame's last symbol unit closes it (speculative normalisation)
-            if (spec && cu.phase == 3 && cu.j + 1 == sch.ND) {
-                float mm = sp_mx, rr = sp_r;
+            bool closes;
+            if constexpr (SPAN) closes = cu.s0 + (unsigned)SPW >= S;  // (frame k ends in this unit)
+            else closes = cu.phase == 3 && cu.j + 1 == sch.ND;
+            if (spec && closes) {
+                const bool p1 = SPAN && (k & 1u) != 0u;
+                float mm = p1 ? sp_mx1 : sp_mx, rr = p1 ? sp_r1 : sp_r;
+                const unsigned fl = p1 ? sp_fl1 : sp_fl;
 #pragma unroll
                 for (int off = 32; off >= 1; off >>= 1) {
                     mm = fmaxf(mm, __shfl_xor(mm, off, 64));
                     rr = fminf(rr, __shfl_xor(rr, off, 64));
                 }
-                const bool nan = __ballot(sp_fl & 1u) != 0, open = __ballot(sp_fl & 2u) != 0;
-                sp_mx = 0.0f;
-                sp_r = kBig;
-                sp_fl = 0u;
-                if (R.ok) {
+                const bool nan = __ballot(fl & 1u) != 0, open = __ballot(fl & 2u) != 0;
+                if (p1) {
+                    sp_mx1 = 0.0f;
+                    sp_r1 = kBig;
+                    sp_fl1 = 0u;
+                } else {
+                    sp_mx = 0.0f;
+                    sp_r = kBig;
+                    sp_fl = 0u;
+                }
+                if (R0.ok) {
                     const WDma nd = dma_plan(nx);
-                    wclose<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, f, R.rate, R.scale, R.t_off, R.mx, mm,
-                                     rr, nan, open, nd.f, nd.j, nd.t_off, nd.est, nd.on, nd.fstride, nd.nest);
+                    wclose<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, f, R0.rate, R0.scale, R0.t_off, R0.mx,
+                                     mm, rr, nan, open, nd);
                 }
             }
             WPH(6);
@@ -1501,7 +1721,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                 if ((h & 1) == 0 && l == 0 && (unsigned)(h >> 1) < nest) {
                     bound_check(fglob(kj), (long long)A.frames);
                     meta_put_est(&A.meta[fglob(kj)], m);
-                    lds_frame& q = ring[kj & 7u];
+                    lds_frame& q = ring[kj & (unsigned)(W::RING - 1)];
                     q.rate = m.rate;
                     q.scale = m.scale;
                     q.mx = eu.mx;

@@ -45,6 +45,7 @@ F_UNFUSED = 32  # separate prologue / symbol launches (lphy_hip.h)
 F_EXACT_ROTATION = 64  # every symbol with the reference's per-sample rotation
 F_SCAN_FIRST = 256  # modes 1/2: whole-frame max-abs pre-scan (no speculation)
 F_DEBUG_RECHECK = 512  # every symbol / estimated frame left to the exact re-run
+F_FRAMES_KERNEL = 1024  # SF 7-9: k_frames where k_wave would run (matrix-core tests)
 WINDOW_NONE = 0
 WINDOW_HANN = 1
 # Smallest batch new Demodulators send to the fused kernels

@@ -12,10 +12,12 @@ geometrically from 1 to 2^10 over the frame's symbols, under CFO and delay.
 Every output (symbols, sync word, cfo / time_offset bits) must equal the
 oracle's, and lphy_hip_recheck_count must show the exact re-run fired.
 
-Kernels: SF 7-8 k_frames (modes 1/2: symbol tiles on the matrix cores,
-lphy_mfma.h, whose f16 roundings the certificate charges; mode 0 packed
-f32); SF 9-12 k_wave (no window) and, with a Hann window,
-k_frames (SF 9) or the separate launches' certified k_demod (SF 11-12)."""
+Kernels: SF 7-12 k_wave (no window; SF 7-9 with units spanning frames);
+SF 7-9 also k_frames (the test build's LPHY_F_FRAMES_KERNEL: modes 1/2
+with symbol tiles on the matrix cores, lphy_mfma.h, whose f16 roundings the
+certificate charges; mode 0 packed f32), which the product takes for
+frames shorter than a wave unit and with a Hann window; with a window
+SF 11-12 take the separate launches' certified k_demod."""
 import numpy as np
 import pytest
 
@@ -53,14 +55,17 @@ def _two_tone_frames(oracle, sf, nf, seed):
 
 @pytest.mark.parametrize("sf,nf", [(7, 48), (8, 24), (9, 20), (11, 6), (12, 4)])
 @pytest.mark.parametrize("mode", [0, 2])
-@pytest.mark.parametrize("hann", [False, True])
-def test_near_ties_straddling_the_certificate(oracle, lphy, sf, nf, mode, hann):
-    if sf <= 8 and hann:
-        pytest.skip("SF 7-8 take k_frames either way")
+@pytest.mark.parametrize("kernel", ["default", "hann", "frames"])
+def test_near_ties_straddling_the_certificate(oracle, lphy, sf, nf, mode, kernel):
+    hann = kernel == "hann"
+    if kernel == "frames" and sf > 9:
+        pytest.skip("k_frames: SF <= 10")
     iq = _two_tone_frames(oracle, sf, nf, seed=sf * 13 + mode + 7 * hann)
-    d = lphy.Demodulator(sf, window=lphy.WINDOW_HANN if hann else lphy.WINDOW_NONE)
+    d = lphy.Demodulator(sf, window=lphy.WINDOW_HANN if hann else lphy.WINDOW_NONE,
+                         test_build=kernel == "frames")
+    flags = lphy.F_DECODE | (lphy.F_FRAMES_KERNEL if kernel == "frames" else 0)
     d.recheck_count(reset=True)
-    syms, _, meta = d.demod_host(iq, nf, iq.shape[1], mode, lphy.F_DECODE)
+    syms, _, meta = d.demod_host(iq, nf, iq.shape[1], mode, flags)
     n_exact = d.recheck_count(reset=True)
     for f in range(nf):
         if mode == 0:
@@ -99,7 +104,8 @@ def _pure_two_tone_frame(sf, ratio, seed, nsym=64):
 
 @pytest.mark.parametrize("sf", [7, 8])
 def test_matrix_core_threshold_straddled(oracle, lphy, sf):
-    """SF 7-8 modes 1/2 (the C1 bench path): k_frames' symbol tiles run the
+    """SF 7-8 modes 1/2 in k_frames (frames shorter than a wave unit, or any
+    frame with the test build's LPHY_F_FRAMES_KERNEL): its symbol tiles run the
     transform in f16 on the matrix cores (lphy_mfma.h) and the certificate
     charges kMfmaExtra = 3 * 2^14 u of A for it: with
     A = N sqrt2 and two tones of amplitude 1/2, a lead N (r - 1) / 2 must
@@ -114,12 +120,12 @@ def test_matrix_core_threshold_straddled(oracle, lphy, sf):
     L = (sf + 1) // 2
     thr = 4.0 * 2.0 ** -24 * np.sqrt(2.0) * (24 + 12 * L + 6 + 49152) * 1.001 / 0.5  # r - 1 at the bound
     ks = 2.0 ** np.linspace(-11, -2, 37)
-    d = lphy.Demodulator(sf)
+    d = lphy.Demodulator(sf, test_build=True)  # (k_frames: LPHY_F_FRAMES_KERNEL)
     rows = []
     for i, k in enumerate(ks):
         x = _pure_two_tone_frame(sf, 1.0 + k, seed=4000 + 97 * sf + i)
         d.recheck_count(reset=True)
-        syms, _, meta = d.demod_host(x[None, :], 1, x.size, 1, lphy.F_DECODE)
+        syms, _, meta = d.demod_host(x[None, :], 1, x.size, 1, lphy.F_DECODE | lphy.F_FRAMES_KERNEL)
         n_exact = d.recheck_count(reset=True)
         r, osyms, osync, omet = oracle.lora_demodulate(x, sf)
         ctx = f"sf {sf} r-1 {k:.3g}"
@@ -152,7 +158,7 @@ def test_matrix_core_weak_symbols(oracle, lphy, sf):
     inside kMfmaExtra's slack; a weak near-tie is re-run.  Every output bit
     equals the oracle's across data gains 2^-2 .. 2^-16 (mode 1, two pure
     tones at ratio 1.3, sync symbols of amplitude 2)."""
-    d = lphy.Demodulator(sf)
+    d = lphy.Demodulator(sf, test_build=True)  # (k_frames: LPHY_F_FRAMES_KERNEL)
     counts = []
     for i, gexp in enumerate([2, 4, 6, 8, 12, 16]):
         x = _pure_two_tone_frame(sf, 1.3, seed=5000 + sf + i).astype(np.complex128)
@@ -161,7 +167,7 @@ def test_matrix_core_weak_symbols(oracle, lphy, sf):
         x[2 * N:] *= 2.0 ** -gexp
         x = x.astype(np.complex64)
         d.recheck_count(reset=True)
-        syms, _, meta = d.demod_host(x[None, :], 1, x.size, 1, lphy.F_DECODE)
+        syms, _, meta = d.demod_host(x[None, :], 1, x.size, 1, lphy.F_DECODE | lphy.F_FRAMES_KERNEL)
         counts.append(d.recheck_count(reset=True))
         r, osyms, osync, omet = oracle.lora_demodulate(x, sf)
         ctx = f"sf {sf} gain 2^-{gexp}"

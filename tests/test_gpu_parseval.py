@@ -1,5 +1,5 @@
-"""The Parseval certificate of the SF 9-12 wave kernels (csrc/lphy_wave.h,
-k_wave): a symbol unit whose every symbol carries most of its
+"""The Parseval certificate of the wave kernel (csrc/lphy_wave.h, k_wave,
+SF 7-12; SF 7-9 with units spanning frames): a symbol unit whose every symbol carries most of its
 energy in one bin is proven from that bin and the symbol's energy alone,
 without its FFT (|Y_k| - sqrt(N E - |Y_k|^2) > 4 B); any other unit runs the
 transform and the runner-up certificate, and whatever neither proves is
@@ -96,7 +96,7 @@ def _pure_tone_frame(sf, amps, gains, seed, nsym=64):
     return np.concatenate(out).astype(np.complex64)
 
 
-@pytest.mark.parametrize("sf", [9, 10, 11, 12])
+@pytest.mark.parametrize("sf", [7, 8, 9, 10, 11, 12])
 def test_runner_up_threshold_straddled(oracle, lphy, sf):
     """One frame per call (mode 1), every data symbol two pure tones at a
     constant amplitude ratio r.  Two comparable tones give the Parseval
@@ -173,7 +173,7 @@ def _parseval_leads(x, sf):
     return lead, B, A
 
 
-@pytest.mark.parametrize("sf", [9, 10, 11, 12])
+@pytest.mark.parametrize("sf", [7, 8, 9, 10, 11, 12])
 def test_parseval_threshold_straddled(oracle, lphy, sf):
     """One frame per call (mode 1), every data symbol a clean tone plus a
     half-symbol tone that adds energy but nothing to the winner's bin
@@ -206,7 +206,7 @@ def test_parseval_threshold_straddled(oracle, lphy, sf):
     assert all(p < 66 for _, r, _, p in rows if r < 4.0), msg
 
 
-@pytest.mark.parametrize("sf", [9, 10, 11, 12])
+@pytest.mark.parametrize("sf", [7, 8, 9, 10, 11, 12])
 def test_three_tones_take_the_transform(oracle, lphy, sf):
     d = lphy.Demodulator(sf, test_build=True)
     for i in range(3):
@@ -221,7 +221,7 @@ def test_three_tones_take_the_transform(oracle, lphy, sf):
         assert n_pv <= 2 and n_exact == 0, (n_pv, n_exact)
 
 
-@pytest.mark.parametrize("sf,nf", [(9, 800), (10, 400), (11, 200), (12, 100)])
+@pytest.mark.parametrize("sf,nf", [(7, 3200), (8, 1600), (9, 800), (10, 400), (11, 200), (12, 100)])
 @pytest.mark.parametrize("mode", [0, 2])
 def test_awgn_mixed_paths(oracle, lphy, sf, nf, mode):
     """AWGN from 30 dB down to -10 dB per-sample SNR over the batch's frames

@@ -1,4 +1,4 @@
-"""Frames of few symbols through k_wave (csrc/lphy_wave.h) at SF 9-10,
+"""Frames of few symbols through k_wave (csrc/lphy_wave.h) at SF 7-10,
 where a unit holds SPW = 8 / 4 symbols and one estimate unit holds the two
 estimate symbols of EPU = 4 / 2 frames of a wave (halves 2j, 2j + 1: frame
 j of the group).  Frames of 2-10 symbols: every frame's last unit is
@@ -9,9 +9,14 @@ frames each (1,024 waves on the GPU).  Some frames carry a late sample
 louder than their estimate symbols (the speculative normalisation settles
 them, re-running their estimate unit alone).  Every output byte against the
 separate launches over the whole batch and against the oracle
-(LoRaDemod.cpp:50-197, phy.cpp:182-243) on a sample.  (Round 4's k_wave2s,
-whose units spanned frames and which these tests were first written for,
-was removed in round 5.)"""
+(LoRaDemod.cpp:50-197, phy.cpp:182-243) on a sample.
+
+test_units_spanning_frames: SF 7-9 with S >= SPW symbols per frame, where a
+wave's frames form one symbol stream and a unit holds the end of one frame
+and the start of the next (WSchedSpan): S = SPW (units aligned with
+frames), S just above SPW and S of the bench's 66, frames delayed both ways
+(windows shifted up to the frame's edges), batches of one to many estimate
+groups per wave."""
 import numpy as np
 import pytest
 
@@ -22,7 +27,7 @@ def _bits(x):
     return np.asarray(x, np.float32).view(np.uint32)
 
 
-def _frames(oracle, sf, nf, nbytes, seed, loud_every=3):
+def _frames(oracle, sf, nf, nbytes, seed, loud_every=3, delay=False):
     """nf frames of `nbytes` payload bytes (2 nbytes data symbols + 2 sync),
     CFO, noise, gain; every `loud_every`-th frame has a late sample larger
     than any in its estimate symbols (the speculative normalisation settles
@@ -36,6 +41,8 @@ def _frames(oracle, sf, nf, nbytes, seed, loud_every=3):
         t = np.arange(x.size)
         x = x * np.exp(2j * np.pi * rng.uniform(-0.4, 0.4) / N * t) * [0.8, 1.0, 2.2][f % 3]
         x = x + 0.05 * (rng.standard_normal(x.size) + 1j * rng.standard_normal(x.size))
+        if delay:
+            x = np.roll(x, int(rng.integers(-N // 4, N // 4 + 1)))
         x = x.astype(np.complex64)
         if loud_every and f % loud_every == 1 and x.size > 2 * N:
             j = int(rng.integers(2 * N, x.size))
@@ -67,6 +74,21 @@ def test_short_frames(oracle, lphy, sf, nf, nbytes, mode):
     d = lphy.Demodulator(sf)
     syms, pay, meta = d.demod_host(iq, nf, iq.shape[1], mode, lphy.F_DECODE)
     # the separate launches as a second reference over the whole batch
+    s2, p2, m2 = d.demod_host(iq, nf, iq.shape[1], mode, lphy.F_DECODE | lphy.F_UNFUSED)
+    np.testing.assert_array_equal(syms, s2)
+    np.testing.assert_array_equal(pay, p2)
+    np.testing.assert_array_equal(meta.view(np.uint8), m2.view(np.uint8))
+    _check(oracle, sf, iq, mode, syms, meta, range(0, nf, max(1, nf // 40)), f"SF{sf} S={2 * nbytes + 2}")
+
+
+@pytest.mark.parametrize("sf,nbytes,nf", [(7, 15, 3000), (7, 16, 20000), (7, 32, 5000), (8, 7, 2500),
+                                          (8, 8, 9000), (8, 32, 3000), (9, 3, 4000), (9, 5, 9000),
+                                          (9, 32, 1500)])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_units_spanning_frames(oracle, lphy, sf, nbytes, nf, mode):
+    iq = _frames(oracle, sf, nf, nbytes, seed=1700 + 10 * nbytes + mode + sf, delay=True)
+    d = lphy.Demodulator(sf)
+    syms, pay, meta = d.demod_host(iq, nf, iq.shape[1], mode, lphy.F_DECODE)
     s2, p2, m2 = d.demod_host(iq, nf, iq.shape[1], mode, lphy.F_DECODE | lphy.F_UNFUSED)
     np.testing.assert_array_equal(syms, s2)
     np.testing.assert_array_equal(pay, p2)
