@@ -134,7 +134,7 @@ class Workload:
 
     def stage_times(self, mode: int, reps: int = 20) -> dict:
         """Device time per launch of each kernel of the product path: the
-        fused prologue+symbols kernel (k_frames, PROLOGUE|SYMBOLS selects it
+        fused prologue+symbols kernel (k_wave / k_frames, PROLOGUE|SYMBOLS selects it
         alone) and k_finalize; plus the separate-launch path's stages
         (LPHY_F_UNFUSED) for comparison."""
         D = lphy.F_DECODE
@@ -216,7 +216,7 @@ def timed(wl: Workload, mode: int, steps: int, warmup: int, world: int, events: 
           settle_s: float = 0.0, gat: Gatherer | None = None):
     """Wall time of `steps` steps between barriers.  With `events`, each
     step issues the demodulation as two calls on the same stream - prologue
-    + symbols (the fused k_frames launch and its fix-up), then the per-frame
+    + symbols (the fused launch and its fix-up), then the per-frame
     finalisation - and HIP events bracket the first, so the dominant
     kernel's duration is measured inside the timed region; the per-step
     (start, end) event pairs are appended to `events`.  With `gat` (N > 1)
@@ -427,7 +427,7 @@ def write_perf_csv(path: str, run_id: str, rows: list) -> None:
 
 def frames_fused(sf: int) -> bool:
     """Whether the bench frame shape takes a fused launch: every SF (k_frames
-    up to SF 8, k_wave at SF 9-12; lphy_hip.hip frames_fit /
+    up to SF 6, k_wave at SF 7-12; lphy_hip.hip frames_fit /
     wave_fit: the bench's batches are far above the fused crossover)."""
     return True
 
@@ -435,8 +435,10 @@ def frames_fused(sf: int) -> bool:
 def fused_kernel(sf: int) -> str:
     """Name of the fused launch's kernel, as the PMC summaries key it, by the
     library's own rule for the bench's frames (66 symbols, osr 1, no window;
-    lphy_hip.hip wave_fit)."""
-    if sf <= 8:
+    lphy_hip.hip wave_fit: k_wave from SF 7 when a frame holds at least one
+    wave unit of symbols, 4096 / N - which the bench's 66 always do; below
+    SF 7, k_frames)."""
+    if sf <= 6:
         return f"k_frames<{sf}>"
     return f"k_wave<{sf}>"
 
@@ -759,14 +761,14 @@ def main():
     st = wl.stage_times(mode_b)
 
     N = wl.N
-    # dominant kernel = the fused launch (k_frames up to SF 8, k_wave from
-    # SF 9): algorithmic bytes = every IQ sample once + one u16 per data
+    # dominant kernel = the fused launch (k_wave from SF 7, k_frames below):
+    # algorithmic bytes = every IQ sample once + one u16 per data
     # symbol + the 32-B frame record (the two-symbol scans and the
     # settled frames' estimate re-reads are extra traffic, which the PMC
     # summary below shows)
     fused = frames_fused(args.sf)
     kern_bytes = frames * (wl.fs * 8 + DATA_SYMS * 2 + (32 if fused else 0))
-    # the fused launch timed live in the timed region (k_frames + its fix-up
+    # the fused launch timed live in the timed region (k_wave + its fix-up
     # launch, which is empty unless a frame needs the exact re-run)
     kern_ms = live_kernel_ms if fused else st["unfused_symbols"]
     achieved = kern_bytes / (kern_ms * 1e-3) / 1e9
