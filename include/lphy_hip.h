@@ -138,9 +138,11 @@ size_t lphy_hip_syms_per_frame(const lphy_hip_ctx* ctx, size_t frame_samples,
  * Limits: frames * (frame_samples / (N*osr)) < 2^32 symbols per call and
  * frame_samples < 2^31 (32-bit symbol bookkeeping in the kernels): larger
  * batches give -ERANGE; split them across calls.
- * Launch choice: the fused launches (k_frames up to SF 8 and for windowed
- * SF 9-10; k_wave at SF 9-12 for osr 1, no window,
- * modes 1/2 with the speculative normalisation or mode 0) for batches of at
+ * Launch choice: the fused launches (k_wave at SF 7-12 for osr 1, no
+ * window, modes 1/2 with the speculative normalisation or mode 0, and below
+ * SF 9 at least 4096/N symbols per frame - SF 7-9 with units spanning
+ * frames; k_frames otherwise up to SF 10, e.g. windowed or short frames)
+ * for batches of at
  * least a per-SF crossover (256 frames at SF <= 7 ... 384 at SF 10-12,
  * DESIGN.md 4.7; lphy_hip_ctx_set_fused_min_frames overrides it per
  * context), the separate symbol-parallel launches below it (a packet at a
