@@ -140,7 +140,7 @@ size_t lphy_hip_syms_per_frame(const lphy_hip_ctx* ctx, size_t frame_samples,
  * batches give -ERANGE; split them across calls.
  * Launch choice: the fused launches (k_wave at SF 7-12 for osr 1, no
  * window, modes 1/2 with the speculative normalisation or mode 0, and below
- * SF 9 at least 4096/N symbols per frame - SF 7-9 with units spanning
+ * SF 9 at least 4096/N symbols per frame - SF 7-10 with units spanning
  * frames; k_frames otherwise up to SF 10, e.g. windowed or short frames)
  * for batches of at
  * least a per-SF crossover (256 frames at SF <= 7 ... 384 at SF 10-12,

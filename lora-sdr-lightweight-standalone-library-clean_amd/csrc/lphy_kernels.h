@@ -2877,7 +2877,10 @@ int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symb
 // shared exchange buffers, were removed in round 5: with the Parseval
 // certificate and the grouped estimate units k_wave was faster at every SF,
 // DESIGN §4.9.)
-// SF 7-9 with at least SPW symbols per frame: units spanning frames
+#ifndef LPHY_SPAN_MIN_SPW  // (-D for timing experiments only)
+#define LPHY_SPAN_MIN_SPW 4
+#endif
+// SF 7-10 with at least SPW symbols per frame: units spanning frames
 // (WSchedSpan); SF 7-8 take k_wave only then (wave_fit).
 template <int SF, int MODE>
 int launch_wave_mode(const DemodArgs& A, hipStream_t st) {
@@ -2887,7 +2890,7 @@ int launch_wave_mode(const DemodArgs& A, hipStream_t st) {
     const unsigned long long need = (A.frames + WGeo<SF>::WPB - 1) / WGeo<SF>::WPB;
     if (blocks > need) blocks = need;
     P.waves = (unsigned)(blocks * WGeo<SF>::WPB);
-    if constexpr (WGeo<SF>::SPW >= 8) {
+    if constexpr (WGeo<SF>::SPW >= LPHY_SPAN_MIN_SPW) {
         if (A.total_syms >= (unsigned long long)WGeo<SF>::SPW) {
             hipLaunchKernelGGL((k_wave<SF, MODE, true>), dim3((unsigned)blocks), dim3(256), 0, st, P);
             HIP_OK(hipGetLastError());

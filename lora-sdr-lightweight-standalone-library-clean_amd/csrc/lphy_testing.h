@@ -23,7 +23,7 @@ enum lphy_test_flags {
                                    // marked "has open symbols" first; fused
                                    // kernels: every symbol left to k_post's
                                    // exact re-run (tests/test_gpu_concurrency.py)
-    LPHY_F_FRAMES_KERNEL = 1024u,  // SF 7-9: k_frames where k_wave would run
+    LPHY_F_FRAMES_KERNEL = 1024u,  // SF 7-10: k_frames where k_wave would run
                                    // (the matrix-core symbol tiles' tests,
                                    // tests/test_gpu_certificate.py)
 };

@@ -427,7 +427,7 @@ __device__ __forceinline__ void wexchange(cf32 (&v)[64], cf32* buf, int h, int l
 
 // One unit's LDS-DMA.  Symbol unit: frame f's symbols s0, s0 + 1, ... (time
 // shift t_off) from half 0 up to the frame's end, then (units spanning
-// frames, SF 7-9) n1 halves of frame f1's symbols 0, 1, ... (shift t1).
+// frames, SF 7-10) n1 halves of frame f1's symbols 0, 1, ... (shift t1).
 // Estimate unit (est): SF 12 symbol s0 of frame f; below, the EPU frames
 // f + j fstride, j < nest, symbols 0 and 1 in halves 2j, 2j + 1.  on = 0:
 // no unit.
@@ -1235,7 +1235,7 @@ struct WSched {
     __device__ __forceinline__ unsigned frame(const WCursor& c) const { return c.phase == 2 ? c.k + 1 : c.k; }
 };
 
-// Units spanning frames (SF 7-9, S >= SPW symbols per frame): the wave's
+// Units spanning frames (SF 7-10, S >= SPW symbols per frame): the wave's
 // frames are one stream of nk S symbols, symbol unit j holds stream symbols
 // SPW j .. SPW j + SPW - 1 (at most two frames: the end of frame k0 and the
 // start of k0 + 1), so no half idles at a frame's end (SF 7: 66 symbols in
@@ -1287,7 +1287,7 @@ template <int SF, int MODE, bool SPAN = false>
 __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     using W = WGeo<SF>;
     constexpr int N = W::N, LPS = W::LPS, SPW = W::SPW;
-    static_assert(!SPAN || (SPW >= 8 && W::EPU >= 3), "units spanning frames: SF 7-9");
+    static_assert(!SPAN || (SPW >= 4 && W::RING >= W::EPU + 3), "units spanning frames: SF 7-10");
     constexpr bool M0 = (MODE & 3) == LPHY_MODE_DEMODULATE;
     constexpr bool DECH = (MODE & 3) == LPHY_MODE_DECHIRP_LORA_DEMODULATE;
     constexpr bool DN = (MODE & 3) != LPHY_MODE_LORA_DEMODULATE;  // down-chirp used

@@ -11,7 +11,7 @@ them, re-running their estimate unit alone).  Every output byte against the
 separate launches over the whole batch and against the oracle
 (LoRaDemod.cpp:50-197, phy.cpp:182-243) on a sample.
 
-test_units_spanning_frames: SF 7-9 with S >= SPW symbols per frame, where a
+test_units_spanning_frames: SF 7-10 with S >= SPW symbols per frame, where a
 wave's frames form one symbol stream and a unit holds the end of one frame
 and the start of the next (WSchedSpan): S = SPW (units aligned with
 frames), S just above SPW and S of the bench's 66, frames delayed both ways
@@ -83,7 +83,7 @@ def test_short_frames(oracle, lphy, sf, nf, nbytes, mode):
 
 @pytest.mark.parametrize("sf,nbytes,nf", [(7, 15, 3000), (7, 16, 20000), (7, 32, 5000), (8, 7, 2500),
                                           (8, 8, 9000), (8, 32, 3000), (9, 3, 4000), (9, 5, 9000),
-                                          (9, 32, 1500)])
+                                          (9, 32, 1500), (10, 1, 3000), (10, 3, 5000), (10, 32, 800)])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_units_spanning_frames(oracle, lphy, sf, nbytes, nf, mode):
     iq = _frames(oracle, sf, nf, nbytes, seed=1700 + 10 * nbytes + mode + sf, delay=True)
