@@ -1102,6 +1102,78 @@ __device__ __forceinline__ void wclose(KArgs ka, lds_cf32* lbuf, const lds_cf32*
     if (nd.on) wdma<SF>(A, buf, nd, lane);
 }
 
+// Units spanning frames (SF 7-10): a frame whose end overturns its
+// speculative normalisation is not re-run at once (wclose would spend a unit
+// on two of its halves and expose two DMA round trips per frame); it is
+// queued, and EPU queued frames are settled together in one unit: their
+// estimate symbols in halves 2j, 2j + 1, each pair transformed with its own
+// frame's true max-abs (KISS's arithmetic, as wclose), folded, and the
+// symbols kept or the frame sent to the exact re-run by wclose's rule.
+// AWGN, tools/noise_ab.py, profiles/r5/noise_ab.txt.
+struct WSettle {
+    unsigned f;
+    float mt, r, rate, scale;
+    int t_off, open, pad;
+};
+typedef __attribute__((address_space(3))) WSettle lds_settle;
+template <int SF, int MODE>
+__device__ __forceinline__ void wsettle(KArgs ka, lds_cf32* lbuf, const lds_cf32* ldnl, const lds_settle* es,
+                                        unsigned n, const WDma& nd, int lane) {
+    using W = WGeo<SF>;
+    constexpr int N = W::N, LPS = W::LPS;
+    typedef __attribute__((address_space(3))) void lds_void;
+    typedef __attribute__((address_space(1))) const void g_void;
+    const DemodArgs& A = kargs(ka);
+    cf32* const buf = (cf32*)lbuf;
+    const int h = lane / LPS, l = lane % LPS;
+    wait_vm0();  // the next unit's IQ has landed (it is fetched again at the end)
+#pragma unroll 1
+    for (unsigned j = 0; j < n; ++j) {
+        const unsigned fj = es[j].f;
+        bound_check(fj, (long long)A.frames);
+        const cf32* src = A.iq + (unsigned long long)fj * A.frame_samples + 2 * lane;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+#pragma unroll
+            for (int r = 0; r < W::PPS; r += 4) {
+                g_void* g = (g_void*)(src + s * N + 128 * r);
+                lds_void* ld = (lds_void*)(buf + (2 * j + s) * W::SS + 128 * r);
+                __builtin_amdgcn_global_load_lds(g, ld, 16, 0, LPHY_IQ_CPOL);
+                if constexpr (W::PPS >= 2) __builtin_amdgcn_global_load_lds(g, ld, 16, 1024, LPHY_IQ_CPOL);
+                if constexpr (W::PPS >= 4) {
+                    __builtin_amdgcn_global_load_lds(g, ld, 16, 2048, LPHY_IQ_CPOL);
+                    __builtin_amdgcn_global_load_lds(g, ld, 16, 3072, LPHY_IQ_CPOL);
+                }
+            }
+        }
+    }
+    wait_vm0();
+    const unsigned jp = (unsigned)(h >> 1) < n ? (unsigned)(h >> 1) : 0u;
+    const lds_settle& q = es[jp];
+    const WSettle e{q.f, q.mt, q.r, q.rate, q.scale, q.t_off, q.open, 0};
+    const WEstU eu = west_unit<SF, MODE>(ka, lbuf, ldnl, e.mt, false, n);
+    const int hb = (h & ~1) * LPS;
+    const UnitResult ua = wur_from(eu.ur, hb), ub = wur_from(eu.ur, hb + LPS);
+    lphy_frame_meta em = norm_meta(e.mt, true, 0);
+    EstFold fold;
+    if (ua.valid) fold.add(ua.idx, ua.findex, 0, ua.phase);
+    else fold.add(0, 0.0f, 0, 0.0f);
+    if (ub.valid) fold.add(ub.idx, ub.findex, 0, ub.phase);
+    else fold.add(0, 0.0f, 0, 0.0f);
+    fold.finish(em, 2, N, 1);
+    const float a = fmaxf(1.0f, e.mt * e.scale) * 1.0001f;
+    const float b1 = cert_bound<SF>(e.rate, e.rate * (float)e.t_off, 1.0f);
+    const float d = fabsf(em.rate - e.rate) * (1.0f + 4.0f * kU);
+    const float A1 = (float)N * 1.41421366f * 1.0001f;
+    const bool ok = !ua.nan && !ub.nan && em.t_off == e.t_off && e.t_off >= -N && e.t_off <= N &&
+                    e.r > 4.0f * a + 4.0f * d * (float)N * A1 * a / b1;
+    if ((h & 1) == 0 && l == 0 && (unsigned)(h >> 1) < n) {
+        em.status = !ok ? kStatusFixup : (e.open ? kStatusRecheck : 0);
+        meta_put_est(&A.meta[e.f], em);
+    }
+    if (nd.on) wdma<SF>(A, buf, nd, lane);
+}
+
 // A frame's symbol outputs, collected in registers and stored 128 at a time
 // (lane t holds entries base + 2t and base + 2t + 1 as a u16 pair), the
 // sync symbols (the frame record's sw0, sw1) at the frame's end.  Stored
@@ -1301,6 +1373,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     // frame parity: [scale] e^{j rate i}, i < 8 LPS, then e^{j rate 8 LPS a}
     constexpr int RT = 8 * LPS + 8;
     __shared__ cf32 rtabs[SPAN ? W::WPB : 1][2][SPAN ? RT : 1];
+    __shared__ WSettle settles[SPAN ? W::WPB : 1][SPAN ? W::EPU : 1];  // (SPAN: frames to settle)
     cf32* const dnl = lds_all;
     cf32 (*const sbuf)[W::BUF] = reinterpret_cast<cf32 (*)[W::BUF]>(lds_all + (DN ? N : 0));
 
@@ -1400,6 +1473,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     float sp_mx1 = 0.0f, sp_r1 = kBig;  // (SPAN: the odd frames')
     unsigned sp_fl1 = 0u;
     unsigned tab0 = 0xffffffffu, tab1 = 0xffffffffu;  // (SPAN: the frames in rtabs)
+    unsigned nset = 0;  // (SPAN: frames queued in settles)
     UnitResult ur0{0, 0, 0.0f, 0.0f, 0};  // SF 12: the first estimate unit's result
 
     WOut<SF> wo;  // the frame's symbol outputs until they are stored
@@ -1687,9 +1761,30 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                     sp_fl = 0u;
                 }
                 if (R0.ok) {
-                    const WDma nd = dma_plan(nx);
-                    wclose<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, f, R0.rate, R0.scale, R0.t_off, R0.mx,
-                                     mm, rr, nan, open, nd);
+                    if constexpr (SPAN) {
+                        // wclose's frame-end check; a settle is queued (wsettle)
+                        const unsigned cnt = DECH ? S * N : (unsigned)A.frame_samples;
+                        const unsigned end = covered_end(S, N, cnt, R0.t_off);
+                        bool fbad = false;
+                        if (end < cnt) mm = fmaxf(mm, wave_range_maxabs<SF, MODE>(A, f, end, cnt, dnl, fbad));
+                        const float mt = fmaxf(mm, R0.mx);
+                        const lphy_frame_meta mg = norm_meta(R0.mx, true, 0), me = norm_meta(mt, true, 0);
+                        if (nan || fbad || !(mt <= 3.40282347e38f)) {
+                            if (lane == 0) A.meta[f].status = kStatusFixup;
+                        } else if (me.scale != mg.scale || me.normalised != mg.normalised) {
+                            if (lane == 0)
+                                settles[wv][nset] = WSettle{f, mt, rr, R0.rate, R0.scale, R0.t_off, open ? 1 : 0, 0};
+                            if (++nset == (unsigned)W::EPU) {
+                                wsettle<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl,
+                                                  (const lds_settle*)settles[wv], nset, dma_plan(nx), lane);
+                                nset = 0;
+                            }
+                        }
+                    } else {
+                        const WDma nd = dma_plan(nx);
+                        wclose<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, f, R0.rate, R0.scale, R0.t_off,
+                                         R0.mx, mm, rr, nan, open, nd);
+                    }
                 }
             }
             WPH(6);
@@ -1794,6 +1889,13 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
         cu = nx;
     }
     wo.flush(A, lane);  // (every frame's last unit has stored it already)
+    if constexpr (SPAN) {
+        if (nset) {
+            const WDma none{0u, 0u, 0, 0, 0, 0u, 1u, 0u, 0, 0u};
+            wsettle<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, (const lds_settle*)settles[wv], nset, none,
+                              lane);
+        }
+    }
     WPH(7);
     WPH_FLUSH(A)
 }

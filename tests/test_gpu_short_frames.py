@@ -44,7 +44,7 @@ def _frames(oracle, sf, nf, nbytes, seed, loud_every=3, delay=False):
         if delay:
             x = np.roll(x, int(rng.integers(-N // 4, N // 4 + 1)))
         x = x.astype(np.complex64)
-        if loud_every and f % loud_every == 1 and x.size > 2 * N:
+        if loud_every and f % loud_every == 1 % loud_every and x.size > 2 * N:
             j = int(rng.integers(2 * N, x.size))
             x[j] = np.complex64(complex(6.0, -2.0))
         out.append(x)
@@ -87,6 +87,23 @@ def test_short_frames(oracle, lphy, sf, nf, nbytes, mode):
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_units_spanning_frames(oracle, lphy, sf, nbytes, nf, mode):
     iq = _frames(oracle, sf, nf, nbytes, seed=1700 + 10 * nbytes + mode + sf, delay=True)
+    d = lphy.Demodulator(sf)
+    syms, pay, meta = d.demod_host(iq, nf, iq.shape[1], mode, lphy.F_DECODE)
+    s2, p2, m2 = d.demod_host(iq, nf, iq.shape[1], mode, lphy.F_DECODE | lphy.F_UNFUSED)
+    np.testing.assert_array_equal(syms, s2)
+    np.testing.assert_array_equal(pay, p2)
+    np.testing.assert_array_equal(meta.view(np.uint8), m2.view(np.uint8))
+    _check(oracle, sf, iq, mode, syms, meta, range(0, nf, max(1, nf // 40)), f"SF{sf} S={2 * nbytes + 2}")
+
+
+@pytest.mark.parametrize("sf,nbytes,nf", [(7, 16, 20000), (8, 8, 12000), (9, 5, 6000), (10, 3, 5000)])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_spanning_units_every_frame_settles(oracle, lphy, sf, nbytes, nf, mode):
+    """Every frame carries a late sample louder than its estimate symbols, so
+    every frame's speculative normalisation is overturned at its end and
+    queued for a batched settle (wsettle: EPU frames per unit, then the
+    remainder after a wave's last unit); waves hold more than EPU frames."""
+    iq = _frames(oracle, sf, nf, nbytes, seed=2300 + 10 * nbytes + mode + sf, loud_every=1, delay=True)
     d = lphy.Demodulator(sf)
     syms, pay, meta = d.demod_host(iq, nf, iq.shape[1], mode, lphy.F_DECODE)
     s2, p2, m2 = d.demod_host(iq, nf, iq.shape[1], mode, lphy.F_DECODE | lphy.F_UNFUSED)

@@ -17,7 +17,11 @@ lphy = bench.lphy
 
 
 def main():
-    sfs = [int(a) for a in sys.argv[1:]] or [7, 8, 9, 10]
+    args = [a for a in sys.argv[1:] if not a.startswith("--lib=")]
+    libs = [a[6:] for a in sys.argv[1:] if a.startswith("--lib=")]
+    if libs:  # --lib=<variant .so>: time that build's default launch only
+        lphy.use(libs[0])
+    sfs = [int(a) for a in args] or [7, 8, 9, 10]
     dev = torch.device("cuda:0")
     mode = lphy.MODE_DECHIRP_LORA_DEMODULATE
     flags = lphy.F_DECODE | lphy.F_STAGE_PROLOGUE | lphy.F_STAGE_SYMBOLS
@@ -33,6 +37,10 @@ def main():
                 g.manual_seed(1234 + sf)
                 wl.iq.add_(torch.randn(wl.iq.shape, generator=g, device=dev) * float(np.sqrt(10 ** (-snr / 10) / 2)))
             t_wave = wl._event_ms(mode, flags, 10)
+            if libs:
+                print(f"SF{sf} snr {'clean' if snr is None else f'{snr:+.0f} dB'}: {Path(libs[0]).name} "
+                      f"{t_wave:.3f} ms", flush=True)
+                continue
             syms, pay, meta = wl.outs[0]
             st = torch.cuda.current_stream().cuda_stream
 
