@@ -162,19 +162,21 @@ inline bool frames_fit(unsigned sf, unsigned osr, int est_units, size_t total) {
     return total + 1 >= 2 * wt;
 }
 
-// Whether the fused SF 9-12 kernel (k_wave, 64 x 64 values per
-// wavefront unit) take this batch: osr 1, the two-symbol estimate, no
-// window, the certified rotation, and in modes 1/2 the speculative
-// normalisation.  Hann windows, LPHY_F_EXACT_ROTATION and the pre-scan
-// schedule stay on k_frames (SF 9-10) or the separate launches (SF 11-12).
-// smallest SF on k_wave (-D for timing experiments only)
-#ifndef LPHY_WAVE_MIN_SF
+// Whether the fused kernel k_wave (64 x 64 values per wavefront unit)
+// takes this batch: SF 7-12, osr 1, the two-symbol estimate, no window, the
+// certified rotation, in modes 1/2 the speculative normalisation, and below
+// SF 9 at least one unit of symbols per frame (4096 / N: its units span
+// frames there).  Hann windows, LPHY_F_EXACT_ROTATION, the pre-scan schedule
+// and shorter frames stay on k_frames (SF <= 10) or the separate launches
+// (SF 11-12).
+#ifndef LPHY_WAVE_MIN_SF  // smallest SF on k_wave (-D for timing experiments only)
 #define LPHY_WAVE_MIN_SF 7
 #endif
 inline bool wave_fit(unsigned sf, unsigned osr, int window, int est_units, size_t total, int mode,
                      const DemodArgs& A) {
-    return sf >= LPHY_WAVE_MIN_SF && sf <= 12 && (sf >= 9 || total >= (size_t)(4096u >> sf)) && osr == 1 && window == LPHY_WINDOW_NONE && est_units == 2 && total >= 2 &&
-           !A.exact_rotation && (mode == LPHY_MODE_DEMODULATE || A.spec);
+    return sf >= LPHY_WAVE_MIN_SF && sf <= 12 && (sf >= 9 || total >= (size_t)(4096u >> sf)) && osr == 1 &&
+           window == LPHY_WINDOW_NONE && est_units == 2 && total >= 2 && !A.exact_rotation &&
+           (mode == LPHY_MODE_DEMODULATE || A.spec);
 }
 
 const SfOps* sf_ops(unsigned sf) {

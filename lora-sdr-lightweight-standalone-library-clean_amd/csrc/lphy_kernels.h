@@ -77,7 +77,7 @@ struct DemodArgs {
     // atomic max / min), flags (1 NaN, 2 symbol left open)}; nullptr = off
     uint4* spec_big;
     int debug_recheck;       // LPHY_F_DEBUG_RECHECK: mark estimated frames kStatusRecheck before k_demod
-    int wave;                // the fused SF 9-12 launch (k_wave) ran (it settles its frames itself)
+    int wave;                // the fused k_wave launch ran (it settles its frames itself)
     // persistent demod workers: symbol stride per step split into whole
     // frames + symbols (host-computed, so the kernel never divides)
     unsigned stride_f, stride_s;
@@ -2871,7 +2871,7 @@ int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symb
     return 0;
 }
 
-// Fused wave-per-symbol path, SF 9-12: k_wave (lphy_wave.h): one wave per
+// Fused wave-per-symbol path, SF 7-12: k_wave (lphy_wave.h): one wave per
 // SIMD, 256-thread workgroups, the next unit staged through LDS by DMA while
 // a unit computes.  (Round 4's k_wave2 / k_wave2s, two waves per SIMD with
 // shared exchange buffers, were removed in round 5: with the Parseval

@@ -1,6 +1,7 @@
-// lphy_wave.h — fused single launch for SF 9-12 (N = 512 .. 4096): one
+// lphy_wave.h — fused single launch for SF 7-12 (N = 128 .. 4096): one
 // wavefront per unit of 64 x 64 complex values, i.e. one symbol at SF 12,
-// 2 / 4 / 8 symbols at SF 11 / 10 / 9, no workgroup barrier in the loop.  Included by lphy_kernels.h inside its anonymous
+// 2 / 4 / 8 / 16 / 32 symbols at SF 11 / 10 / 9 / 8 / 7 (SF 7-10: units
+// spanning frames, WSchedSpan), no workgroup barrier in the loop.  Included by lphy_kernels.h inside its anonymous
 // namespace, after k_frames (it reuses SymCtx, EstFold, the certificate and
 // the speculative normalisation of the SF <= 10 path).
 //
@@ -8,7 +9,8 @@
 // (/root/reference/src/phy/LoRaDemod.cpp:142-176, phy.cpp:204-238) with
 // KISS's recursive radix-4 DIT (kissfft.hh:106-185).  Here a lane holds 64
 // complex values of one symbol (LPS = N/64 lanes per symbol: 64 at SF 12,
-// 32 / 16 / 8 at SF 11 / 10 / 9 where a wave carries SPW = 64 / LPS symbols):
+// 32 / 16 / 8 / 4 / 2 at SF 11 .. 7 where a wave carries SPW = 64 / LPS
+// symbols):
 //
 //   staging  the unit's IQ was copied HBM -> LDS by LDS-DMA during the
 //            previous unit (global_load_lds_dwordx4, 1 KiB per wave
@@ -38,7 +40,7 @@
 //
 // Per wave, frames w, w + W, ... (W waves); per frame the estimate units (2
 // at SF 12, each folding its symbol's max-abs for the normalisation; SF 11
-// one unit whose halves 0 and 1 hold symbols 0 and 1; SF 9-10 one unit for
+// one unit whose halves 0 and 1 hold symbols 0 and 1; SF 7-10 one unit for
 // EPU frames), then the symbol units.  The next frame's estimate units run two
 // symbol units before the current frame's end, so its time shift is known
 // when its first symbol unit's LDS-DMA is issued:
@@ -66,7 +68,7 @@ struct WGeo {
     static constexpr int LPS = N / 64;    // lanes per symbol = pass-1 sub-transform length
     static constexpr int SPW = 64 / LPS;  // symbols per unit (1 | 2 | 4 | 8)
     static constexpr int NE = SPW == 1 ? 2 : 1;  // estimate units per frame (group)
-    // frames per estimate unit: SF 9-10 put EPU frames' two estimate symbols
+    // frames per estimate unit: SF 7-10 put EPU frames' two estimate symbols
     // in one unit (halves 2j, 2j + 1: frame j), SF 11-12 one frame's
     static constexpr int EPU = SPW >= 4 ? SPW / 2 : 1;
     // frame records in the per-wave LDS ring (EPU > 1): the group in
@@ -906,7 +908,7 @@ __device__ __forceinline__ UnitResult wur_from(const UnitResult& u, int src) {
 // re-run, as in k_frames).  Modes 1/2 normalise with the max-abs `mx`, or
 // with find_mx with the max-abs folded here from the unit's own samples, as
 // the reference's normalisation scans them (LoRaDemod.cpp:60-78; NaN when one
-// is not finite): SF 9-11 both estimate symbols' (both are in the unit), SF
+// is not finite): SF 7-11 both estimate symbols' (both are in the unit), SF
 // 12 this symbol's folded with `mx` (0, or symbol 0's for symbol 1).  No
 // blocking pre-scan of the frame is then needed.  Returns the max-abs used.
 struct WEstU {
@@ -933,7 +935,7 @@ __device__ __forceinline__ WEstU west_unit(KArgs ka, lds_cf32* lbuf, const lds_c
         if constexpr (DECH) x = cmul(x, dnl[l + LPS * e]);
         v[e] = x;
     }
-    // (SF 9-11: halves 2j, 2j + 1 hold frame j's two estimate symbols, j <
+    // (SF 7-11: halves 2j, 2j + 1 hold frame j's two estimate symbols, j <
     // nlive; the other halves hold nothing of use)
     const bool live_frame = SPW == 1 || (unsigned)(h >> 1) < nlive;
     if constexpr (!M0) {
@@ -1791,8 +1793,8 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
         } else {
             // estimate unit(s): KISS's arithmetic, bit for bit (LoRaDemod.cpp:80-136,
             // phy.cpp:81-148); SF 12 symbol j, SF 11 symbol h of the pair,
-            // SF 9-10 symbol h & 1 of frame k + (h >> 1) of the group
-            // (SF 9-11: the unit folds the two estimate symbols' max-abs itself)
+            // SF 7-10 symbol h & 1 of frame k + (h >> 1) of the group
+            // (SF 7-11: the unit folds the two estimate symbols' max-abs itself)
             if constexpr (W::EPU > 1) {
                 const unsigned nest = (sch.nk - k) < (unsigned)W::EPU ? (sch.nk - k) : (unsigned)W::EPU;
                 const WEstU eu = west_unit<SF, MODE>(ka, (lds_cf32*)buf, (const lds_cf32*)dnl, 0.0f, true, nest);
