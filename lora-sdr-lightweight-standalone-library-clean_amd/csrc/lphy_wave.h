@@ -510,6 +510,13 @@ __device__ __forceinline__ void wdma(const DemodArgs& A, cf32* buf, const WDma& 
     }
     // symbols sy0 .. sy0 + nh - 1 of frame f (shift t) into halves h0, h0 + 1, ...
     auto run = [&](unsigned f, int t, unsigned sy0, unsigned nh, unsigned h0) __attribute__((always_inline)) {
+        // (debug build: the run's frame, its symbols and halves exist; each
+        // window is checked against the frame below)
+        bound_check(f, (long long)A.frames);
+        if (nh) {
+            bound_check(sy0 + nh - 1, (long long)S);
+            bound_check(h0 + nh - 1, (long long)W::SPW);
+        }
         const cf32* fsrc = A.iq + (unsigned long long)f * A.frame_samples + 2 * lane;
         // the shifted symbols (as above): s_lo .. s_hi
         unsigned s_lo = 0u, s_hi = 0xffffffffu;
@@ -530,6 +537,10 @@ __device__ __forceinline__ void wdma(const DemodArgs& A, cf32* buf, const WDma& 
         {
             const cf32* src = fsrc + (sy0 + h) * N + t;
             cf32* dst = b0 + h * W::SS;
+            if (hb > h) {  // (debug build: the shifted run's first and last windows lie in the frame)
+                bound_check((long long)(sy0 + h) * N + t, (long long)count - N + 1);
+                bound_check((long long)(sy0 + hb - 1) * N + t, (long long)count - N + 1);
+            }
 #pragma unroll 1
             for (; h < hb; ++h, src += N, dst += W::SS) piece(src, dst);
         }
