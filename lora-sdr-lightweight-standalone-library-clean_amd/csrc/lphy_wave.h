@@ -51,6 +51,15 @@
 // rows padded by LPS entries) + the down-chirp (N entries): the whole
 // 160 KiB of a CU at SF 12, one 256-thread workgroup per CU.
 
+// unroll of the LDS-DMA's run of shifted windows: 4 (the loop's counter,
+// compare and branch per 1 KiB piece were a third of a piece's ~8
+// instructions at SF 7, 32 pieces per unit; same-box A/B SF 7 fused
+// 0.785-0.801 -> 0.767-0.771 ms, SF 8-9 within noise).  (-D for timing
+// experiments only.)
+#ifndef LPHY_DMA_UNROLL
+#define LPHY_DMA_UNROLL 4
+#endif
+
 // cache policy of the IQ's LDS-DMA: nt (2), streaming. Every IQ line is
 // read once (twice for the estimate symbols), so it should not push the
 // twiddle table and the partly written output lines out of L2: same-box
@@ -541,7 +550,7 @@ __device__ __forceinline__ void wdma(const DemodArgs& A, cf32* buf, const WDma& 
                 bound_check((long long)(sy0 + h) * N + t, (long long)count - N + 1);
                 bound_check((long long)(sy0 + hb - 1) * N + t, (long long)count - N + 1);
             }
-#pragma unroll 1
+#pragma unroll LPHY_DMA_UNROLL
             for (; h < hb; ++h, src += N, dst += W::SS) piece(src, dst);
         }
 #pragma unroll 1
