@@ -353,7 +353,7 @@ class Demodulator:
         _chk(self.lib.lphy_hip_ctx_reserve(self.ctx, frames, frame_samples), "lphy_hip_ctx_reserve")
 
     def parseval_count(self, reset: bool = True) -> int:
-        """Test build only: symbols the wave kernels (SF 9-12) certified by
+        """Test build only: symbols the wave kernel (k_wave, SF 7-12) certified by
         the Parseval certificate, without their FFT (device sync)."""
         fn = self.lib.lphy_hip_test_counter
         fn.argtypes = [_vp, C.c_int, C.POINTER(C.c_ulonglong), C.c_int]

@@ -1,5 +1,6 @@
-"""Concurrency and ordering at SF 9-12 (the fused wave kernel and the
-separate launches) and SF <= 10 with LPHY_F_UNFUSED:
+"""Concurrency and ordering at SF 7-12 (the fused wave kernel, with units
+spanning frames at SF 7-10, and the separate launches) and SF <= 10 with
+LPHY_F_UNFUSED:
 
 * two lphy_hip_demod_batch calls on ONE context issued on two streams at
   once give the single-stream results bit for bit (the SF 11-12
@@ -53,7 +54,7 @@ def _host(lphy, syms, pay, meta, nf, per):
             meta.cpu().numpy().view(lphy.META_DTYPE))
 
 
-@pytest.mark.parametrize("sf,mode", [(12, 2), (11, 2), (12, 1), (11, 0), (10, 2), (9, 1)])
+@pytest.mark.parametrize("sf,mode", [(12, 2), (11, 2), (12, 1), (11, 0), (10, 2), (9, 1), (8, 1), (7, 2)])
 @pytest.mark.parametrize("unfused", [False, True])
 def test_two_streams_one_context(oracle, lphy, sf, mode, unfused):
     nf = 40
@@ -86,7 +87,8 @@ def test_two_streams_one_context(oracle, lphy, sf, mode, unfused):
 
 @pytest.mark.parametrize("sf,mode,unfused", [(12, 2, True), (11, 1, True), (12, 0, True),
                                              (12, 2, False), (11, 2, False), (10, 2, False), (9, 1, False),
-                                             (9, 2, True), (7, 0, True)])
+                                             (9, 2, True), (7, 0, True), (8, 2, False), (7, 2, False),
+                                             (7, 0, False)])
 def test_forced_recheck_no_symbol_lost(oracle, lphy, sf, mode, unfused):
     nf = 24 if sf >= 11 else 96
     iq, fs = _noisy_frames(oracle, sf, nf, -12.0, seed=sf * 11 + mode)
