@@ -207,16 +207,18 @@ int launch_post(unsigned sf, int mode, const DemodArgs& A, const FinalArgs& F, b
 // wavefront that walks its symbols in order, so a small batch leaves most
 // of the GPU idle and the separate launches (symbol-parallel k_demod) finish
 // first.  Crossovers measured per SF, mode 2 with decode, device time per
-// call (tools/fused_crossover.py, profiles/r4/fused_crossover.json); the
-// per-packet latency of the lora_phy:: API rides on the small end.  A
-// context's own setting (lphy_hip_ctx_set_fused_min_frames) wins; the test
-// build also reads a process default from LPHY_FUSED_MIN_FRAMES.
+// call (tools/fused_crossover.py, profiles/r5/fused_crossover.json: with
+// k_wave at SF 7-12 the fused kernel wins from 256 frames at SF 7-10, from
+// 512 at SF 11-12, where 256 is a tie); the per-packet latency of the
+// lora_phy:: API rides on the small end.  A context's own setting
+// (lphy_hip_ctx_set_fused_min_frames) wins; the test build also reads a
+// process default from LPHY_FUSED_MIN_FRAMES.
 size_t fused_min_frames(const lphy_hip_ctx* c) {
     const long own = c->fused_min.load(std::memory_order_relaxed);
     if (own >= 0) return (size_t)own;
     const long test = lphy_test_fused_min_frames();
     if (test >= 0) return (size_t)test;
-    static const size_t t[13] = {256, 256, 256, 256, 256, 256, 256, 256, 1536, 768, 384, 384, 384};
+    static const size_t t[13] = {256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 384, 384};
     return t[c->sf <= 12 ? c->sf : 12];
 }
 

@@ -3,6 +3,7 @@ same inputs.  Bit-exact on every integer output (symbol indices, sync word,
 decoded bytes, CRC flag, return status) and on the float32 bit patterns of
 the per-frame cfo / time_offset estimates."""
 import numpy as np
+import torch
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -106,6 +107,28 @@ def test_modulate_bit_exact(oracle, lphy):
         a = d.modulate_host(syms, 1.0, 0x34)
         b = oracle.modulate(syms, sf, bw_hz=bw, sync=0x34)
         np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("sf,osr,nf,nsyms", [(7, 1, 1, 64), (7, 1, 5, 64), (8, 1, 3, 64), (9, 1, 2, 64),
+                                              (5, 3, 4, 21), (7, 2, 2, 30), (3, 3, 3, 7), (2, 1, 2, 5),
+                                              (10, 1, 2, 64), (7, 1, 70, 64)])
+def test_modulate_batch_frames(oracle, lphy, sf, osr, nf, nsyms):
+    """lphy_hip_modulate_batch, frame by frame == the oracle: the one-launch
+    packet kernel (phases in LDS: up to SF 9 at 66 symbols, few frames), the
+    three-kernel few-symbol form (SF 10) and the batch form (70 frames)."""
+    rng = np.random.default_rng(sf * 100 + nf)
+    syms = rng.integers(0, 1 << min(sf, 8), (nf, nsyms), dtype=np.uint16)
+    d = lphy.Demodulator(sf, 125000, osr)
+    dev = torch.device("cuda", 0)
+    step = (1 << sf) * osr
+    iq = torch.zeros(nf * (nsyms + 2) * step * 2, dtype=torch.float32, device=dev)
+    s_t = torch.from_numpy(syms.reshape(-1).astype(np.int16)).to(dev)
+    d.modulate_batch(s_t, nf, nsyms, iq, 1.0, 0x34, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = iq.cpu().numpy().view(np.complex64).reshape(nf, -1)
+    for f in range(nf):
+        b = oracle.modulate(syms[f], sf, osr=osr, sync=0x34)
+        np.testing.assert_array_equal(got[f].view(np.uint32), b.view(np.uint32), err_msg=f"frame {f}")
 
 
 def test_modulate_repeated_contexts(oracle, lphy):
