@@ -646,6 +646,9 @@ int compensate_impl(lphy_hip_ctx* c, float* d_iq, size_t count, float cfo, float
 // holds mod_scratch_bytes(): the per-symbol start phases, and below
 // mod_walk_all_below symbols every sample's phase too.
 constexpr size_t mod_walk_all_below = 4096;
+#ifndef LPHY_MOD_FAST  // 0: the three-kernel few-symbol form only (A/B builds)
+#define LPHY_MOD_FAST 1
+#endif
 
 size_t mod_scratch_bytes(const lphy_hip_ctx* c, size_t frames, size_t nsyms) {
     const size_t nph = frames * (nsyms + 2);
@@ -665,6 +668,7 @@ int modulate_impl(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames, size_t
     A.bws = (float)c->bw_hz / 125000.0f;
     A.ampl = std::max(-1.0f, std::min(1.0f, amplitude));  // LoRaMod.cpp:18
     A.sync = sync;
+    A.slow = c->d_counters + 8;  // lphy_hip_test_counter(8)
     const size_t nph = frames * (nsyms + 2);
     const size_t samples = nph * (size_t)c->N * c->osr;
     // few symbols: every sample's phase from the walk, then sample-parallel
@@ -675,7 +679,18 @@ int modulate_impl(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames, size_t
     A.phase0 = static_cast<float*>(scratch.p);
     A.phases = walk_all ? reinterpret_cast<float*>(static_cast<char*>(scratch.p) + align_up(nph * sizeof(float)))
                         : nullptr;
-    if (walk_all) {
+    // ... and when a frame's f rows fit one CU's LDS, the walk by candidate
+    // windows and a chain of lookups (k_mod_fast), then the sincos
+    const int stride = (int)(c->N * c->osr) + 4;
+    const size_t lds = (nsyms + 2) * (size_t)stride * sizeof(float);
+    if (LPHY_MOD_FAST && walk_all && nsyms + 2 <= (size_t)kModFastSyms && lds <= kModFastLds) {
+        if (lds > (size_t(64) << 10))
+            HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_mod_fast),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kModFastLds));
+        hipLaunchKernelGGL(k_mod_fast, dim3((unsigned)frames), dim3(kModFastThreads), lds, st, A, stride);
+        hipLaunchKernelGGL(k_mod_sincos, dim3((unsigned)((samples + 255) / 256)), dim3(256), 0, st, A,
+                           (unsigned long long)samples);
+    } else if (walk_all) {
         hipLaunchKernelGGL(k_mod_freq, dim3((unsigned)((nph + 63) / 64)), dim3(64), 0, st, A);
         hipLaunchKernelGGL(k_mod_accumulate, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, A);
         hipLaunchKernelGGL(k_mod_sincos, dim3((unsigned)((samples + 255) / 256)), dim3(256), 0, st, A,

@@ -2492,6 +2492,7 @@ struct ModArgs {
     int N, osr;
     float bws, ampl;
     uint8_t sync;
+    unsigned long long* slow;  // (k_mod_fast) frames that took the serial walk
 };
 
 __device__ __forceinline__ float mod_f0(const ModArgs& A, unsigned long long f, unsigned long long s) {
@@ -2677,6 +2678,311 @@ __global__ __launch_bounds__(64) void k_mod_accumulate(ModArgs A) {
         phase = wrap_phase(phase);
     }
 }
+
+// A packet's walk without walking it in order, one
+// workgroup per frame, everything in LDS.  Symbol s's walk from its pivot
+// sample k_s (where |phase| is largest, so consecutive floats are furthest
+// apart) to the next symbol's pivot depends only on the float at k_s.  So:
+// estimate every symbol's start in double (exact sums of its f row, then
+// once more with each symbol's own rounding error, measured by walking every
+// symbol from the first estimate in parallel), take the 64 consecutive
+// floats around each pivot's estimate as candidates, walk every candidate in
+// parallel to the next pivot (tail, symbol-end wrap, head of the next
+// symbol) and record where it lands among that symbol's candidates.  The
+// serial part is then a chain of ns table lookups from symbol 0's pivot,
+// which is walked exactly from phase 0.  Every step is the reference's
+// arithmetic on floats (ChirpGenerator.hpp:39-49), so a chain that stays
+// inside the windows is the serial walk; one that leaves them (an estimate
+// off by more than 32 floats, measured ≤ 19 at SF 7-8: tools/walk_lattice.py)
+// falls back to the serial walk of the whole frame.  Rows `stride` floats
+// apart in LDS; at most kModFastSyms symbols; the phases go to A.phases for
+// k_mod_sincos.
+constexpr int kModFastThreads = 1024;
+constexpr int kModFastSyms = 256;
+constexpr int kModFastWin = 64;
+constexpr size_t kModFastLds = size_t(120) << 10;  // the f rows (dynamic)
+
+__device__ __forceinline__ int f_ord(float x) {
+    const int i = __float_as_int(x);
+    return i >= 0 ? i : (int)(0x80000000u - (unsigned)i);
+}
+__device__ __forceinline__ float f_unord(int o) {
+    return __int_as_float(o >= 0 ? o : (int)(0x80000000u - (unsigned)o));
+}
+
+struct ModFastShared {
+    double est[kModFastSyms + 1];  // start estimates
+    double tot[kModFastSyms];      // exact sum of each f row
+    double err[kModFastSyms];      // each row's rounding error from est
+    double piv[kModFastSyms];      // exact partial sum up to the pivot
+    int kp[kModFastSyms];          // pivot sample
+    int base[kModFastSyms];        // f_ord of the window's first candidate
+    int J[kModFastSyms];           // the chain's candidate per symbol
+    float xs[kModFastSyms];        // exact symbol starts
+    unsigned char T[kModFastSyms][kModFastWin];  // landing candidate, 255: outside
+    int ok;
+};
+
+// f rows read 8 at a time: one LDS round trip per 8 steps of a walk, the
+// loads of a block issued before its adds (and stores)
+template <class Fn>
+__device__ __forceinline__ void row_blocks(const float* row, int i0, int i1, Fn fn) {
+    int i = i0;
+    for (; i + 8 <= i1; i += 8) {
+        float b[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) b[k] = row[i + k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) fn(i + k, b[k]);
+    }
+    for (; i < i1; ++i) fn(i, row[i]);
+}
+
+#ifdef LPHY_MODFAST_CLOCKS  // timing aid only: per-phase wall clock sums into counters 1..7
+#define MF_T(k)                                                                   \
+    if (tid == 0) {                                                               \
+        const unsigned long long now = wall_clock64();                            \
+        if (k > 0) atomicAdd(A.slow - 8 + k, now - mf_t);                         \
+        mf_t = now;                                                               \
+    }
+#else
+#define MF_T(k)
+#endif
+__global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int stride) {
+    extern __shared__ float4 mod_lds[];
+    __shared__ ModFastShared M;
+    float* rows = reinterpret_cast<float*>(mod_lds);
+    const unsigned long long f = blockIdx.x;
+    const int step = A.N * A.osr;
+    const int ns = (int)(A.nsyms + 2);
+    const int tid = threadIdx.x;
+    const ChirpWalk W = chirp_walk(A);
+    const double two_pi = 2.0 * (double)kPi;
+#ifdef LPHY_MODFAST_CLOCKS
+    unsigned long long mf_t = 0;
+#endif
+    MF_T(0)
+    // 1. f rows (ChirpGenerator.hpp:39-40) and their exact sums
+    for (int s = tid; s < ns; s += blockDim.x) {
+        float fr = W.fmin + mod_f0(A, f, (unsigned long long)s);
+        float* row = rows + (size_t)s * stride;
+        double t = 0.0;
+        int i = 0;
+        for (; i + 8 <= step; i += 8) {
+            float g[8];
+            float x = fr;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                x += W.fstep;
+                g[k] = x;
+            }
+            if (g[7] > W.fmax) {  // (f only grows between wraps: ChirpWalk::step8)
+                x = fr;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    x += W.fstep;
+                    if (x > W.fmax) x -= (W.fmax - W.fmin);
+                    g[k] = x;
+                }
+            }
+            fr = g[7];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                row[i + k] = g[k];
+                t += (double)g[k];
+            }
+        }
+        for (; i < step; ++i) {
+            fr += W.fstep;
+            if (fr > W.fmax) fr -= (W.fmax - W.fmin);
+            row[i] = fr;
+            t += (double)fr;
+        }
+        M.tot[s] = t;
+    }
+    __syncthreads();
+    MF_T(1)
+    // 2. first estimates of the starts: unwrapped running sums (one add per
+    //    symbol in order), wrapped per symbol in parallel
+    if (tid == 0) {
+        double e = 0.0;
+        for (int s = 0; s < ns; ++s) {
+            M.est[s] = e;
+            e += M.tot[s];
+        }
+        M.ok = 1;
+    }
+    __syncthreads();
+    MF_T(2)
+    // 3. each row walked in float from its estimate: its rounding error, and
+    //    the pivot (largest |phase| among every 8th sample) with the exact
+    //    partial sum up to it
+    for (int s = tid; s < ns; s += blockDim.x) {
+        const float* row = rows + (size_t)s * stride;
+        const double e = M.est[s];
+        const float x0 = (float)(e - floor(e * (1.0 / two_pi)) * two_pi);
+        float p = x0;
+        double q = 0.0, qb = 0.0;
+        float best = -1.0f;
+        int kb = 0;
+        int i = 0;
+        for (; i + 8 <= step; i += 8) {
+            float b[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) b[k] = row[i + k];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                p += b[k];
+                q += (double)b[k];
+            }
+            const float a = fabsf(p);
+            if (a > best) {
+                best = a;
+                kb = i + 7;
+                qb = q;
+            }
+        }
+        for (; i < step; ++i) {
+            p += row[i];
+            q += (double)row[i];
+            if (fabsf(p) > best) {
+                best = fabsf(p);
+                kb = i;
+                qb = q;
+            }
+        }
+        M.err[s] = (double)p - ((double)x0 + M.tot[s]);
+        M.kp[s] = kb;
+        M.piv[s] = qb;
+    }
+    __syncthreads();
+    MF_T(3)
+    // 4. corrected estimates (unwrapped, in order); 5. the windows, and
+    //    symbol 0's pivot walked exactly from 0
+    if (tid == 0) {
+        double e = 0.0;
+        for (int s = 0; s < ns; ++s) {
+            M.est[s] = e;
+            e += M.tot[s] + M.err[s];
+        }
+    }
+    __syncthreads();
+    for (int s = tid; s < ns; s += blockDim.x) {
+        const double e = M.est[s];
+        M.base[s] = f_ord((float)(e - floor(e * (1.0 / two_pi)) * two_pi + M.piv[s])) - kModFastWin / 2;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        float p = 0.0f;
+        const float* row = rows;
+        row_blocks(row, 0, M.kp[0] + 1, [&](int, float x) { p += x; });
+        const int j = f_ord(p) - M.base[0];
+        M.J[0] = j;
+        if (j < 0 || j >= kModFastWin) M.ok = 0;
+    }
+    MF_T(4)
+    // 6. every candidate of every symbol walked to the next symbol's pivot,
+    //    8 candidates (j = g, g + 8, ...) per thread: one LDS read feeds 8
+    //    independent chains
+    constexpr int kPer = 8, kGroups = kModFastWin / kPer;
+    for (int idx = tid; idx < (ns - 1) * kGroups; idx += blockDim.x) {
+        const int s = idx / kGroups, g = idx - s * kGroups;
+        const float* row = rows + (size_t)s * stride;
+        float p[kPer];
+#pragma unroll
+        for (int m = 0; m < kPer; ++m) p[m] = f_unord(M.base[s] + g + kPer * m);
+        row_blocks(row, M.kp[s] + 1, step, [&](int, float x) {
+#pragma unroll
+            for (int m = 0; m < kPer; ++m) p[m] += x;
+        });
+#pragma unroll
+        for (int m = 0; m < kPer; ++m) p[m] = wrap_phase(p[m]);
+        const float* nrow = row + stride;
+        const int kn = M.kp[s + 1];
+        row_blocks(nrow, 0, kn + 1, [&](int, float x) {
+#pragma unroll
+            for (int m = 0; m < kPer; ++m) p[m] += x;
+        });
+        const int b1 = M.base[s + 1];
+#pragma unroll
+        for (int m = 0; m < kPer; ++m) {
+            const int jj = f_ord(p[m]) - b1;
+            M.T[s][g + kPer * m] = (jj >= 0 && jj < kModFastWin) ? (unsigned char)jj : (unsigned char)255;
+        }
+    }
+    __syncthreads();
+    MF_T(5)
+    // 7. the chain, one wave: lane j holds T[s][j], the next candidate is a
+    //    lane read at the current one (uniform); T rows read 16 at a time
+    if (tid < 64 && M.ok) {
+        int j = M.J[0];
+        int bad = 0;
+        for (int s0 = 0; s0 + 1 < ns; s0 += 16) {
+            int t[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) t[k] = s0 + k + 1 < ns ? M.T[s0 + k][tid] : 0;
+            int jv = 0;  // lane k: the candidate of symbol s0 + k + 1
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                if (s0 + k + 1 < ns) {
+                    j = __builtin_amdgcn_readlane(t[k], j & 63);
+                    bad |= j == 255;
+                    jv = tid == k ? j : jv;
+                }
+            }
+            if (tid < 16 && s0 + tid + 1 < ns) M.J[s0 + tid + 1] = jv;
+        }
+        if (bad && tid == 0) M.ok = 0;
+    }
+    __syncthreads();
+    MF_T(6)
+    if (M.ok) {
+        // 8. the rows from their exact pivots: each symbol's tail (after the
+        //    pivot) and, from the start that tail's wrap gives the next
+        //    symbol, each symbol's head (up to its pivot)
+        for (int s = tid; s < ns; s += blockDim.x) {
+            float* row = rows + (size_t)s * stride;
+            float p = f_unord(M.base[s] + M.J[s]);
+            row_blocks(row, M.kp[s] + 1, step, [&](int i, float x) {
+                p += x;
+                row[i] = p;
+            });
+            M.xs[s + 1 < ns ? s + 1 : 0] = s + 1 < ns ? wrap_phase(p) : 0.0f;
+        }
+        __syncthreads();
+        for (int s = tid; s < ns; s += blockDim.x) {
+            float* row = rows + (size_t)s * stride;
+            float p = M.xs[s];
+            row_blocks(row, 0, M.kp[s] + 1, [&](int i, float x) {
+                p += x;
+                row[i] = p;
+            });
+        }
+    } else if (tid == 0) {
+        // the serial walk (k_mod_accumulate's order)
+        if (A.slow) atomicAdd(A.slow, 1ull);
+        float phase = 0.0f;
+        for (int s = 0; s < ns; ++s) {
+            float* row = rows + (size_t)s * stride;
+            for (int i = 0; i < step; ++i) {
+                phase += row[i];
+                row[i] = phase;
+            }
+            phase = wrap_phase(phase);
+        }
+    }
+    __syncthreads();
+    // 9. the phases out, row after row (k_mod_sincos, GPU-wide, turns them
+    //    into IQ: one CU's sincos would be the longest phase)
+    const int count = ns * step;
+    float* out = A.phases + f * (unsigned long long)count;
+    for (int g = tid; g < count; g += blockDim.x) {
+        const int s = g / step;
+        out[g] = rows[(size_t)s * stride + (g - s * step)];
+    }
+    MF_T(7)
+}
+#undef MF_T
 
 __global__ void k_mod_samples(ModArgs A) {
     const unsigned long long g = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;

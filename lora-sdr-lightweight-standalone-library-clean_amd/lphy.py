@@ -361,6 +361,16 @@ class Demodulator:
         _chk(fn(self.ctx, 1, C.byref(n), int(reset)), "lphy_hip_test_counter")
         return int(n.value)
 
+    def mod_serial_count(self, reset: bool = True) -> int:
+        """Test build only: frames the one-launch modulator (k_mod_fast) gave
+        to its serial walk because the candidate chain left its windows
+        (device sync)."""
+        fn = self.lib.lphy_hip_test_counter
+        fn.argtypes = [_vp, C.c_int, C.POINTER(C.c_ulonglong), C.c_int]
+        n = C.c_ulonglong(0)
+        _chk(fn(self.ctx, 8, C.byref(n), int(reset)), "lphy_hip_test_counter")
+        return int(n.value)
+
     def recheck_count(self, reset: bool = True) -> int:
         """Symbols the fused kernel re-ran with the exact rotation (device sync)."""
         n = C.c_ulonglong(0)

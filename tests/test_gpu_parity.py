@@ -131,6 +131,28 @@ def test_modulate_batch_frames(oracle, lphy, sf, osr, nf, nsyms):
         np.testing.assert_array_equal(got[f].view(np.uint32), b.view(np.uint32), err_msg=f"frame {f}")
 
 
+@pytest.mark.parametrize("sf", [5, 6, 7, 8])
+def test_modulate_candidate_chain(oracle, lphy, sf):
+    """The one-launch modulator (k_mod_fast: candidate windows around each
+    symbol's pivot, chained by lookups) == the oracle's serial walk, every
+    float bit, over random packets and constant-symbol ones (all 0, all
+    N-1, a repeated value); and the chain, not its serial fallback, is what
+    ran for nearly every packet (lphy_hip_test_counter 8)."""
+    rng = np.random.default_rng(sf * 31)
+    N = 1 << sf
+    d = lphy.Demodulator(sf, test_build=True)
+    d.mod_serial_count(reset=True)
+    packets = [rng.integers(0, N, 64, dtype=np.uint16) for _ in range(40)]
+    packets += [np.zeros(64, np.uint16), np.full(64, N - 1, np.uint16), np.full(30, N // 3, np.uint16),
+                rng.integers(0, N, 200, dtype=np.uint16), rng.integers(0, N, 1, dtype=np.uint16)]
+    for k, syms in enumerate(packets):
+        a = d.modulate_host(syms, 1.0, 0x34)
+        b = oracle.modulate(syms, sf, sync=0x34)
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32), err_msg=f"packet {k}")
+    slow = d.mod_serial_count()
+    assert slow <= len(packets) // 10, f"{slow} of {len(packets)} packets took the serial walk"
+
+
 def test_modulate_repeated_contexts(oracle, lphy):
     """Stress: many producer calls with fresh contexts and varying sizes
     (guards the phase-scratch hand-off between the two modulate kernels)."""
