@@ -2738,6 +2738,24 @@ __device__ __forceinline__ void row_blocks(const float* row, int i0, int i1, Fn 
     for (; i < i1; ++i) fn(i, row[i]);
 }
 
+// est[s] = sum over r < s of (a[r] + b[r]) (exclusive prefix, unwrapped),
+// one wave, 64 symbols per pass
+__device__ __forceinline__ void mf_scan(double* est, const double* a, const double* b, int ns, int lane) {
+    double carry = 0.0;
+    for (int s0 = 0; s0 < ns; s0 += 64) {
+        const int s = s0 + lane;
+        const double v = s < ns ? a[s] + (b ? b[s] : 0.0) : 0.0;
+        double x = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const double y = __shfl_up(x, off, 64);
+            if (lane >= off) x += y;
+        }
+        if (s < ns) est[s] = carry + (x - v);
+        carry += __shfl(x, 63, 64);
+    }
+}
+
 #ifdef LPHY_MODFAST_CLOCKS  // timing aid only: per-phase wall clock sums into counters 1..7
 #define MF_T(k)                                                                   \
     if (tid == 0) {                                                               \
@@ -2787,10 +2805,9 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
             }
             fr = g[7];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                row[i + k] = g[k];
-                t += (double)g[k];
-            }
+            for (int k = 0; k < 8; ++k) row[i + k] = g[k];
+            t += (((double)g[0] + (double)g[1]) + ((double)g[2] + (double)g[3])) +
+                 (((double)g[4] + (double)g[5]) + ((double)g[6] + (double)g[7]));  // (an estimate)
         }
         for (; i < step; ++i) {
             fr += W.fstep;
@@ -2804,14 +2821,8 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     MF_T(1)
     // 2. first estimates of the starts: unwrapped running sums (one add per
     //    symbol in order), wrapped per symbol in parallel
-    if (tid == 0) {
-        double e = 0.0;
-        for (int s = 0; s < ns; ++s) {
-            M.est[s] = e;
-            e += M.tot[s];
-        }
-        M.ok = 1;
-    }
+    if (tid < 64) mf_scan(M.est, M.tot, nullptr, ns, tid);
+    if (tid == 0) M.ok = 1;
     __syncthreads();
     MF_T(2)
     // 3. each row walked in float from its estimate: its rounding error, and
@@ -2831,10 +2842,9 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
 #pragma unroll
             for (int k = 0; k < 8; ++k) b[k] = row[i + k];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                p += b[k];
-                q += (double)b[k];
-            }
+            for (int k = 0; k < 8; ++k) p += b[k];
+            q += (((double)b[0] + (double)b[1]) + ((double)b[2] + (double)b[3])) +
+                 (((double)b[4] + (double)b[5]) + ((double)b[6] + (double)b[7]));
             const float a = fabsf(p);
             if (a > best) {
                 best = a;
@@ -2859,13 +2869,7 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     MF_T(3)
     // 4. corrected estimates (unwrapped, in order); 5. the windows, and
     //    symbol 0's pivot walked exactly from 0
-    if (tid == 0) {
-        double e = 0.0;
-        for (int s = 0; s < ns; ++s) {
-            M.est[s] = e;
-            e += M.tot[s] + M.err[s];
-        }
-    }
+    if (tid < 64) mf_scan(M.est, M.tot, M.err, ns, tid);
     __syncthreads();
     for (int s = tid; s < ns; s += blockDim.x) {
         const double e = M.est[s];
