@@ -682,7 +682,7 @@ int modulate_impl(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames, size_t
     // ... and when a frame's f rows fit one CU's LDS, the walk by candidate
     // windows and a chain of lookups (k_mod_fast), then the sincos
     const int stride = (int)(c->N * c->osr) + 4;
-    const size_t lds = (nsyms + 2) * (size_t)stride * sizeof(float);
+    const size_t lds = (nsyms + 2) * ((size_t)stride * sizeof(float) + kModFastWin);
     if (LPHY_MOD_FAST && walk_all && nsyms + 2 <= (size_t)kModFastSyms && lds <= kModFastLds) {
         if (lds > (size_t(64) << 10))
             HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_mod_fast),

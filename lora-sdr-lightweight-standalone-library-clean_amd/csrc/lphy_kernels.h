@@ -2695,12 +2695,12 @@ __global__ __launch_bounds__(64) void k_mod_accumulate(ModArgs A) {
 // inside the windows is the serial walk; one that leaves them (an estimate
 // off by more than 32 floats, measured ≤ 19 at SF 7-8: tools/walk_lattice.py)
 // falls back to the serial walk of the whole frame.  Rows `stride` floats
-// apart in LDS; at most kModFastSyms symbols; the phases go to A.phases for
-// k_mod_sincos.
+// apart in LDS, then T (dynamic LDS: up to SF 9 at 66 symbols); at most
+// kModFastSyms symbols; the phases go to A.phases for k_mod_sincos.
 constexpr int kModFastThreads = 1024;
 constexpr int kModFastSyms = 256;
 constexpr int kModFastWin = 64;
-constexpr size_t kModFastLds = size_t(120) << 10;  // the f rows (dynamic)
+constexpr size_t kModFastLds = size_t(144) << 10;  // the f rows and T (dynamic)
 
 __device__ __forceinline__ int f_ord(float x) {
     const int i = __float_as_int(x);
@@ -2719,7 +2719,6 @@ struct ModFastShared {
     int base[kModFastSyms];        // f_ord of the window's first candidate
     int J[kModFastSyms];           // the chain's candidate per symbol
     float xs[kModFastSyms];        // exact symbol starts
-    unsigned char T[kModFastSyms][kModFastWin];  // landing candidate, 255: outside
     int ok;
 };
 
@@ -2774,6 +2773,8 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     const int step = A.N * A.osr;
     const int ns = (int)(A.nsyms + 2);
     const int tid = threadIdx.x;
+    // T[s][j]: where candidate j of symbol s lands among symbol s+1's, 255 outside
+    unsigned char* T = reinterpret_cast<unsigned char*>(rows + (size_t)ns * stride);
     const ChirpWalk W = chirp_walk(A);
     const double two_pi = 2.0 * (double)kPi;
 #ifdef LPHY_MODFAST_CLOCKS
@@ -2911,7 +2912,7 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
 #pragma unroll
         for (int m = 0; m < kPer; ++m) {
             const int jj = f_ord(p[m]) - b1;
-            M.T[s][g + kPer * m] = (jj >= 0 && jj < kModFastWin) ? (unsigned char)jj : (unsigned char)255;
+            T[s * kModFastWin + g + kPer * m] = (jj >= 0 && jj < kModFastWin) ? (unsigned char)jj : (unsigned char)255;
         }
     }
     __syncthreads();
@@ -2924,7 +2925,7 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
         for (int s0 = 0; s0 + 1 < ns; s0 += 16) {
             int t[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) t[k] = s0 + k + 1 < ns ? M.T[s0 + k][tid] : 0;
+            for (int k = 0; k < 16; ++k) t[k] = s0 + k + 1 < ns ? T[(s0 + k) * kModFastWin + tid] : 0;
             int jv = 0;  // lane k: the candidate of symbol s0 + k + 1
 #pragma unroll
             for (int k = 0; k < 16; ++k) {

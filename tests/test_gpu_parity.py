@@ -113,8 +113,8 @@ def test_modulate_bit_exact(oracle, lphy):
                                               (5, 3, 4, 21), (7, 2, 2, 30), (3, 3, 3, 7), (2, 1, 2, 5),
                                               (10, 1, 2, 64), (7, 1, 70, 64)])
 def test_modulate_batch_frames(oracle, lphy, sf, osr, nf, nsyms):
-    """lphy_hip_modulate_batch, frame by frame == the oracle: the one-launch
-    packet kernel (phases in LDS: up to SF 9 at 66 symbols, few frames), the
+    """lphy_hip_modulate_batch, frame by frame == the oracle: k_mod_fast (f
+    rows in LDS: up to SF 9 at 66 symbols, few frames, osr 2-3 too), the
     three-kernel few-symbol form (SF 10) and the batch form (70 frames)."""
     rng = np.random.default_rng(sf * 100 + nf)
     syms = rng.integers(0, 1 << min(sf, 8), (nf, nsyms), dtype=np.uint16)
@@ -131,7 +131,7 @@ def test_modulate_batch_frames(oracle, lphy, sf, osr, nf, nsyms):
         np.testing.assert_array_equal(got[f].view(np.uint32), b.view(np.uint32), err_msg=f"frame {f}")
 
 
-@pytest.mark.parametrize("sf", [5, 6, 7, 8])
+@pytest.mark.parametrize("sf", [5, 6, 7, 8, 9])
 def test_modulate_candidate_chain(oracle, lphy, sf):
     """The one-launch modulator (k_mod_fast: candidate windows around each
     symbol's pivot, chained by lookups) == the oracle's serial walk, every
