@@ -746,15 +746,18 @@ __device__ __forceinline__ UnitResult wunit_result(const cf32 (&v)[64], int h, i
 //     candidate only fails the test;
 //   * Y_k = sum_l W^{k l} sum_a W_8^{k a} sum_b y[l + LPS (8 a + b)] W_64^{k b}
 //     (W_64 / W_8 powers: the correctly rounded 64th roots, read from a
-//     register table by ds_bpermute; W^{k l}: the KISS table entry), and E,
-//     both with per-lane partial sums and a tree over the symbol's lanes;
+//     register table by ds_bpermute; W^{k l} = W_64^{m / LPS} W_N^{m mod LPS}
+//     for m = k l mod N, from that table and a second one of the KISS
+//     entries W_N^s, s < LPS), and E, both with per-lane partial sums and a
+//     tree over the symbol's lanes;
 //   * the samples are taken before the frame's rotation, which is folded
 //     into the twiddles (pv_lane_sums): the staging then skips the two
 //     rotation products per sample, and only a failed unit applies them;
 //   * |dY_k| <= kPvErr u A (A = N sqrt2 amax >= sum |y_n|): the folded
 //     twiddle products (<= 3 u each, two), fused products and 8-term partial
-//     sums (<= 16 u each, two stages), the KISS entry (<= 7.3 u) and its
-//     product (3 u), the tree (<= 6 u): < 58 u; E's relative error (8-term
+//     sums (<= 16 u each, two stages), W^{k l} (the KISS entry W_N^s <= 7.3 u
+//     from the ideal root, root64 <= 1 u, their fused product <= 2 u: <= 10.3
+//     u) and its product (3 u), the tree (<= 6 u): < 58 u; E's relative error (8-term
 //     partial sums, the tree, scale^2) < 26 u (charged 32 u);
 //   * lead = Ylo - sqrt(max(0, N E (1 + 32 u) - Ylo^2)) (1 + 4 u) with
 //     Ylo = sqrt(|Y_k|^2) (1 - 4 u) - kPvErr u A (v_sqrt within 2 u, the
@@ -1394,7 +1397,13 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     // SPAN: the rotation tables of the (at most two) frames of a unit, by
     // frame parity: [scale] e^{j rate i}, i < 8 LPS, then e^{j rate 8 LPS a}
     constexpr int RT = 8 * LPS + 8;
-    __shared__ cf32 rtabs[SPAN ? W::WPB : 1][2][SPAN ? RT : 1];
+    // SPAN mode 0 at SF 7-8 (LDS room): one table per frame instead, t_i =
+    // down_i e^{j rate i} (k_frames' mode-0 table, build_rtab), so a sample's
+    // dechirp and rotation are one fused product (k_frames' certificate:
+    // no charge beyond cert_bound's own, kWaveExtra's two-table share unused)
+    constexpr bool M0T = M0 && SPAN && SF <= 8;
+    __shared__ cf32 rtabs[SPAN && !M0T ? W::WPB : 1][2][SPAN && !M0T ? RT : 1];
+    __shared__ cf32 m0tabs[M0T ? W::WPB : 1][2][M0T ? N : 1];
     __shared__ WSettle settles[SPAN ? W::WPB : 1][SPAN ? W::EPU : 1];  // (SPAN: frames to settle)
     cf32* const dnl = lds_all;
     cf32 (*const sbuf)[W::BUF] = reinterpret_cast<cf32 (*)[W::BUF]>(lds_all + (DN ? N : 0));
@@ -1487,7 +1496,31 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     // Parseval certificate: the 64th roots as a register table (lane j holds
     // root64(j)); tried while no unit of the frame has failed it
     const cf32 rr = root64(lane);
+    // ... and lane s < LPS holds the KISS entry W_N^s: W^{k l} = root64(m / LPS)
+    // W_N^{m mod LPS} (m = k l mod N) from two register tables, so no global
+    // load sits between the next unit's LDS-DMA and the lead (its wait would
+    // be vmcnt(0): the whole DMA)
+    const cf32 rs = A.tw[lane & (LPS - 1)];
     bool pv_on = true;
+    // Adaptive attempts (wave-uniform, speed only: the candidate never
+    // decides what is stored): after a frame whose attempt failed, the next
+    // 2^m - 1 frames skip it (m = consecutive failed frames, at most
+    // kPvBackoff), so input that never certifies this way (mode 0's IQ, whose
+    // offsets put every tone between two bins; noise) pays one attempt per
+    // 2^kPvBackoff frames instead of one per frame; a success resets m.
+#ifndef LPHY_PV_BACKOFF  // (-D0: an attempt on every frame, the round-5 rule; timing A/B)
+#define LPHY_PV_BACKOFF 4
+#endif
+    constexpr unsigned kPvBackoff = LPHY_PV_BACKOFF;
+    unsigned pv_miss = 0, pv_wait = 0;
+    auto pv_frame = [&]() __attribute__((always_inline)) {
+        if (pv_wait != 0) {
+            --pv_wait;
+            pv_on = false;
+        } else {
+            pv_on = true;
+        }
+    };
     // speculative normalisation of the frame in demodulation (lane state)
     constexpr float kBig = 3.0e38f;
     float sp_mx = 0.0f, sp_r = kBig;
@@ -1520,13 +1553,14 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             bool second = false;  // SPAN: the lane's half is in frame k + 1
             unsigned n0 = (unsigned)SPW;
             bool two = false;
+            const lds_cf32* mt = nullptr;  // (M0T: the lane's frame's table)
             if constexpr (SPAN) {
                 n0 = S - cu.s0 < (unsigned)SPW ? S - cu.s0 : (unsigned)SPW;
                 two = n0 < (unsigned)SPW && k + 1 < sch.nk;
                 const WFrame R1 = two ? rec(k + 1) : R0;
                 if (k != rot_frame) {
                     rot_frame = k;
-                    pv_on = true;
+                    pv_frame();
                 }
                 // the rotation tables of frames k and k + 1, built once per
                 // frame (by parity) by the whole wave: the wrot values
@@ -1534,6 +1568,16 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                     if (((kk & 1u) ? tab1 : tab0) == kk) return;
                     if (kk & 1u) tab1 = kk;
                     else tab0 = kk;
+                    if constexpr (M0T) {
+                        lds_cf32* tm = (lds_cf32*)m0tabs[wv][kk & 1u];
+#pragma unroll 1
+                        for (int i = lane; i < N; i += 64) {
+                            float sn, cs;
+                            lphy_libm::sincosf_exact(Rk.rate * (float)i, &sn, &cs);
+                            tm[i] = cmul(dnl[i], cf32{cs, sn});
+                        }
+                        return;
+                    }
                     lds_cf32* tb = (lds_cf32*)rtabs[wv][kk & 1u];
 #pragma unroll 1
                     for (int i = lane; i < RT; i += 64) {
@@ -1556,15 +1600,21 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                     R = R1;
                     fh = fglob(k + 1);
                 }
-                const lds_cf32* tb = (const lds_cf32*)rtabs[wv][(k + (second ? 1u : 0u)) & 1u];
+                if constexpr (M0T) {
+                    mt = (const lds_cf32*)m0tabs[wv][(k + (second ? 1u : 0u)) & 1u];
 #pragma unroll
-                for (int b = 0; b < 8; ++b) Qr[b] = tb[l + LPS * b];
+                    for (int b = 0; b < 8; ++b) Qr[b] = Pr[b] = cf32{1.0f, 0.0f};  // (rotated in the staging)
+                } else {
+                    const lds_cf32* tb = (const lds_cf32*)rtabs[wv][(k + (second ? 1u : 0u)) & 1u];
 #pragma unroll
-                for (int a = 0; a < 8; ++a) Pr[a] = tb[8 * LPS + a];
+                    for (int b = 0; b < 8; ++b) Qr[b] = tb[l + LPS * b];
+#pragma unroll
+                    for (int a = 0; a < 8; ++a) Pr[a] = tb[8 * LPS + a];
+                }
             } else {
                 if (k != rot_frame) {
                     rot_frame = k;
-                    pv_on = true;
+                    pv_frame();
                     const WRot rt = wrot<SF, MODE>(R.rate, R.scale);
 #pragma unroll
                     for (int b = 0; b < 8; ++b) Qr[b] = rt.q[b];
@@ -1607,7 +1657,8 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                     xs[i] = cf32{(float)e, (float)l};
 #endif
                     if constexpr (DECH) ds[i] = lds_ld(dnl, (int)((d0 + (unsigned)((LPS * e) << 3)) & (unsigned)(8 * N - 1)));
-                    if constexpr (M0) ds[i] = dnl[l + LPS * e];
+                    if constexpr (M0T) ds[i] = mt[l + LPS * e];
+                    else if constexpr (M0) ds[i] = dnl[l + LPS * e];
                 }
             };
 #pragma unroll
@@ -1623,7 +1674,8 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                     cf32 p = x;
                     if constexpr (DECH) p = cmul(x, dq[q % SB][i]);
                     amax = max3_abs(amax, p.x, p.y);
-                    if constexpr (M0) p = cmul(p, dq[q % SB][i]);
+                    if constexpr (M0T) p = cmul_fma(p, dq[q % SB][i]);  // dechirp and rotation
+                    else if constexpr (M0) p = cmul(p, dq[q % SB][i]);
                     // (a unit whose symbol is not demodulated transforms whatever
                     // its window holds; nothing of it is stored; the rotation
                     // is applied below, or folded into the Parseval sums)
@@ -1646,8 +1698,9 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                 // Parseval certificate (above): the candidate, its DFT bin
                 // and the energy; the buffer is free after the staging, so
                 // the next unit's IQ is on its way meanwhile
-                const int kc = pv_candidate<SF>(v, l, c.rate);
-                const cf32 wkl = A.tw[(unsigned)(kc * l) & (unsigned)(N - 1)];
+                const int kc = pv_candidate<SF>(v, l, M0T ? 0.0f : c.rate);
+                const unsigned mkl = (unsigned)(kc * l) & (unsigned)(N - 1);
+                const cf32 wkl = cmul_fma(pv_root(rr, (int)(mkl / (unsigned)LPS)), pv_root(rs, (int)(mkl % (unsigned)LPS)));
                 wait_lgkm0();
                 dma_unit(nx);
                 cf32 ykl;
@@ -1661,16 +1714,22 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                     pv_count(A, live && c.ok && l == 0);
                     sym = kc;
                     cgap = lead;
+                    pv_miss = 0;
                 } else {
                     pv_on = false;  // the frame's other units: the transform
+                    if (pv_miss < kPvBackoff) ++pv_miss;
+                    pv_wait = (1u << pv_miss) - 1u;
                     wait_vm0();     // the early DMA has landed before the exchange reuses the buffer
                 }
             }
             WPH(2);
             if (!pv) {
-                // the certified rotation (staging left the samples unrotated)
+                // the certified rotation (staging left the samples unrotated;
+                // M0T: rotated there)
+                if constexpr (!M0T) {
 #pragma unroll
-                for (int e = 0; e < 64; ++e) v[e] = cmul_fma(cmul_fma(v[e], Qr[e & 7]), Pr[e >> 3]);
+                    for (int e = 0; e < 64; ++e) v[e] = cmul_fma(cmul_fma(v[e], Qr[e & 7]), Pr[e >> 3]);
+                }
                 wpass1<SF, true>(v, ctw(A.tw));
 #ifndef LPHY_ABLATE_W_EXCH  // timing experiments only
                 wexchange<SF>(v, buf, h, l);

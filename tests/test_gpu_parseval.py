@@ -73,6 +73,17 @@ def _check_one(oracle, sf, x, mode, syms, meta, ctx):
     assert _bits(meta["time_offset"][0]) == _bits(omet[1]), ctx
 
 
+def _product_one(oracle, dp, sf, x, mode, ctx):
+    """The same frame through the product library (lib/liblphy_hip.so, the
+    fused kernel the tests force with fused_min_frames 0): every output bit
+    against the oracle; returns its exact re-run count."""
+    dp.recheck_count(reset=True)
+    syms, _, meta = dp.demod_host(x[None, :], 1, x.size, mode, 0x1)  # F_DECODE
+    n = dp.recheck_count(reset=True)
+    _check_one(oracle, sf, x, mode, syms, meta, ctx)
+    return n
+
+
 def _pure_tone_frame(sf, amps, gains, seed, nsym=64):
     """Mode-1 input (dechirped samples) built directly: two sync symbols of
     one tone each, then data symbols of len(amps) pure integer tones at
@@ -106,6 +117,7 @@ def test_runner_up_threshold_straddled(oracle, lphy, sf):
     below it every data symbol is re-run exactly; the switch lies where
     |X_a| - |X_b| = N (r - 1) / 2 meets 4 B."""
     d = lphy.Demodulator(sf, test_build=True)
+    dp = lphy.Demodulator(sf)  # the product library's code objects, same frames
     ks = 2.0 ** np.linspace(-22, -8, 29)
     rows = []
     for i, k in enumerate(ks):
@@ -116,9 +128,13 @@ def test_runner_up_threshold_straddled(oracle, lphy, sf):
         syms, _, meta = d.demod_host(x[None, :], 1, x.size, 1, lphy.F_DECODE)
         n_exact, n_pv = d.recheck_count(reset=True), d.parseval_count(reset=True)
         _check_one(oracle, sf, x, 1, syms, meta, f"sf {sf} r-1 {k:.3g}")
-        rows.append((k, n_exact, n_pv))
+        n_prod = _product_one(oracle, dp, sf, x, 1, f"product sf {sf} r-1 {k:.3g}")
+        rows.append((k, n_exact, n_pv, n_prod))
     assert d.bounds_violations() == 0
-    msg = "\n".join(f"r-1 {k:.3g}: exact {n} parseval {p}" for k, n, p in rows)
+    msg = "\n".join(f"r-1 {k:.3g}: exact {n} parseval {p} product exact {q}" for k, n, p, q in rows)
+    # the product build takes the same decisions: the same symbols re-run
+    assert all(n == q for _, n, _, q in rows), msg
+    rows = [r[:3] for r in rows]
     certified = [k for k, n, p in rows if n == 0]
     rerun = [k for k, n, p in rows if n == 64]
     assert certified and rerun, msg
@@ -184,6 +200,7 @@ def test_parseval_threshold_straddled(oracle, lphy, sf):
     which certifies them: nothing is re-run).  Every output bit equals the
     oracle's."""
     d = lphy.Demodulator(sf, test_build=True)
+    dp = lphy.Demodulator(sf)  # the product library's code objects, same frames
     a = 0.3
     rows = []
     for i, dl in enumerate(2.0 ** np.linspace(-20, -6, 43)):
@@ -193,6 +210,7 @@ def test_parseval_threshold_straddled(oracle, lphy, sf):
         syms, _, meta = d.demod_host(x[None, :], 1, x.size, 1, lphy.F_DECODE)
         n_exact, n_pv = d.recheck_count(reset=True), d.parseval_count(reset=True)
         _check_one(oracle, sf, x, 1, syms, meta, f"sf {sf} delta {dl:.3g}")
+        assert _product_one(oracle, dp, sf, x, 1, f"product sf {sf} delta {dl:.3g}") == 0
         lead, B, A = _parseval_leads(x, sf)
         rows.append((dl, lead.min() / B, n_exact, n_pv))
     assert d.bounds_violations() == 0
@@ -209,6 +227,7 @@ def test_parseval_threshold_straddled(oracle, lphy, sf):
 @pytest.mark.parametrize("sf", [7, 8, 9, 10, 11, 12])
 def test_three_tones_take_the_transform(oracle, lphy, sf):
     d = lphy.Demodulator(sf, test_build=True)
+    dp = lphy.Demodulator(sf)
     for i in range(3):
         x = _tones_frame(oracle, sf, lambda s: [1.0, 0.8, 0.8], seed=8000 + sf * 7 + i)
         d.recheck_count(reset=True)
@@ -216,6 +235,7 @@ def test_three_tones_take_the_transform(oracle, lphy, sf):
         syms, _, meta = d.demod_host(x[None, :], 1, x.size, 2, lphy.F_DECODE)
         n_exact, n_pv = d.recheck_count(reset=True), d.parseval_count(reset=True)
         _check_one(oracle, sf, x, 2, syms, meta, f"sf {sf} frame {i}")
+        assert _product_one(oracle, dp, sf, x, 2, f"product sf {sf} frame {i}") == 0
         # Parseval proves the one-tone sync symbols at most (SF 12: its
         # units hold one symbol each); the data symbols: the transform
         assert n_pv <= 2 and n_exact == 0, (n_pv, n_exact)
@@ -242,11 +262,14 @@ def test_awgn_mixed_paths(oracle, lphy, sf, nf, mode):
     dt.parseval_count(reset=True)
     got = dt.demod_host(iq, nf, iq.shape[1], mode, lphy.F_DECODE)
     n_pv = dt.parseval_count(reset=True)
+    # the product library's fused launch over the same batch
+    prod = lphy.Demodulator(sf).demod_host(iq, nf, iq.shape[1], mode, lphy.F_DECODE)
     # the separate launches (no Parseval) as the whole-batch reference
     ref = lphy.Demodulator(sf).demod_host(iq, nf, iq.shape[1], mode, lphy.F_DECODE | lphy.F_UNFUSED)
-    np.testing.assert_array_equal(got[0], ref[0])
-    np.testing.assert_array_equal(got[1], ref[1])
-    np.testing.assert_array_equal(got[2].view(np.uint8), ref[2].view(np.uint8))
+    for out in (got, prod):
+        np.testing.assert_array_equal(out[0], ref[0])
+        np.testing.assert_array_equal(out[1], ref[1])
+        np.testing.assert_array_equal(out[2].view(np.uint8), ref[2].view(np.uint8))
     assert 0 < n_pv < nf * 66, n_pv
     for f in range(0, nf, max(1, nf // 25)):
         if mode == 0:
@@ -254,6 +277,9 @@ def test_awgn_mixed_paths(oracle, lphy, sf, nf, mode):
         else:
             r, osyms, osync, omet = oracle.lora_demodulate(oracle.dechirp(iq[f], sf), sf)
         ctx = f"sf {sf} mode {mode} frame {f} snr {snrs[f]:.1f}"
-        assert got[2]["status"][f] == 0, ctx
-        np.testing.assert_array_equal(got[0][f], osyms, err_msg=ctx)
-        assert _bits(got[2]["cfo"][f]) == _bits(omet[0]), ctx
+        for out, who in ((got, "test build"), (prod, "product")):
+            assert out[2]["status"][f] == 0, (who, ctx)
+            np.testing.assert_array_equal(out[0][f], osyms, err_msg=f"{who} {ctx}")
+            assert out[2]["sync_word"][f] == osync, (who, ctx)
+            assert _bits(out[2]["cfo"][f]) == _bits(omet[0]), (who, ctx)
+            assert _bits(out[2]["time_offset"][f]) == _bits(omet[1]), (who, ctx)
