@@ -1701,8 +1701,10 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                 const int kc = pv_candidate<SF>(v, l, M0T ? 0.0f : c.rate);
                 const unsigned mkl = (unsigned)(kc * l) & (unsigned)(N - 1);
                 const cf32 wkl = cmul_fma(pv_root(rr, (int)(mkl / (unsigned)LPS)), pv_root(rs, (int)(mkl % (unsigned)LPS)));
+                WPH(3);  // (timing builds: slots 3 / 4 time the Parseval candidate / DMA issue)
                 wait_lgkm0();
                 dma_unit(nx);
+                WPH(4);
                 cf32 ykl;
                 float el;
                 pv_lane_sums<SF>(v, kc, rr, Qr, Pr, ykl, el);

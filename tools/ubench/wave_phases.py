@@ -29,5 +29,5 @@ lib.lphy_hip_phase_cycles(wl.dem.ctx, out)  # clear
 ms = wl._event_ms(mode, flags, 1)
 lib.lphy_hip_phase_cycles(wl.dem.ctx, out)
 tot = sum(out) or 1
-names = ["iq_wait", "staging", "pass1", "exchange+dma", "pass2", "top2+cert", "estimate+close", "scan+cursor"]
+names = ["iq_wait", "staging", "parseval_sums+lead | transform: -", "pv_candidate | rot+pass1+exch+dma", "pv_dma_issue | pass2", "top2+cert+stores", "estimate+close", "scan+cursor"]
 print(f"SF{sf} mode {mode} fused {ms:.3f} ms; phase shares: " + ", ".join(f"{n} {out[i] / tot:.3f}" for i, n in enumerate(names)))
