@@ -90,7 +90,7 @@ struct lphy_hip_ctx {
     // of the runtime's pageable path (per-packet latency)
     void* h_stage = nullptr;
     size_t h_stage_bytes = 0;
-    unsigned long long* d_counters = nullptr;  // [0] rechecks, [1..8] phase clocks (experiments)
+    unsigned long long* d_counters = nullptr;  // kCounters slots (lphy_testing.h: kCtr*)
     size_t stage_bytes = 0;
     // the streaming entry point's pinned slots and streams (lphy_stream.hip),
     // made by its first call, kept for the next ones, freed with the context
@@ -99,6 +99,7 @@ struct lphy_hip_ctx {
     // smallest batch the fused kernels take on this context (-1: the measured
     // per-SF crossover, fused_min_frames; lphy_hip_ctx_set_fused_min_frames)
     std::atomic<long> fused_min{-1};
+    std::atomic<int> mod_force_serial{0};  // (test build: lphy_hip_test_mod_force_serial)
     // (per-call scratch of the device entry points - the SF 11-12 speculation
     // records, the producer's phases, the compensation's shift buffer - comes
     // from the stream-ordered allocator on the caller's stream, so concurrent
@@ -320,8 +321,8 @@ namespace {
 // A context's own state: the host entry points' stream and the counters
 // (the tables are set by the caller).
 int ctx_own_state(lphy_hip_ctx* c) {
-    if (hipMalloc(&c->d_counters, 9 * sizeof(unsigned long long)) != hipSuccess) return -ENOMEM;
-    HIP_OK(hipMemset(c->d_counters, 0, 9 * sizeof(unsigned long long)));
+    if (hipMalloc(&c->d_counters, kCounters * sizeof(unsigned long long)) != hipSuccess) return -ENOMEM;
+    HIP_OK(hipMemset(c->d_counters, 0, kCounters * sizeof(unsigned long long)));
     HIP_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     return 0;
 }
@@ -511,7 +512,7 @@ int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t f
     // two streams, prologue of chunk c+1 beside the symbol kernel of chunk
     // c: the co-running kernels slowed each other ~2x, 1.1x slower overall.)
     // (LPHY_F_FRAMES_KERNEL, test build: k_frames where k_wave would run -
-    // the SF 7-8 matrix-core tests)
+    // SF 7-10; the matrix-core tests)
     const bool wfit = wave_fit(c->sf, c->osr, c->window, A.est_units, total, mode, A) &&
                       !(flags & LPHY_F_FRAMES_KERNEL);
     const bool fused = (all || (stages & both) == both) && !(flags & LPHY_F_UNFUSED) &&
@@ -558,8 +559,8 @@ int lphy_hip_phase_cycles(lphy_hip_ctx* c, unsigned long long* out8) {
     if (!c || !out8) return -EINVAL;
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(out8, c->d_counters + 1, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemset(c->d_counters + 1, 0, 8 * sizeof(unsigned long long)));
+    HIP_OK(hipMemcpy(out8, c->d_counters + kCtrClocks, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemset(c->d_counters + kCtrClocks, 0, 8 * sizeof(unsigned long long)));
     return 0;
 }
 #endif
@@ -656,6 +657,37 @@ size_t mod_scratch_bytes(const lphy_hip_ctx* c, size_t frames, size_t nsyms) {
            (nph < mod_walk_all_below ? align_up(nph * (size_t)c->N * c->osr * sizeof(float)) : 0);
 }
 
+// k_mod_fast's dynamic LDS limit on the context's device, found once per
+// device: the device's LDS per workgroup less the kernel's static LDS
+// (ModFastShared), and the kernel's attribute raised to it once, outside the
+// per-packet path (the limit was a gfx950 constant, set per call).
+struct ModFastLimits {
+    size_t lds = 0;
+};
+const ModFastLimits& mod_fast_limits(int device) {
+    static ModFastLimits lim[64];
+    static std::once_flag once[64];
+    const int d = device >= 0 && device < 64 ? device : 0;
+    std::call_once(once[d], [d] {
+        int cur = 0, per_block = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(d);
+        (void)hipDeviceGetAttribute(&per_block, hipDeviceAttributeMaxSharedMemoryPerBlock, d);
+        size_t stat = 0;
+        hipFuncAttributes fa{};
+        if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_mod_fast<false>)) == hipSuccess)
+            stat = fa.sharedSizeBytes;
+        size_t avail = per_block > 0 && (size_t)per_block > stat ? (size_t)per_block - stat : 0;
+        if (avail > kModFastLds) avail = kModFastLds;
+        for (const void* k : {reinterpret_cast<const void*>(k_mod_fast<false>), reinterpret_cast<const void*>(k_mod_fast<true>)})
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)avail) != hipSuccess)
+                avail = std::min<size_t>(avail, size_t(64) << 10);  // the default limit stands
+        lim[d].lds = avail;
+        (void)hipSetDevice(cur);
+    });
+    return lim[d];
+}
+
 int modulate_impl(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames, size_t nsyms,
                   float* d_iq, float amplitude, uint8_t sync, hipStream_t st, void* lent) {
     ModArgs A{};
@@ -668,7 +700,10 @@ int modulate_impl(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames, size_t
     A.bws = (float)c->bw_hz / 125000.0f;
     A.ampl = std::max(-1.0f, std::min(1.0f, amplitude));  // LoRaMod.cpp:18
     A.sync = sync;
-    A.slow = c->d_counters + 8;  // lphy_hip_test_counter(8)
+    A.slow = c->d_counters + kCtrModSerial;  // lphy_hip_test_counter(kCtrModSerial)
+#ifdef LPHY_TEST_PATHS
+    A.force_serial = c->mod_force_serial.load(std::memory_order_relaxed);
+#endif
     const size_t nph = frames * (nsyms + 2);
     const size_t samples = nph * (size_t)c->N * c->osr;
     // few symbols: every sample's phase from the walk, then sample-parallel
@@ -679,15 +714,20 @@ int modulate_impl(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames, size_t
     A.phase0 = static_cast<float*>(scratch.p);
     A.phases = walk_all ? reinterpret_cast<float*>(static_cast<char*>(scratch.p) + align_up(nph * sizeof(float)))
                         : nullptr;
-    // ... and when a frame's f rows fit one CU's LDS, the walk by candidate
-    // windows and a chain of lookups (k_mod_fast), then the sincos
+    // ... then the walk by candidate windows and a chain of lookups
+    // (k_mod_fast): with the f rows in LDS when they fit there beside the
+    // kernel's static LDS (up to SF 9 at 66 symbols), else in A.phases
+    // (k_mod_fast<true>), then the sincos
     const int stride = (int)(c->N * c->osr) + 4;
-    const size_t lds = (nsyms + 2) * ((size_t)stride * sizeof(float) + kModFastWin);
-    if (LPHY_MOD_FAST && walk_all && nsyms + 2 <= (size_t)kModFastSyms && lds <= kModFastLds) {
-        if (lds > (size_t(64) << 10))
-            HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_mod_fast),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kModFastLds));
-        hipLaunchKernelGGL(k_mod_fast, dim3((unsigned)frames), dim3(kModFastThreads), lds, st, A, stride);
+    const size_t ns = nsyms + 2;
+    const size_t lds = ns * ((size_t)stride * sizeof(float) + kModFastWin);
+    const ModFastLimits& lim = mod_fast_limits(c->device);
+    if (LPHY_MOD_FAST && walk_all && ns <= (size_t)kModFastSyms && (lds <= lim.lds || ns * kModFastWin <= lim.lds)) {
+        if (lds <= lim.lds)
+            hipLaunchKernelGGL(k_mod_fast<false>, dim3((unsigned)frames), dim3(kModFastThreads), lds, st, A, stride);
+        else
+            hipLaunchKernelGGL(k_mod_fast<true>, dim3((unsigned)frames), dim3(kModFastThreads), ns * kModFastWin, st,
+                               A, (int)(c->N * c->osr));
         hipLaunchKernelGGL(k_mod_sincos, dim3((unsigned)((samples + 255) / 256)), dim3(256), 0, st, A,
                            (unsigned long long)samples);
     } else if (walk_all) {
@@ -731,16 +771,25 @@ int lphy_hip_recheck_count(lphy_hip_ctx* c, unsigned long long* out, int reset) 
     if (!c || !out) return -EINVAL;
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(out, c->d_counters, sizeof(*out), hipMemcpyDeviceToHost));
-    if (reset) HIP_OK(hipMemset(c->d_counters, 0, sizeof(*out)));
+    HIP_OK(hipMemcpy(out, c->d_counters + kCtrRecheck, sizeof(*out), hipMemcpyDeviceToHost));
+    if (reset) HIP_OK(hipMemset(c->d_counters + kCtrRecheck, 0, sizeof(*out)));
     return 0;
 }
 
 #ifdef LPHY_TEST_PATHS
 // Test build only (csrc/lphy_testing.h): the context's device counter `idx`
-// (1: symbols the wave kernels certified by Parseval).  Synchronises.
+// (kCtrParseval: symbols the wave kernels certified by Parseval; kCtrModSerial:
+// frames k_mod_fast walked serially).  Synchronises.
+// Test build only: every k_mod_fast frame takes the serial walk (its
+// fallback, otherwise reached only when a candidate chain leaves its windows).
+int lphy_hip_test_mod_force_serial(lphy_hip_ctx* c, int on) {
+    if (!c) return -EINVAL;
+    c->mod_force_serial.store(on ? 1 : 0, std::memory_order_relaxed);
+    return 0;
+}
+
 int lphy_hip_test_counter(lphy_hip_ctx* c, int idx, unsigned long long* out, int reset) {
-    if (!c || !out || idx < 0 || idx > 8) return -EINVAL;
+    if (!c || !out || idx < 0 || idx >= kCounters) return -EINVAL;
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipDeviceSynchronize());
     HIP_OK(hipMemcpy(out, c->d_counters + idx, sizeof(*out), hipMemcpyDeviceToHost));

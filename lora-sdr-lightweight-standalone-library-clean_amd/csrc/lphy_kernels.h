@@ -39,6 +39,8 @@
 #include <type_traits>
 #include <vector>
 
+#include "lphy_testing.h"  // (the device counter slots)
+
 #include "../../include/lphy_hip.h"
 #include "libm_exact.h"
 #include "lphy_testing.h"
@@ -931,9 +933,9 @@ __global__ __launch_bounds__(kTile, OCC) void k_demod(DemodArgs A) {
     }
 #ifdef LPHY_PROFILE_PHASES
     if ((tid & 63) == 0) {
-        atomicAdd(&A.counters[1], ph_stage);
-        atomicAdd(&A.counters[2], ph_fft);
-        atomicAdd(&A.counters[3], ph_tail);
+        atomicAdd(&A.counters[kCtrClocks + 0], ph_stage);
+        atomicAdd(&A.counters[kCtrClocks + 1], ph_fft);
+        atomicAdd(&A.counters[kCtrClocks + 2], ph_tail);
     }
 #endif
 }
@@ -1800,10 +1802,10 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     }
 #ifdef LPHY_PROFILE_PHASES
     if (lane == 0) {
-        atomicAdd(&A.counters[1], ph_mix);
-        atomicAdd(&A.counters[2], ph_sym);
-        atomicAdd(&A.counters[3], ph_fold);
-        atomicAdd(&A.counters[4], n_mix);
+        atomicAdd(&A.counters[kCtrClocks + 0], ph_mix);
+        atomicAdd(&A.counters[kCtrClocks + 1], ph_sym);
+        atomicAdd(&A.counters[kCtrClocks + 2], ph_fold);
+        atomicAdd(&A.counters[kCtrClocks + 3], n_mix);
     }
 #endif
 }
@@ -2208,7 +2210,25 @@ __device__ void recheck_frames(const DemodArgs& A, unsigned long long fb, bool m
             const unsigned long long f = fb + tid;
             const bool hs = mm.have_sync != 0;
             const uint16_t* out = A.syms + f * A.out_per_frame;
+            const unsigned ofs = hs ? 2u : 0u;
             for (; cur < S; ++cur) {
+                if (cur >= ofs) {
+                    // eight data symbols at once where they sit in one aligned
+                    // 16-B word: a clean word is skipped whole (one load per 8
+                    // symbols instead of a dependent load per symbol; mode A's
+                    // SF 7 fix-up 41 -> see DESIGN)
+                    const unsigned d = cur - ofs;
+                    const uint16_t* p = out + d;
+                    if ((d & 7u) == 0u && d + 8u <= (unsigned)A.out_per_frame &&
+                        ((unsigned long long)p & 15ull) == 0ull) {
+                        const uint4 q = *reinterpret_cast<const uint4*>(p);
+                        auto hit = [](unsigned x) { return (x & 0xffffu) == kSymRecheck || (x >> 16) == kSymRecheck; };
+                        if (!(hit(q.x) || hit(q.y) || hit(q.z) || hit(q.w))) {
+                            cur += 7u;  // (+1 by the loop)
+                            continue;
+                        }
+                    }
+                }
                 const uint16_t v = (hs && cur < 2) ? (cur == 0 ? mm.sw0 : mm.sw1) : out[hs ? cur - 2 : cur];
                 if (v != kSymRecheck) continue;
                 const unsigned k = atomicAdd(&sh.count, 1u);
@@ -2244,7 +2264,7 @@ __device__ void recheck_frames(const DemodArgs& A, unsigned long long fb, bool m
             __syncthreads();
         }
     }
-    if (tid == 0 && done) atomicAdd(&A.counters[0], done);
+    if (tid == 0 && done) atomicAdd(&A.counters[kCtrRecheck], done);
 }
 
 // Frames k_frames demodulated under a speculative normalisation that the
@@ -2493,6 +2513,7 @@ struct ModArgs {
     float bws, ampl;
     uint8_t sync;
     unsigned long long* slow;  // (k_mod_fast) frames that took the serial walk
+    int force_serial;          // (test build) k_mod_fast takes its serial walk for every frame
 };
 
 __device__ __forceinline__ float mod_f0(const ModArgs& A, unsigned long long f, unsigned long long s) {
@@ -2697,6 +2718,13 @@ __global__ __launch_bounds__(64) void k_mod_accumulate(ModArgs A) {
 // falls back to the serial walk of the whole frame.  Rows `stride` floats
 // apart in LDS, then T (dynamic LDS: up to SF 9 at 66 symbols); at most
 // kModFastSyms symbols; the phases go to A.phases for k_mod_sincos.
+// GROWS (round 6, frames whose rows do not fit the LDS: SF 10-12): the rows
+// live in A.phases itself (stride = step, where k_mod_sincos reads the
+// phases anyway), only T in dynamic LDS; the walks read them through L1/L2
+// (one frame's rows: 66 x 16 KiB at SF 12), 16 candidates per thread in the
+// candidate walks (one load per 16 chains).  The drift of the corrected
+// estimates stays inside the window there too: <= 27 floats at SF 10-12
+// after one correction (tools/walk_lattice.py 10 11 12, host).
 constexpr int kModFastThreads = 1024;
 constexpr int kModFastSyms = 256;
 constexpr int kModFastWin = 64;
@@ -2755,26 +2783,28 @@ __device__ __forceinline__ void mf_scan(double* est, const double* a, const doub
     }
 }
 
-#ifdef LPHY_MODFAST_CLOCKS  // timing aid only: per-phase wall clock sums into counters 1..7
+#ifdef LPHY_MODFAST_CLOCKS  // timing aid only: per-phase wall clock sums into the clock counters
 #define MF_T(k)                                                                   \
     if (tid == 0) {                                                               \
         const unsigned long long now = wall_clock64();                            \
-        if (k > 0) atomicAdd(A.slow - 8 + k, now - mf_t);                         \
+        if (k > 0) atomicAdd(A.slow - kCtrModSerial + kCtrClocks + k - 1, now - mf_t); \
         mf_t = now;                                                               \
     }
 #else
 #define MF_T(k)
 #endif
+template <bool GROWS>
 __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int stride) {
     extern __shared__ float4 mod_lds[];
     __shared__ ModFastShared M;
-    float* rows = reinterpret_cast<float*>(mod_lds);
     const unsigned long long f = blockIdx.x;
     const int step = A.N * A.osr;
     const int ns = (int)(A.nsyms + 2);
     const int tid = threadIdx.x;
+    float* rows = GROWS ? A.phases + f * (unsigned long long)ns * step : reinterpret_cast<float*>(mod_lds);
     // T[s][j]: where candidate j of symbol s lands among symbol s+1's, 255 outside
-    unsigned char* T = reinterpret_cast<unsigned char*>(rows + (size_t)ns * stride);
+    unsigned char* T = GROWS ? reinterpret_cast<unsigned char*>(mod_lds)
+                             : reinterpret_cast<unsigned char*>(rows + (size_t)ns * stride);
     const ChirpWalk W = chirp_walk(A);
     const double two_pi = 2.0 * (double)kPi;
 #ifdef LPHY_MODFAST_CLOCKS
@@ -2823,7 +2853,7 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     // 2. first estimates of the starts: unwrapped running sums (one add per
     //    symbol in order), wrapped per symbol in parallel
     if (tid < 64) mf_scan(M.est, M.tot, nullptr, ns, tid);
-    if (tid == 0) M.ok = 1;
+    if (tid == 0) M.ok = A.force_serial ? 0 : 1;  // (force_serial: test build, the fallback's tests)
     __syncthreads();
     MF_T(2)
     // 3. each row walked in float from its estimate: its rounding error, and
@@ -2887,15 +2917,15 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     }
     MF_T(4)
     // 6. every candidate of every symbol walked to the next symbol's pivot,
-    //    8 candidates (j = g, g + 8, ...) per thread: one LDS read feeds 8
-    //    independent chains
-    constexpr int kPer = 8, kGroups = kModFastWin / kPer;
+    //    kPer candidates (j = g, g + kGroups, ...) per thread: one read of
+    //    the row feeds kPer independent chains (8 from LDS, 16 from GROWS)
+    constexpr int kPer = GROWS ? 16 : 8, kGroups = kModFastWin / kPer;
     for (int idx = tid; idx < (ns - 1) * kGroups; idx += blockDim.x) {
         const int s = idx / kGroups, g = idx - s * kGroups;
         const float* row = rows + (size_t)s * stride;
         float p[kPer];
 #pragma unroll
-        for (int m = 0; m < kPer; ++m) p[m] = f_unord(M.base[s] + g + kPer * m);
+        for (int m = 0; m < kPer; ++m) p[m] = f_unord(M.base[s] + g + kGroups * m);
         row_blocks(row, M.kp[s] + 1, step, [&](int, float x) {
 #pragma unroll
             for (int m = 0; m < kPer; ++m) p[m] += x;
@@ -2912,7 +2942,7 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
 #pragma unroll
         for (int m = 0; m < kPer; ++m) {
             const int jj = f_ord(p[m]) - b1;
-            T[s * kModFastWin + g + kPer * m] = (jj >= 0 && jj < kModFastWin) ? (unsigned char)jj : (unsigned char)255;
+            T[s * kModFastWin + g + kGroups * m] = (jj >= 0 && jj < kModFastWin) ? (unsigned char)jj : (unsigned char)255;
         }
     }
     __syncthreads();
@@ -2978,7 +3008,9 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     }
     __syncthreads();
     // 9. the phases out, row after row (k_mod_sincos, GPU-wide, turns them
-    //    into IQ: one CU's sincos would be the longest phase)
+    //    into IQ: one CU's sincos would be the longest phase); GROWS: they
+    //    are there already
+    if constexpr (GROWS) return;
     const int count = ns * step;
     float* out = A.phases + f * (unsigned long long)count;
     for (int g = tid; g < count; g += blockDim.x) {

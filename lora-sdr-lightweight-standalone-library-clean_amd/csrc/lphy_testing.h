@@ -12,6 +12,16 @@
 
 #include <cstdlib>
 
+// A context's device counters (lphy_hip_ctx::d_counters, kCounters slots),
+// each with a slot of its own (the modulator's fallback count
+// shared slot 8 with the phase clocks, and the modulator clocks slot 1 with
+// the Parseval count):
+constexpr int kCtrRecheck = 0;    // symbols re-run exactly (lphy_hip_recheck_count)
+constexpr int kCtrParseval = 1;   // test build: symbols the wave kernel certified by Parseval
+constexpr int kCtrModSerial = 2;  // frames k_mod_fast gave to its serial walk
+constexpr int kCtrClocks = 8;     // timing builds only: 8 phase-clock sums (lphy_hip_phase_cycles)
+constexpr int kCounters = 16;
+
 enum lphy_test_flags {
     LPHY_F_EXACT_ROTATION = 64u,   // every symbol with the reference's per-sample
                                    // sincos rotation instead of the certified

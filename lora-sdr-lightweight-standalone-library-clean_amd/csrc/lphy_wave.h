@@ -772,12 +772,12 @@ __device__ __forceinline__ UnitResult wunit_result(const cf32 (&v)[64], int h, i
 // ---------------------------------------------------------------------------
 constexpr float kPvErr = 64.0f;
 
-// Test build: symbols certified by Parseval, summed in counters[1]
+// Test build: symbols certified by Parseval, summed in counters[kCtrParseval]
 // (lphy_hip_test_counter; tests/test_gpu_parseval.py).
 __device__ __forceinline__ void pv_count(const DemodArgs& A, bool mine) {
 #ifdef LPHY_TEST_PATHS
     const unsigned long long m = __ballot(mine);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&A.counters[1], (unsigned long long)__popcll(m));
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&A.counters[kCtrParseval], (unsigned long long)__popcll(m));
 #else
     (void)A;
     (void)mine;
@@ -798,6 +798,19 @@ __device__ __forceinline__ float half_sum(float x) {
     if constexpr (LPS >= 16) x = x + dpp_f32<0x140>(x);  // row_mirror: 16
     if constexpr (LPS >= 32) x = x + __shfl_xor(x, 16, 64);
     if constexpr (LPS >= 64) x = x + __shfl_xor(x, 32, 64);
+    return x;
+}
+// Max over the LPS lanes of each symbol, by DPP as half_sum (mode 0's
+// per-symbol amax: no LDS round trip of __shfl_xor in the unit's path).
+template <int LPS>
+__device__ __forceinline__ float half_max(float x) {
+    static_assert(LPS >= 2 && LPS <= 64 && (LPS & (LPS - 1)) == 0, "2 to 64 lanes per symbol");
+    x = fmaxf(x, dpp_f32<0xB1>(x));                             // quad_perm [1,0,3,2]
+    if constexpr (LPS >= 4) x = fmaxf(x, dpp_f32<0x4E>(x));     // quad_perm [2,3,0,1]
+    if constexpr (LPS >= 8) x = fmaxf(x, dpp_f32<0x141>(x));    // row_half_mirror
+    if constexpr (LPS >= 16) x = fmaxf(x, dpp_f32<0x140>(x));  // row_mirror
+    if constexpr (LPS >= 32) x = fmaxf(x, __shfl_xor(x, 16, 64));
+    if constexpr (LPS >= 64) x = fmaxf(x, __shfl_xor(x, 32, 64));
     return x;
 }
 // root64(idx) for a per-lane idx from the register table rr = root64(lane)
@@ -1273,7 +1286,7 @@ struct WOut {
 };
 
 // Timing experiments only (-DLPHY_PROFILE_PHASES, tools/ubench): per-wave
-// clock sums of the unit phases, added to A.counters[1..8] at the end.
+// clock sums of the unit phases, added to the clock counters at the end.
 #ifdef LPHY_PROFILE_PHASES
 #define WPH_DECL unsigned long long wph[8] = {}, wpt = clock64();
 #define WPH(i)                                  \
@@ -1284,7 +1297,7 @@ struct WOut {
     } while (0)
 #define WPH_FLUSH(A)                                                  \
     if ((threadIdx.x & 63) == 0)                                      \
-        for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&(A).counters[1 + i_], wph[i_]);
+        for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&(A).counters[kCtrClocks + i_], wph[i_]);
 #else
 #define WPH_DECL
 #define WPH(i) \
@@ -1686,8 +1699,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
             WPH(1);
             float am = 1.0f;  // modes 1/2: normalised frame (see fast_certified)
             if constexpr (M0) {
-#pragma unroll
-                for (int off = 1; off < LPS; off <<= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
+                amax = half_max<LPS>(amax);
                 am = amax;
             }
             const float cb1 = cert_bound<SF>(c.rate, c.start, 1.0f, kWaveExtra);

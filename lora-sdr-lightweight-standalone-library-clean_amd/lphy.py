@@ -45,7 +45,7 @@ F_UNFUSED = 32  # separate prologue / symbol launches (lphy_hip.h)
 F_EXACT_ROTATION = 64  # every symbol with the reference's per-sample rotation
 F_SCAN_FIRST = 256  # modes 1/2: whole-frame max-abs pre-scan (no speculation)
 F_DEBUG_RECHECK = 512  # every symbol / estimated frame left to the exact re-run
-F_FRAMES_KERNEL = 1024  # SF 7-9: k_frames where k_wave would run (matrix-core tests)
+F_FRAMES_KERNEL = 1024  # SF 7-10: k_frames where k_wave would run (test build; matrix-core tests)
 WINDOW_NONE = 0
 WINDOW_HANN = 1
 # Smallest batch new Demodulators send to the fused kernels
@@ -358,7 +358,7 @@ class Demodulator:
         fn = self.lib.lphy_hip_test_counter
         fn.argtypes = [_vp, C.c_int, C.POINTER(C.c_ulonglong), C.c_int]
         n = C.c_ulonglong(0)
-        _chk(fn(self.ctx, 1, C.byref(n), int(reset)), "lphy_hip_test_counter")
+        _chk(fn(self.ctx, 1, C.byref(n), int(reset)), "lphy_hip_test_counter")  # kCtrParseval
         return int(n.value)
 
     def mod_serial_count(self, reset: bool = True) -> int:
@@ -368,8 +368,14 @@ class Demodulator:
         fn = self.lib.lphy_hip_test_counter
         fn.argtypes = [_vp, C.c_int, C.POINTER(C.c_ulonglong), C.c_int]
         n = C.c_ulonglong(0)
-        _chk(fn(self.ctx, 8, C.byref(n), int(reset)), "lphy_hip_test_counter")
+        _chk(fn(self.ctx, 2, C.byref(n), int(reset)), "lphy_hip_test_counter")  # kCtrModSerial
         return int(n.value)
+
+    def mod_force_serial(self, on: bool) -> None:
+        """Test build only: k_mod_fast takes its serial walk for every frame."""
+        fn = self.lib.lphy_hip_test_mod_force_serial
+        fn.argtypes = [_vp, C.c_int]
+        _chk(fn(self.ctx, int(bool(on))), "lphy_hip_test_mod_force_serial")
 
     def recheck_count(self, reset: bool = True) -> int:
         """Symbols the fused kernel re-ran with the exact rotation (device sync)."""

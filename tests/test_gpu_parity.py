@@ -131,18 +131,19 @@ def test_modulate_batch_frames(oracle, lphy, sf, osr, nf, nsyms):
         np.testing.assert_array_equal(got[f].view(np.uint32), b.view(np.uint32), err_msg=f"frame {f}")
 
 
-@pytest.mark.parametrize("sf", [5, 6, 7, 8, 9])
+@pytest.mark.parametrize("sf", [5, 6, 7, 8, 9, 10, 11, 12])
 def test_modulate_candidate_chain(oracle, lphy, sf):
     """The one-launch modulator (k_mod_fast: candidate windows around each
-    symbol's pivot, chained by lookups) == the oracle's serial walk, every
-    float bit, over random packets and constant-symbol ones (all 0, all
-    N-1, a repeated value); and the chain, not its serial fallback, is what
-    ran for nearly every packet (lphy_hip_test_counter 8)."""
+    symbol's pivot, chained by lookups; f rows in LDS up to SF 9, in the
+    phase buffer from SF 10) == the oracle's serial walk, every float bit,
+    over random packets and constant-symbol ones (all 0, all N-1, a repeated
+    value); and the chain, not its serial fallback, is what ran for nearly
+    every packet (lphy_hip_test_counter kCtrModSerial)."""
     rng = np.random.default_rng(sf * 31)
     N = 1 << sf
     d = lphy.Demodulator(sf, test_build=True)
     d.mod_serial_count(reset=True)
-    packets = [rng.integers(0, N, 64, dtype=np.uint16) for _ in range(40)]
+    packets = [rng.integers(0, N, 64, dtype=np.uint16) for _ in range(40 if sf <= 9 else 15)]
     packets += [np.zeros(64, np.uint16), np.full(64, N - 1, np.uint16), np.full(30, N // 3, np.uint16),
                 rng.integers(0, N, 200, dtype=np.uint16), rng.integers(0, N, 1, dtype=np.uint16)]
     for k, syms in enumerate(packets):
@@ -151,6 +152,29 @@ def test_modulate_candidate_chain(oracle, lphy, sf):
         np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32), err_msg=f"packet {k}")
     slow = d.mod_serial_count()
     assert slow <= len(packets) // 10, f"{slow} of {len(packets)} packets took the serial walk"
+
+
+@pytest.mark.parametrize("sf,osr", [(5, 1), (7, 1), (8, 1), (9, 1), (10, 1), (12, 1), (7, 2), (5, 3), (9, 2)])
+def test_modulate_forced_serial_fallback(oracle, lphy, sf, osr):
+    """k_mod_fast's serial fallback (the whole frame walked in order by one
+    thread, taken when a candidate chain leaves its windows) forced for
+    every packet by the test build's switch: every float bit == the oracle's,
+    and the fallback counter counts every packet."""
+    rng = np.random.default_rng(sf * 7 + osr)
+    N = 1 << sf
+    d = lphy.Demodulator(sf, 125000, osr, test_build=True)
+    d.mod_force_serial(True)
+    d.mod_serial_count(reset=True)
+    packets = [rng.integers(0, N, 64, dtype=np.uint16) for _ in range(3)] + [np.zeros(5, np.uint16)]
+    for k, syms in enumerate(packets):
+        a = d.modulate_host(syms, 1.0, 0x34)
+        b = oracle.modulate(syms, sf, osr=osr, sync=0x34)
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32), err_msg=f"packet {k}")
+    assert d.mod_serial_count() == len(packets)
+    d.mod_force_serial(False)
+    a = d.modulate_host(packets[0], 1.0, 0x34)
+    np.testing.assert_array_equal(a.view(np.uint32), oracle.modulate(packets[0], sf, osr=osr, sync=0x34).view(np.uint32))
+    assert d.mod_serial_count() == 0
 
 
 def test_modulate_repeated_contexts(oracle, lphy):

@@ -31,7 +31,7 @@ def main():
         lib.lphy_hip_phase_cycles(d.ctx, out)
         us = [out[k] / n / 100.0 for k in range(7)]  # wall_clock64: 100 MHz
         print(f"SF{sf}: total {sum(us):.1f} us: " + ", ".join(f"{a} {b:.1f}" for a, b in zip(NAMES, us)),
-              f"| serial fallbacks {out[7]}", flush=True)
+              flush=True)
         d.close()
 
 
