@@ -167,16 +167,17 @@ inline bool frames_fit(unsigned sf, unsigned osr, int est_units, size_t total) {
 // takes this batch: SF 7-12, osr 1, the two-symbol estimate, no window, the
 // certified rotation, in modes 1/2 the speculative normalisation, and below
 // SF 9 at least one unit of symbols per frame (4096 / N: its units span
-// frames there).  Hann windows, LPHY_F_EXACT_ROTATION, the pre-scan schedule
-// and shorter frames stay on k_frames (SF <= 10) or the separate launches
-// (SF 11-12).
+// frames there); a Hann window up to SF 11 (round 6: its N floats beside the
+// down-chirp in LDS; SF 12's LDS is full).  LPHY_F_EXACT_ROTATION, the
+// pre-scan schedule, shorter frames and SF 12 windows stay on k_frames (SF
+// <= 10) or the separate launches (SF 11-12).
 #ifndef LPHY_WAVE_MIN_SF  // smallest SF on k_wave (-D for timing experiments only)
 #define LPHY_WAVE_MIN_SF 7
 #endif
 inline bool wave_fit(unsigned sf, unsigned osr, int window, int est_units, size_t total, int mode,
                      const DemodArgs& A) {
     return sf >= LPHY_WAVE_MIN_SF && sf <= 12 && (sf >= 9 || total >= (size_t)(4096u >> sf)) && osr == 1 &&
-           window == LPHY_WINDOW_NONE && est_units == 2 && total >= 2 && !A.exact_rotation &&
+           (window == LPHY_WINDOW_NONE || sf <= 11) && est_units == 2 && total >= 2 && !A.exact_rotation &&
            (mode == LPHY_MODE_DEMODULATE || A.spec);
 }
 
@@ -651,19 +652,35 @@ constexpr size_t mod_walk_all_below = 4096;
 #define LPHY_MOD_FAST 1
 #endif
 
+struct ModFastLimits {
+    size_t lds = 0;
+};
+const ModFastLimits& mod_fast_limits(int device);
+
+// Which modulator form a call takes (modulate_impl): 0 the three-kernel or
+// batch forms, 1 k_mod_fast with the f rows in LDS, 2 k_mod_fast's split
+// form with the f rows in the phase buffer (GROWS: k_mod_fast<true, 1>,
+// k_mod_cand, k_mod_fast<true, 3>).
+int mod_form(const lphy_hip_ctx* c, size_t frames, size_t nsyms) {
+    const size_t ns = nsyms + 2, nph = frames * ns;
+    if (!LPHY_MOD_FAST || nph >= mod_walk_all_below || ns > (size_t)kModFastSyms) return 0;
+    const size_t lds = ns * (((size_t)c->N * c->osr + 4) * sizeof(float) + kModFastWin);
+    return lds <= mod_fast_limits(c->device).lds ? 1 : 2;
+}
+
 size_t mod_scratch_bytes(const lphy_hip_ctx* c, size_t frames, size_t nsyms) {
     const size_t nph = frames * (nsyms + 2);
     return align_up(nph * sizeof(float)) +
-           (nph < mod_walk_all_below ? align_up(nph * (size_t)c->N * c->osr * sizeof(float)) : 0);
+           (nph < mod_walk_all_below ? align_up(nph * (size_t)c->N * c->osr * sizeof(float)) : 0) +
+           (mod_form(c, frames, nsyms) == 2
+                ? align_up(frames * sizeof(ModFastG)) + align_up(frames * (size_t)kModFastSyms * kModFastWin)
+                : 0);
 }
 
 // k_mod_fast's dynamic LDS limit on the context's device, found once per
 // device: the device's LDS per workgroup less the kernel's static LDS
 // (ModFastShared), and the kernel's attribute raised to it once, outside the
 // per-packet path (the limit was a gfx950 constant, set per call).
-struct ModFastLimits {
-    size_t lds = 0;
-};
 const ModFastLimits& mod_fast_limits(int device) {
     static ModFastLimits lim[64];
     static std::once_flag once[64];
@@ -679,9 +696,9 @@ const ModFastLimits& mod_fast_limits(int device) {
             stat = fa.sharedSizeBytes;
         size_t avail = per_block > 0 && (size_t)per_block > stat ? (size_t)per_block - stat : 0;
         if (avail > kModFastLds) avail = kModFastLds;
-        for (const void* k : {reinterpret_cast<const void*>(k_mod_fast<false>), reinterpret_cast<const void*>(k_mod_fast<true>)})
-            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)avail) != hipSuccess)
-                avail = std::min<size_t>(avail, size_t(64) << 10);  // the default limit stands
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_mod_fast<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)avail) != hipSuccess)
+            avail = std::min<size_t>(avail, size_t(64) << 10);  // the default limit stands
         lim[d].lds = avail;
         (void)hipSetDevice(cur);
     });
@@ -709,25 +726,35 @@ int modulate_impl(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames, size_t
     // few symbols: every sample's phase from the walk, then sample-parallel
     // sincos (a per-symbol pass would run a handful of threads N steps each)
     const bool walk_all = nph < mod_walk_all_below;
+    const int form = mod_form(c, frames, nsyms);
     StreamScratch scratch(st, lent);
-    if (int rc = scratch.get(align_up(nph * sizeof(float)) + (walk_all ? samples * sizeof(float) : 0))) return rc;
+    if (int rc = scratch.get(mod_scratch_bytes(c, frames, nsyms))) return rc;
     A.phase0 = static_cast<float*>(scratch.p);
     A.phases = walk_all ? reinterpret_cast<float*>(static_cast<char*>(scratch.p) + align_up(nph * sizeof(float)))
                         : nullptr;
+    if (form == 2) {
+        char* g = static_cast<char*>(scratch.p) + align_up(nph * sizeof(float)) + align_up(samples * sizeof(float));
+        A.mfg = reinterpret_cast<ModFastG*>(g);
+        A.mft = reinterpret_cast<unsigned char*>(g + align_up(frames * sizeof(ModFastG)));
+    }
     // ... then the walk by candidate windows and a chain of lookups
     // (k_mod_fast): with the f rows in LDS when they fit there beside the
     // kernel's static LDS (up to SF 9 at 66 symbols), else in A.phases
-    // (k_mod_fast<true>), then the sincos
+    // (k_mod_fast<true, 1> / k_mod_cand / k_mod_fast<true, 3>), then the sincos
     const int stride = (int)(c->N * c->osr) + 4;
     const size_t ns = nsyms + 2;
     const size_t lds = ns * ((size_t)stride * sizeof(float) + kModFastWin);
-    const ModFastLimits& lim = mod_fast_limits(c->device);
-    if (LPHY_MOD_FAST && walk_all && ns <= (size_t)kModFastSyms && (lds <= lim.lds || ns * kModFastWin <= lim.lds)) {
-        if (lds <= lim.lds)
-            hipLaunchKernelGGL(k_mod_fast<false>, dim3((unsigned)frames), dim3(kModFastThreads), lds, st, A, stride);
-        else
-            hipLaunchKernelGGL(k_mod_fast<true>, dim3((unsigned)frames), dim3(kModFastThreads), ns * kModFastWin, st,
-                               A, (int)(c->N * c->osr));
+    if (form == 1 || form == 2) {
+        if (form == 1) {
+            hipLaunchKernelGGL((k_mod_fast<false>), dim3((unsigned)frames), dim3(kModFastThreads), lds, st, A, stride);
+        } else {
+            // (the candidate walks, 64 per symbol boundary, are 64x the work of
+            // a row walk: across the GPU, between the two halves)
+            const int step = (int)(c->N * c->osr);
+            hipLaunchKernelGGL((k_mod_fast<true, 1>), dim3((unsigned)frames), dim3(kModFastThreads), 0, st, A, step);
+            hipLaunchKernelGGL(k_mod_cand, dim3((unsigned)(frames * ((ns - 1 + 3) / 4))), dim3(256), 0, st, A);
+            hipLaunchKernelGGL((k_mod_fast<true, 3>), dim3((unsigned)frames), dim3(kModFastThreads), 0, st, A, step);
+        }
         hipLaunchKernelGGL(k_mod_sincos, dim3((unsigned)((samples + 255) / 256)), dim3(256), 0, st, A,
                            (unsigned long long)samples);
     } else if (walk_all) {

@@ -2514,6 +2514,8 @@ struct ModArgs {
     uint8_t sync;
     unsigned long long* slow;  // (k_mod_fast) frames that took the serial walk
     int force_serial;          // (test build) k_mod_fast takes its serial walk for every frame
+    struct ModFastG* mfg;      // (k_mod_fast GROWS, split) per frame: windows, pivots, chain start
+    unsigned char* mft;        // (ditto) per frame: T, kModFastSyms x kModFastWin
 };
 
 __device__ __forceinline__ float mod_f0(const ModArgs& A, unsigned long long f, unsigned long long s) {
@@ -2738,6 +2740,13 @@ __device__ __forceinline__ float f_unord(int o) {
     return __int_as_float(o >= 0 ? o : (int)(0x80000000u - (unsigned)o));
 }
 
+// The split GROWS form's hand-over between its launches (per frame).
+struct ModFastG {
+    int base[kModFastSyms];
+    int kp[kModFastSyms];
+    int j0, ok;
+};
+
 struct ModFastShared {
     double est[kModFastSyms + 1];  // start estimates
     double tot[kModFastSyms];      // exact sum of each f row
@@ -2752,17 +2761,55 @@ struct ModFastShared {
 
 // f rows read 8 at a time: one LDS round trip per 8 steps of a walk, the
 // loads of a block issued before its adds (and stores)
-template <class Fn>
+// (PF, rows in global memory: the next block's loads are issued before the
+// current block's steps, so a walk waits for a cache round trip once, not
+// once per block)
+template <bool PF = false, class Fn>
 __device__ __forceinline__ void row_blocks(const float* row, int i0, int i1, Fn fn) {
     int i = i0;
-    for (; i + 8 <= i1; i += 8) {
-        float b[8];
+    if constexpr (PF) {
+        if (i + 8 <= i1) {
+            float b[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) b[k] = row[i + k];
+            for (int k = 0; k < 8; ++k) b[k] = row[i + k];
+            for (; i + 8 <= i1; i += 8) {
+                const int nx = i + 16 <= i1 ? i + 8 : i;  // (past the last block: a re-read)
+                float nb[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) fn(i + k, b[k]);
+                for (int k = 0; k < 8; ++k) nb[k] = row[nx + k];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) fn(i + k, b[k]);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) b[k] = nb[k];
+            }
+        }
+    } else {
+        for (; i + 8 <= i1; i += 8) {
+            float b[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) b[k] = row[i + k];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) fn(i + k, b[k]);
+        }
     }
     for (; i < i1; ++i) fn(i, row[i]);
+}
+
+// sum of row s's samples [0, i1[s]) in double, a wave per row (GROWS: the
+// rows are in global memory and every thread of the workgroup helps; the
+// sums are estimates, exact to far below a float step)
+template <class I1>
+__device__ __forceinline__ void mf_row_sums(double* out, const float* rows, int stride, int ns, int tid, I1 i1) {
+    const int wave = tid >> 6, lane = tid & 63, nw = kModFastThreads / 64;
+    for (int s = wave; s < ns; s += nw) {
+        const float* row = rows + (size_t)s * stride;
+        const int n = i1(s);
+        double t = 0.0;
+        for (int i = lane; i < n; i += 64) t += (double)row[i];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) t += __shfl_xor(t, off, 64);
+        if (lane == 0) out[s] = t;
+    }
 }
 
 // est[s] = sum over r < s of (a[r] + b[r]) (exclusive prefix, unwrapped),
@@ -2793,7 +2840,10 @@ __device__ __forceinline__ void mf_scan(double* est, const double* a, const doub
 #else
 #define MF_T(k)
 #endif
-template <bool GROWS>
+// PART (GROWS only): 0 the whole walk in this launch; 1 steps 1-5, handing
+// the windows, pivots and chain start to A.mfg; 3 steps 7-8 from A.mfg and
+// the T that k_mod_cand (step 6, spread over the GPU) wrote to A.mft.
+template <bool GROWS, int PART = 0>
 __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int stride) {
     extern __shared__ float4 mod_lds[];
     __shared__ ModFastShared M;
@@ -2803,13 +2853,27 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     const int tid = threadIdx.x;
     float* rows = GROWS ? A.phases + f * (unsigned long long)ns * step : reinterpret_cast<float*>(mod_lds);
     // T[s][j]: where candidate j of symbol s lands among symbol s+1's, 255 outside
-    unsigned char* T = GROWS ? reinterpret_cast<unsigned char*>(mod_lds)
-                             : reinterpret_cast<unsigned char*>(rows + (size_t)ns * stride);
+    unsigned char* T = PART != 0 ? A.mft + f * (unsigned long long)(kModFastSyms * kModFastWin)
+                       : GROWS   ? reinterpret_cast<unsigned char*>(mod_lds)
+                                 : reinterpret_cast<unsigned char*>(rows + (size_t)ns * stride);
     const ChirpWalk W = chirp_walk(A);
     const double two_pi = 2.0 * (double)kPi;
 #ifdef LPHY_MODFAST_CLOCKS
     unsigned long long mf_t = 0;
 #endif
+    if constexpr (PART == 3) {
+        // the hand-over of PART 1 (the rows are in A.phases already)
+        const ModFastG& G = A.mfg[f];
+        for (int s = tid; s < ns; s += blockDim.x) {
+            M.base[s] = G.base[s];
+            M.kp[s] = G.kp[s];
+        }
+        if (tid == 0) {
+            M.J[0] = G.j0;
+            M.ok = G.ok;
+        }
+        __syncthreads();
+    } else {
     MF_T(0)
     // 1. f rows (ChirpGenerator.hpp:39-40) and their exact sums
     for (int s = tid; s < ns; s += blockDim.x) {
@@ -2837,8 +2901,9 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
             fr = g[7];
 #pragma unroll
             for (int k = 0; k < 8; ++k) row[i + k] = g[k];
-            t += (((double)g[0] + (double)g[1]) + ((double)g[2] + (double)g[3])) +
-                 (((double)g[4] + (double)g[5]) + ((double)g[6] + (double)g[7]));  // (an estimate)
+            if constexpr (!GROWS)
+                t += (((double)g[0] + (double)g[1]) + ((double)g[2] + (double)g[3])) +
+                     (((double)g[4] + (double)g[5]) + ((double)g[6] + (double)g[7]));  // (an estimate)
         }
         for (; i < step; ++i) {
             fr += W.fstep;
@@ -2846,9 +2911,13 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
             row[i] = fr;
             t += (double)fr;
         }
-        M.tot[s] = t;
+        if constexpr (!GROWS) M.tot[s] = t;
     }
     __syncthreads();
+    if constexpr (GROWS) {  // (the exact sums by the whole workgroup, off the walks' chains)
+        mf_row_sums(M.tot, rows, stride, ns, tid, [&](int) { return step; });
+        __syncthreads();
+    }
     MF_T(1)
     // 2. first estimates of the starts: unwrapped running sums (one add per
     //    symbol in order), wrapped per symbol in parallel
@@ -2868,6 +2937,20 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
         float best = -1.0f;
         int kb = 0;
         int i = 0;
+        if constexpr (GROWS) {
+            // the walk alone (the pivot's partial sum: mf_row_sums below)
+            row_blocks<true>(row, 0, step, [&](int k, float x) {
+                p += x;
+                if ((k & 7) == 7) {
+                    const float a = fabsf(p);
+                    if (a > best) {
+                        best = a;
+                        kb = k;
+                    }
+                }
+            });
+            i = step;
+        }
         for (; i + 8 <= step; i += 8) {
             float b[8];
 #pragma unroll
@@ -2897,6 +2980,10 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
         M.piv[s] = qb;
     }
     __syncthreads();
+    if constexpr (GROWS) {
+        mf_row_sums(M.piv, rows, stride, ns, tid, [&](int s) { return M.kp[s] + 1; });
+        __syncthreads();
+    }
     MF_T(3)
     // 4. corrected estimates (unwrapped, in order); 5. the windows, and
     //    symbol 0's pivot walked exactly from 0
@@ -2910,23 +2997,36 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     if (tid == 0) {
         float p = 0.0f;
         const float* row = rows;
-        row_blocks(row, 0, M.kp[0] + 1, [&](int, float x) { p += x; });
+        row_blocks<GROWS>(row, 0, M.kp[0] + 1, [&](int, float x) { p += x; });
         const int j = f_ord(p) - M.base[0];
         M.J[0] = j;
         if (j < 0 || j >= kModFastWin) M.ok = 0;
     }
     MF_T(4)
+    if constexpr (PART == 1) {
+        __syncthreads();
+        ModFastG& G = A.mfg[f];
+        for (int s = tid; s < ns; s += blockDim.x) {
+            G.base[s] = M.base[s];
+            G.kp[s] = M.kp[s];
+        }
+        if (tid == 0) {
+            G.j0 = M.J[0];
+            G.ok = M.ok;
+        }
+        return;
+    }
     // 6. every candidate of every symbol walked to the next symbol's pivot,
     //    kPer candidates (j = g, g + kGroups, ...) per thread: one read of
     //    the row feeds kPer independent chains (8 from LDS, 16 from GROWS)
     constexpr int kPer = GROWS ? 16 : 8, kGroups = kModFastWin / kPer;
-    for (int idx = tid; idx < (ns - 1) * kGroups; idx += blockDim.x) {
+    for (int idx = tid; idx < (PART == 0 ? (ns - 1) * kGroups : 0); idx += blockDim.x) {
         const int s = idx / kGroups, g = idx - s * kGroups;
         const float* row = rows + (size_t)s * stride;
         float p[kPer];
 #pragma unroll
         for (int m = 0; m < kPer; ++m) p[m] = f_unord(M.base[s] + g + kGroups * m);
-        row_blocks(row, M.kp[s] + 1, step, [&](int, float x) {
+        row_blocks<GROWS>(row, M.kp[s] + 1, step, [&](int, float x) {
 #pragma unroll
             for (int m = 0; m < kPer; ++m) p[m] += x;
         });
@@ -2934,7 +3034,7 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
         for (int m = 0; m < kPer; ++m) p[m] = wrap_phase(p[m]);
         const float* nrow = row + stride;
         const int kn = M.kp[s + 1];
-        row_blocks(nrow, 0, kn + 1, [&](int, float x) {
+        row_blocks<GROWS>(nrow, 0, kn + 1, [&](int, float x) {
 #pragma unroll
             for (int m = 0; m < kPer; ++m) p[m] += x;
         });
@@ -2947,6 +3047,7 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     }
     __syncthreads();
     MF_T(5)
+    }  // (PART != 3)
     // 7. the chain, one wave: lane j holds T[s][j], the next candidate is a
     //    lane read at the current one (uniform); T rows read 16 at a time
     if (tid < 64 && M.ok) {
@@ -2978,7 +3079,7 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
         for (int s = tid; s < ns; s += blockDim.x) {
             float* row = rows + (size_t)s * stride;
             float p = f_unord(M.base[s] + M.J[s]);
-            row_blocks(row, M.kp[s] + 1, step, [&](int i, float x) {
+            row_blocks<GROWS>(row, M.kp[s] + 1, step, [&](int i, float x) {
                 p += x;
                 row[i] = p;
             });
@@ -2988,7 +3089,7 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
         for (int s = tid; s < ns; s += blockDim.x) {
             float* row = rows + (size_t)s * stride;
             float p = M.xs[s];
-            row_blocks(row, 0, M.kp[s] + 1, [&](int i, float x) {
+            row_blocks<GROWS>(row, 0, M.kp[s] + 1, [&](int i, float x) {
                 p += x;
                 row[i] = p;
             });
@@ -3020,6 +3121,55 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     MF_T(7)
 }
 #undef MF_T
+
+// Step 6 of the split GROWS form across the GPU: one thread per candidate
+// (frame f, symbol s < ns - 1, candidate j), a wave per symbol, so the row
+// reads are wave-uniform (scalar loads) and the 64 walks of a symbol run
+// side by side; each walks its candidate from symbol s's pivot through the
+// symbol-end wrap to symbol s + 1's pivot in the reference's float order and
+// records where it lands (T).  Four symbols per 256-thread workgroup.
+__device__ __forceinline__ float mc_walk(const float* __restrict__ row, int i0, int i1, float p) {
+    int i = i0;
+    for (; i < i1 && (i & 3); ++i) p += row[i];
+    // 16 at a time, the next 16 loaded before the current ones are added
+    if (i + 16 <= i1) {
+        float4 a0 = *reinterpret_cast<const float4*>(row + i), a1 = *reinterpret_cast<const float4*>(row + i + 4),
+               a2 = *reinterpret_cast<const float4*>(row + i + 8), a3 = *reinterpret_cast<const float4*>(row + i + 12);
+        for (; i + 16 <= i1; i += 16) {
+            const int nx = i + 32 <= i1 ? i + 16 : i;  // (past the last block: a harmless re-read)
+            const float4 b0 = *reinterpret_cast<const float4*>(row + nx),
+                         b1 = *reinterpret_cast<const float4*>(row + nx + 4),
+                         b2 = *reinterpret_cast<const float4*>(row + nx + 8),
+                         b3 = *reinterpret_cast<const float4*>(row + nx + 12);
+            p += a0.x; p += a0.y; p += a0.z; p += a0.w;
+            p += a1.x; p += a1.y; p += a1.z; p += a1.w;
+            p += a2.x; p += a2.y; p += a2.z; p += a2.w;
+            p += a3.x; p += a3.y; p += a3.z; p += a3.w;
+            a0 = b0; a1 = b1; a2 = b2; a3 = b3;
+        }
+    }
+    for (; i < i1; ++i) p += row[i];
+    return p;
+}
+
+__global__ __launch_bounds__(256) void k_mod_cand(ModArgs A) {
+    const int ns = (int)(A.nsyms + 2);
+    const int per = (ns - 1 + 3) / 4;  // workgroups per frame
+    const unsigned long long f = blockIdx.x / (unsigned)per;
+    const int s = (int)(blockIdx.x % (unsigned)per) * 4 + (int)(threadIdx.x >> 6);
+    const int j = (int)(threadIdx.x & 63);
+    if (s >= ns - 1) return;  // (wave-uniform)
+    const int step = A.N * A.osr;
+    const ModFastG& G = A.mfg[f];
+    const float* row = A.phases + (f * (unsigned long long)ns + (unsigned)s) * (unsigned)step;
+    float p = f_unord(G.base[s] + j);
+    p = mc_walk(row, G.kp[s] + 1, step, p);
+    p = wrap_phase(p);
+    p = mc_walk(row + step, 0, G.kp[s + 1] + 1, p);
+    const int jj = f_ord(p) - G.base[s + 1];
+    A.mft[f * (unsigned long long)(kModFastSyms * kModFastWin) + (unsigned)(s * kModFastWin + j)] =
+        (jj >= 0 && jj < kModFastWin) ? (unsigned char)jj : (unsigned char)255;
+}
 
 __global__ void k_mod_samples(ModArgs A) {
     const unsigned long long g = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3249,27 +3399,36 @@ int launch_wave_mode(const DemodArgs& A, hipStream_t st) {
     }
 }
 
+// k_wave by mode, windowed (Hann, SF 7-11) or not
+template <int SF>
+int launch_wave_sf(const DemodArgs& A, hipStream_t st) {
+    if constexpr (SF <= 11) {
+        if (A.win) {
+            switch (A.mode) {
+                case LPHY_MODE_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_DEMODULATE | kWinBit>(A, st);
+                case LPHY_MODE_LORA_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_LORA_DEMODULATE | kWinBit>(A, st);
+                default: return launch_wave_mode<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE | kWinBit>(A, st);
+            }
+        }
+    } else {
+        if (A.win) return -ENOTSUP;  // (wave_fit: no SF 12 window)
+    }
+    switch (A.mode) {
+        case LPHY_MODE_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_DEMODULATE>(A, st);
+        case LPHY_MODE_LORA_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_LORA_DEMODULATE>(A, st);
+        default: return launch_wave_mode<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>(A, st);
+    }
+}
+
 template <int SF>
 int launch_frames_sf(const DemodArgs& A, hipStream_t st) {
     if constexpr (Geo<SF>::LPS > 64) {
-        if constexpr (SF == 11 || SF == 12) {
-            switch (A.mode) {
-                case LPHY_MODE_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_DEMODULATE>(A, st);
-                case LPHY_MODE_LORA_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_LORA_DEMODULATE>(A, st);
-                default: return launch_wave_mode<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>(A, st);
-            }
-        }
+        if constexpr (SF == 11 || SF == 12) return launch_wave_sf<SF>(A, st);
         (void)A; (void)st;
         return -ENOTSUP;
     } else {
         if constexpr (SF >= 7) {  // the wave-per-symbol geometry down to 2 lanes per symbol
-            if (A.wave) {
-                switch (A.mode) {
-                    case LPHY_MODE_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_DEMODULATE>(A, st);
-                    case LPHY_MODE_LORA_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_LORA_DEMODULATE>(A, st);
-                    default: return launch_wave_mode<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE>(A, st);
-                }
-            }
+            if (A.wave) return launch_wave_sf<SF>(A, st);
         }
         switch (A.mode) {
             case LPHY_MODE_DEMODULATE:

@@ -1001,10 +1001,15 @@ __device__ __forceinline__ WEstU west_unit(KArgs ka, lds_cf32* lbuf, const lds_c
     nm.scale = 1.0f;
     if constexpr (!M0) nm = norm_meta_hot(mx, true, A.no_scratch);
     const bool live = live_frame && nm.status == 0;
+    // (k_wave's windowed form: the Hann window's N floats right after the
+    // down-chirp in LDS, ldnl + N; mode 1: at ldnl itself)
+    constexpr bool WIN = (MODE & kWinBit) != 0;
+    const float* const wl = reinterpret_cast<const float*>(dnl + ((MODE & 3) != LPHY_MODE_LORA_DEMODULATE ? W::N : 0));
 #pragma unroll
     for (int e = 0; e < 64; ++e) {
         cf32 x = v[e];
         if constexpr (!M0) x = cscale(x, nm.scale);
+        if constexpr (WIN) x = cscale(x, wl[l + LPS * e]);  // samp *= window[i] (LoRaDemod.cpp:97-98, phy.cpp:110-111)
         v[e] = live ? x : czero();
     }
     const WTw<SF> T{};  // unused by the exact pass
@@ -1405,7 +1410,12 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     const KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
     // one LDS block: the down-chirp at offset 0 (its wrapped index is then
     // the byte address itself), the waves' buffers after it
-    __shared__ cf32 lds_all[(DN ? N : 0) + W::WPB * W::BUF];
+    // WIN (Hann window, SF 7-11): the window's N floats after the down-chirp
+    // (west_unit finds them there: wwin_of), the waves' buffers after that
+    constexpr bool WIN = (MODE & kWinBit) != 0;
+    static_assert(!WIN || SF <= 11, "k_wave's windowed form: SF 7-11 (SF 12's LDS is full)");
+    constexpr int WOFS = (DN ? N : 0) + (WIN ? N / 2 : 0);  // (cf32 units)
+    __shared__ cf32 lds_all[WOFS + W::WPB * W::BUF];
     __shared__ WFrame frings[W::WPB][W::RING];  // (EPU > 1: the frame records)
     // SPAN: the rotation tables of the (at most two) frames of a unit, by
     // frame parity: [scale] e^{j rate i}, i < 8 LPS, then e^{j rate 8 LPS a}
@@ -1419,11 +1429,15 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     __shared__ cf32 m0tabs[M0T ? W::WPB : 1][2][M0T ? N : 1];
     __shared__ WSettle settles[SPAN ? W::WPB : 1][SPAN ? W::EPU : 1];  // (SPAN: frames to settle)
     cf32* const dnl = lds_all;
-    cf32 (*const sbuf)[W::BUF] = reinterpret_cast<cf32 (*)[W::BUF]>(lds_all + (DN ? N : 0));
+    cf32 (*const sbuf)[W::BUF] = reinterpret_cast<cf32 (*)[W::BUF]>(lds_all + WOFS);
+    float* const wtab = reinterpret_cast<float*>(lds_all + (DN ? N : 0));  // (WIN)
 
     const int tid = threadIdx.x;
     if constexpr (DN) {
         for (int i = tid; i < N; i += 256) dnl[i] = A.down[i];
+    }
+    if constexpr (WIN) {
+        for (int i = tid; i < N; i += 256) wtab[i] = A.win[i];
     }
     __syncthreads();  // the only workgroup barrier: waves are independent below
 
@@ -1587,7 +1601,9 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                         for (int i = lane; i < N; i += 64) {
                             float sn, cs;
                             lphy_libm::sincosf_exact(Rk.rate * (float)i, &sn, &cs);
-                            tm[i] = cmul(dnl[i], cf32{cs, sn});
+                            cf32 t = cmul(dnl[i], cf32{cs, sn});
+                            if constexpr (WIN) t = cscale(t, wtab[i]);  // (build_rtab's order)
+                            tm[i] = t;
                         }
                         return;
                     }
@@ -1657,13 +1673,16 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
 #endif
             constexpr int SD = LPHY_W_STAGE_DEPTH, SB = SD + 1;  // chunks in flight, buffers
             cf32 xq[SB][8], dq[SB][8];
+            constexpr bool WS = WIN && !M0T;  // the window's product in the staging (M0T: in the table)
+            float wq[SB][WS ? 8 : 1];
             // byte address of the down-chirp entry of element 0; element e's
             // is (d0 + 8 LPS e) mod 8 N (mode 2: the window's own chirp indices)
             const unsigned d0 = ((c.base + (unsigned)l) & (unsigned)(N - 1)) << 3;
-            auto ld_chunk = [&](int q, cf32 (&xs)[8], cf32 (&ds)[8]) __attribute__((always_inline)) {
+            auto ld_chunk = [&](int q, cf32 (&xs)[8], cf32 (&ds)[8], float* ws) __attribute__((always_inline)) {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     const int e = 8 * q + i;
+                    if constexpr (WS) ws[i] = wtab[l + LPS * e];
 #ifndef LPHY_ABLATE_W_STAGE  // timing experiments only
                     xs[i] = lds_ld(buf, rb + ((LPS * e) << 3));
 #else
@@ -1675,10 +1694,10 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                 }
             };
 #pragma unroll
-            for (int q = 0; q < SD; ++q) ld_chunk(q, xq[q], dq[q]);
+            for (int q = 0; q < SD; ++q) ld_chunk(q, xq[q], dq[q], wq[q]);
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                if (q + SD < 8) ld_chunk(q + SD, xq[(q + SD) % SB], dq[(q + SD) % SB]);
+                if (q + SD < 8) ld_chunk(q + SD, xq[(q + SD) % SB], dq[(q + SD) % SB], wq[(q + SD) % SB]);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
@@ -1689,6 +1708,9 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                     amax = max3_abs(amax, p.x, p.y);
                     if constexpr (M0T) p = cmul_fma(p, dq[q % SB][i]);  // dechirp and rotation
                     else if constexpr (M0) p = cmul(p, dq[q % SB][i]);
+                    // Hann window (after the max-abs: the normalisation scans
+                    // the samples themselves, LoRaDemod.cpp:60-78, 154-160)
+                    if constexpr (WS) p = cscale(p, wq[q % SB][i]);
                     // (a unit whose symbol is not demodulated transforms whatever
                     // its window holds; nothing of it is stored; the rotation
                     // is applied below, or folded into the Parseval sums)
@@ -1702,7 +1724,9 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
                 amax = half_max<LPS>(amax);
                 am = amax;
             }
-            const float cb1 = cert_bound<SF>(c.rate, c.start, 1.0f, kWaveExtra);
+            // (WIN: + 2 u for the window's product taken in another order than
+            // the reference's, (x [down]) w before the rotation)
+            const float cb1 = cert_bound<SF>(c.rate, c.start, 1.0f, kWaveExtra + (WIN ? 2.0f : 0.0f));
             int sym = 0;         // the symbol's bin (certified) ...
             float cgap = -1.0f;  // ... and its certified lead (-1: not certified)
             bool pv = false;     // the whole unit certified by Parseval
