@@ -294,7 +294,9 @@ def check_gathered(parts, sf: int, frames: int, world: int) -> dict:
         want = rank_payloads(sf, frames, r)
         m = rec.reshape(-1).view(meta_dt)
         ok_pay += int((pay == want).all(axis=1).sum())
-        ok_sym += int((syms == lphy.encode_payloads(want)).all(axis=1).sum())
+        # (the modulator sends codeword c as bin c mod N: below SF 8 the
+        # demodulated symbol is the codeword's low SF bits)
+        ok_sym += int((syms == (lphy.encode_payloads(want) & ((1 << sf) - 1))).all(axis=1).sum())
         ok_rec += int(((m["status"] == 0) & (m["sync_word"] == 0x12) & (m["have_sync"] == 1)).sum())
     total = world * frames
     return {"frames": total, "payloads_recovered": ok_pay, "symbols_exact": ok_sym,
@@ -533,11 +535,13 @@ def run_c3(args, baseline, world, rank, dev) -> dict:
         parts = gat.finish()
         if rank == 0:
             # the whole stream, every rank's buckets put back in frame order
-            allp = shard.mixed_plan(total, 1, 0, payload=PAYLOAD)[3]
+            _, _, alls, allp, _ = shard.mixed_plan(total, 1, 0, payload=PAYLOAD)
             gs, got, gm = shard.gather_mixed(parts, total, world, DATA_SYMS, PAYLOAD)
             m = gm.reshape(-1).view(lphy.META_DTYPE)
+            # (codeword c arrives as bin c mod N)
+            want_s = lphy.encode_payloads(allp) & ((1 << alls.astype(np.int64)) - 1)[:, None].astype(np.uint16)
             gathered = {"frames": int(total), "stream_in_order": bool(np.array_equal(got, allp)),
-                        "symbols_exact": bool(np.array_equal(gs, lphy.encode_payloads(allp))),
+                        "symbols_exact": bool(np.array_equal(gs, want_s)),
                         "records_ok": int(((m["status"] == 0) & (m["sync_word"] == 0x12)).sum())}
         for wl in buckets:
             wl.run(mode_b)  # slot 0 again for the local checks below

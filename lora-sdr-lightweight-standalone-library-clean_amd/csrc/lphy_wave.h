@@ -1536,7 +1536,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     // offsets put every tone between two bins; noise) pays one attempt per
     // 2^kPvBackoff frames instead of one per frame; a success resets m.
 #ifndef LPHY_PV_BACKOFF  // (-D0: an attempt on every frame, the round-5 rule; timing A/B)
-#define LPHY_PV_BACKOFF 4
+#define LPHY_PV_BACKOFF 6
 #endif
     constexpr unsigned kPvBackoff = LPHY_PV_BACKOFF;
     unsigned pv_miss = 0, pv_wait = 0;

@@ -192,3 +192,33 @@ def test_balanced_ranges_by_cost(world):
         assert a + n == b
     loads = [cost[a:a + n].sum() for a, n in spans]
     assert max(loads) - min(loads) <= 2.5 * cost.max()  # within a couple of frames
+
+
+@pytest.mark.parametrize("sf", [7, 9])
+def test_check_gathered_counts_every_rank(oracle, sf):
+    """bench.check_gathered (rank 0's check of the gathered slabs) on slabs
+    the oracle fills for 2 ranks: every frame's symbols, payload and record
+    count as correct.  Below SF 8 the modulator sends codeword c as bin
+    c mod N, so the demodulated symbols are the codewords'
+    low SF bits: a check against the codewords themselves counted no SF 7
+    frame (the round-5 rehearsal lines' symbols_exact 0)."""
+    import bench
+    import lphy
+    frames, world = 3, 2
+    parts = []
+    for r in range(world):
+        pays = bench.rank_payloads(sf, frames, r)
+        slab = shard.ResultSlab([frames], bench.DATA_SYMS, bench.PAYLOAD, torch.device("cpu"))
+        sv, pv, mv = slab.views(0)
+        meta = np.zeros(frames, lphy.META_DTYPE)
+        for i in range(frames):
+            x = oracle.modulate(lphy.encode_payloads(pays[i:i + 1])[0], sf)
+            _, syms, sync, _ = oracle.lora_demodulate(oracle.dechirp(x, sf), sf)
+            sv[i * bench.DATA_SYMS:(i + 1) * bench.DATA_SYMS] = torch.from_numpy(syms.astype(np.int16))
+            pv[i * bench.PAYLOAD:(i + 1) * bench.PAYLOAD] = torch.from_numpy(oracle.lora_decode(syms)[1].copy())
+            meta["sync_word"][i] = sync
+            meta["have_sync"][i] = 1
+        mv[:] = torch.from_numpy(meta.view(np.uint8).reshape(-1).copy())
+        parts.append(slab.buf)
+    got = bench.check_gathered(parts, sf, frames, world)
+    assert got["all_ok"], got
