@@ -108,7 +108,7 @@ LPHY_HD void sincos_poly(double x, double x2, const SinCosCoef& p, int n,
 }
 
 // 2/pi as 24 overlapping 32-bit windows (Payne-Hanek table).
-LPHY_HD uint32_t inv_pio4(int i) {
+LPHY_HD uint32_t inv_pio4_table(int i) {
     // static: one read-only table (constant memory on the device), not a
     // per-call private array (scratch) that every inlined copy would fill
     static constexpr uint32_t t[24] = {
@@ -119,6 +119,30 @@ LPHY_HD uint32_t inv_pio4(int i) {
         0x34ddc0dbu, 0xddc0db62u, 0xc0db6295u, 0xdb629599u,
         0x6295993cu, 0x95993c43u, 0x993c4390u, 0x3c439041u};
     return t[i];
+}
+// The same windows without a memory access: window i is the 32 bits of the
+// 192-bit string W0:W1:W2 (the table's 24 bytes, big-endian) that end at
+// byte i, i.e. the low word of (W0:W1:W2) >> 8 (23 - i).  On the device a
+// table load is a global load whose wait (vmcnt) also waits for every
+// older vector-memory operation of the wave - in the fused kernels the next
+// unit's LDS-DMA - and at the low occupancy of k_post's exact re-runs each
+// costs a memory round trip.  Checked against the table for every i
+// (tests/test_cpu_checks.py via lphy_oracle / libm_exact_check).
+LPHY_HD uint32_t inv_pio4_shift(int i) {
+    const uint64_t W0 = 0xa2f9836e4e441529ull, W1 = 0xfc2757d1f534ddc0ull, W2 = 0xdb6295993c439041ull;
+    const int s = 8 * (23 - i);  // 0 .. 184
+    const int k = s >> 6, r = s & 63;
+    const uint64_t lo = k == 0 ? W2 : (k == 1 ? W1 : W0);
+    const uint64_t hi = k == 0 ? W1 : (k == 1 ? W0 : 0ull);
+    const uint64_t v = r == 0 ? lo : ((lo >> r) | (hi << (64 - r)));
+    return (uint32_t)v;
+}
+LPHY_HD uint32_t inv_pio4(int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return inv_pio4_shift(i);
+#else
+    return inv_pio4_table(i);
+#endif
 }
 
 // Large |y| (>= 120) and Inf/NaN: glibc's Payne-Hanek path (reduce_large).

@@ -28,6 +28,12 @@ static bool same(float a, float b) {
 int main(int argc, char** argv) {
     if (argc < 4) { fprintf(stderr, "usage\n"); return 2; }
     const char* what = argv[1];
+    if (!strcmp(what, "pio4")) {  // the device's shift form of the Payne-Hanek windows == the table, every index
+        int bad_w = 0;
+        for (int i = 0; i < 24; ++i) bad_w += lphy_libm::inv_pio4_shift(i) != lphy_libm::inv_pio4_table(i);
+        printf("mismatches=%d checked=24\n", bad_w);
+        return bad_w ? 1 : 0;
+    }
     int threads = argc > 4 ? atoi(argv[4]) : 8;
     std::atomic<uint64_t> bad{0}, checked{0};
     std::vector<std::thread> th;

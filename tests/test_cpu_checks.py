@@ -45,6 +45,14 @@ def test_sincosf_exact_ranges(bins, name):
     assert "mismatches=0" in r.stdout
 
 
+def test_payne_hanek_windows_without_memory(bins):
+    """The device's memory-free Payne-Hanek windows (libm_exact.h
+    inv_pio4_shift: shifts of the 2/pi bit string) equal glibc's table for
+    every index, so the large-argument sincos path is unchanged bit for bit."""
+    r = subprocess.run([str(bins / "libm_check"), "pio4", "0", "0"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "mismatches=0 checked=24" in r.stdout, r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("what,seed", [("atan2", 1), ("atan2", 2), ("cabs", 3)])
 def test_atan2f_cabsf_exact(bins, what, seed):
     r = subprocess.run([str(bins / "libm_check"), what, "2000000", str(seed), "8"],
