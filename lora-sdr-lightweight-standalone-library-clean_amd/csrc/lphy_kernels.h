@@ -561,12 +561,18 @@ __device__ __forceinline__ void restage_symbol(cf32* lds, const Stage<SF>& stg, 
                                                const SymCtx& c, int lam, const cf32* down,
                                                const float* win, unsigned osr = 1) {
     using G = Geo<SF>;
-#pragma unroll 1
+    // the lane's samples loaded first, all in flight together (one memory
+    // round trip for the symbol: k_post re-runs run at low occupancy, where
+    // a load per sincos cost a round trip each - mode A's ~6,600 re-runs at
+    // SF 7 took 43 us)
+    cf32 raw[G::E];
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) raw[e] = src[(unsigned)(lam + e * G::LPS) * osr];
+#pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const int i = lam + e * G::LPS;
         const float ph = c.start + c.rate * (float)i;
-        stg.put(lds, e, rotate_sample<SF, MODE, AG>(src[(unsigned)i * osr], i, c, down, win,
-                                                    lphy_libm::sincosf_needs_large(ph)));
+        stg.put(lds, e, rotate_sample<SF, MODE, AG>(raw[e], i, c, down, win, lphy_libm::sincosf_needs_large(ph)));
     }
 }
 
@@ -2201,34 +2207,65 @@ __device__ void recheck_frames(const DemodArgs& A, unsigned long long fb, bool m
     unsigned long long done = 0;
     lphy_frame_meta mm{};
     if (mine) mm = A.meta[fb + tid];
+    // Rows of up to 64 aligned data symbols (every bench shape): the row's
+    // sentinels as a bit mask from its words loaded at once (one memory round
+    // trip per frame; a load per symbol, then per 8, made the scan k_post's
+    // longest part at mode A's ~6,600 re-runs per SF 7 launch)
+    const bool hs0 = mm.have_sync != 0;
+    const uint16_t* const out0 = A.syms + (fb + (unsigned)tid) * A.out_per_frame;
+    const unsigned ofs0 = hs0 ? 2u : 0u;
+    const bool fastscan = A.out_per_frame <= 64 && (A.out_per_frame & 7) == 0 && ((unsigned long long)out0 & 15ull) == 0ull &&
+                          S == A.out_per_frame + ofs0;
+    unsigned long long smask = 0;  // bit b: data symbol b is a sentinel; bits 62/63: sw0/sw1 (shifted below)
+    unsigned smask_sync = 0;
+    if (mine && fastscan) {
+        uint4 q[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w)
+            if (w * 8 < (int)A.out_per_frame) q[w] = reinterpret_cast<const uint4*>(out0)[w];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            if (w * 8 >= (int)A.out_per_frame) break;
+            const unsigned x[4] = {q[w].x, q[w].y, q[w].z, q[w].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if ((x[k] & 0xffffu) == kSymRecheck) smask |= 1ull << (8 * w + 2 * k);
+                if ((x[k] >> 16) == kSymRecheck) smask |= 1ull << (8 * w + 2 * k + 1);
+            }
+        }
+        if (hs0) smask_sync = (mm.sw0 == kSymRecheck ? 1u : 0u) | (mm.sw1 == kSymRecheck ? 2u : 0u);
+    }
     for (;;) {
         __syncthreads();
         if (tid == 0) sh.count = 0;
         __syncthreads();
         // collect up to kTile open symbols
-        if (cur < S) {
+        if (cur < S && fastscan) {
+            for (;;) {
+                // the next sentinel at or after cur
+                unsigned next = S;
+                if (cur < ofs0) {
+                    const unsigned sm = smask_sync >> cur;
+                    if (sm) next = cur + (unsigned)(__ffs(sm) - 1);
+                }
+                if (next == S) {
+                    const unsigned d = cur > ofs0 ? cur - ofs0 : 0u;
+                    const unsigned long long m = d < 64 ? (smask >> d) << d : 0ull;
+                    if (m) next = ofs0 + (unsigned)(__ffsll((long long)m) - 1);
+                }
+                cur = next;
+                if (cur >= S) break;
+                const unsigned k = atomicAdd(&sh.count, 1u);
+                if (k >= kTile) break;  // full: this symbol goes in the next round
+                sh.list[k] = cur;
+                sh.listf[k] = (unsigned)tid;
+                ++cur;
+            }
+        } else if (cur < S) {
             const unsigned long long f = fb + tid;
             const bool hs = mm.have_sync != 0;
             const uint16_t* out = A.syms + f * A.out_per_frame;
-            const unsigned ofs = hs ? 2u : 0u;
             for (; cur < S; ++cur) {
-                if (cur >= ofs) {
-                    // eight data symbols at once where they sit in one aligned
-                    // 16-B word: a clean word is skipped whole (one load per 8
-                    // symbols instead of a dependent load per symbol; mode A's
-                    // SF 7 fix-up 41 -> see DESIGN)
-                    const unsigned d = cur - ofs;
-                    const uint16_t* p = out + d;
-                    if ((d & 7u) == 0u && d + 8u <= (unsigned)A.out_per_frame &&
-                        ((unsigned long long)p & 15ull) == 0ull) {
-                        const uint4 q = *reinterpret_cast<const uint4*>(p);
-                        auto hit = [](unsigned x) { return (x & 0xffffu) == kSymRecheck || (x >> 16) == kSymRecheck; };
-                        if (!(hit(q.x) || hit(q.y) || hit(q.z) || hit(q.w))) {
-                            cur += 7u;  // (+1 by the loop)
-                            continue;
-                        }
-                    }
-                }
                 const uint16_t v = (hs && cur < 2) ? (cur == 0 ? mm.sw0 : mm.sw1) : out[hs ? cur - 2 : cur];
                 if (v != kSymRecheck) continue;
                 const unsigned k = atomicAdd(&sh.count, 1u);
