@@ -164,20 +164,21 @@ inline bool frames_fit(unsigned sf, unsigned osr, int est_units, size_t total) {
 }
 
 // Whether the fused kernel k_wave (64 x 64 values per wavefront unit)
-// takes this batch: SF 7-12, osr 1, the two-symbol estimate, no window, the
-// certified rotation, in modes 1/2 the speculative normalisation, and below
-// SF 9 at least one unit of symbols per frame (4096 / N: its units span
-// frames there); a Hann window up to SF 11 (round 6: its N floats beside the
-// down-chirp in LDS; SF 12's LDS is full).  LPHY_F_EXACT_ROTATION, the
-// pre-scan schedule, shorter frames and SF 12 windows stay on k_frames (SF
-// <= 10) or the separate launches (SF 11-12).
+// takes this batch: SF 7-12, osr 1, the two-symbol estimate, the certified
+// rotation, in modes 1/2 the speculative normalisation, and below SF 9 at
+// least one unit of symbols per frame (4096 / N: its units span frames
+// there); with or without the Hann window (round 6: its N floats beside the
+// down-chirp in LDS; SF 12 with three waves per workgroup, wave_wpb, and not
+// in mode 1, whose windowed k_wave spilled).
+// LPHY_F_EXACT_ROTATION, the pre-scan schedule and shorter frames stay on
+// k_frames (SF <= 10) or the separate launches (SF 11-12).
 #ifndef LPHY_WAVE_MIN_SF  // smallest SF on k_wave (-D for timing experiments only)
 #define LPHY_WAVE_MIN_SF 7
 #endif
-inline bool wave_fit(unsigned sf, unsigned osr, int window, int est_units, size_t total, int mode,
-                     const DemodArgs& A) {
+inline bool wave_fit(unsigned sf, unsigned osr, int est_units, size_t total, int mode, const DemodArgs& A) {
     return sf >= LPHY_WAVE_MIN_SF && sf <= 12 && (sf >= 9 || total >= (size_t)(4096u >> sf)) && osr == 1 &&
-           (window == LPHY_WINDOW_NONE || sf <= 11) && est_units == 2 && total >= 2 && !A.exact_rotation &&
+           !(sf == 12 && A.win && mode == LPHY_MODE_LORA_DEMODULATE) && est_units == 2 && total >= 2 &&
+           !A.exact_rotation &&
            (mode == LPHY_MODE_DEMODULATE || A.spec);
 }
 
@@ -514,7 +515,7 @@ int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t f
     // c: the co-running kernels slowed each other ~2x, 1.1x slower overall.)
     // (LPHY_F_FRAMES_KERNEL, test build: k_frames where k_wave would run -
     // SF 7-10; the matrix-core tests)
-    const bool wfit = wave_fit(c->sf, c->osr, c->window, A.est_units, total, mode, A) &&
+    const bool wfit = wave_fit(c->sf, c->osr, A.est_units, total, mode, A) &&
                       !(flags & LPHY_F_FRAMES_KERNEL);
     const bool fused = (all || (stages & both) == both) && !(flags & LPHY_F_UNFUSED) &&
                        frames >= fused_min_frames(c) && (frames_fit(c->sf, c->osr, A.est_units, total) || wfit);

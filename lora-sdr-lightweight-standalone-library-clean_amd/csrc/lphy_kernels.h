@@ -3416,19 +3416,20 @@ template <int SF, int MODE>
 int launch_wave_mode(const DemodArgs& A, hipStream_t st) {
     FrameArgs P{};
     P.A = A;
+    constexpr int WPB = wave_wpb<SF, MODE>();
     unsigned long long blocks = (unsigned long long)cu_count();
-    const unsigned long long need = (A.frames + WGeo<SF>::WPB - 1) / WGeo<SF>::WPB;
+    const unsigned long long need = (A.frames + WPB - 1) / WPB;
     if (blocks > need) blocks = need;
-    P.waves = (unsigned)(blocks * WGeo<SF>::WPB);
+    P.waves = (unsigned)(blocks * WPB);
     if constexpr (WGeo<SF>::SPW >= LPHY_SPAN_MIN_SPW) {
         if (A.total_syms >= (unsigned long long)WGeo<SF>::SPW) {
-            hipLaunchKernelGGL((k_wave<SF, MODE, true>), dim3((unsigned)blocks), dim3(256), 0, st, P);
+            hipLaunchKernelGGL((k_wave<SF, MODE, true>), dim3((unsigned)blocks), dim3(64 * WPB), 0, st, P);
             HIP_OK(hipGetLastError());
             return 0;
         }
     }
     if constexpr (SF >= 9) {
-        hipLaunchKernelGGL((k_wave<SF, MODE, false>), dim3((unsigned)blocks), dim3(256), 0, st, P);
+        hipLaunchKernelGGL((k_wave<SF, MODE, false>), dim3((unsigned)blocks), dim3(64 * WPB), 0, st, P);
         HIP_OK(hipGetLastError());
         return 0;
     } else {
@@ -3436,19 +3437,17 @@ int launch_wave_mode(const DemodArgs& A, hipStream_t st) {
     }
 }
 
-// k_wave by mode, windowed (Hann, SF 7-11) or not
+// k_wave by mode, windowed (Hann) or not
 template <int SF>
 int launch_wave_sf(const DemodArgs& A, hipStream_t st) {
-    if constexpr (SF <= 11) {
-        if (A.win) {
-            switch (A.mode) {
-                case LPHY_MODE_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_DEMODULATE | kWinBit>(A, st);
-                case LPHY_MODE_LORA_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_LORA_DEMODULATE | kWinBit>(A, st);
-                default: return launch_wave_mode<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE | kWinBit>(A, st);
-            }
+    if (A.win) {
+        switch (A.mode) {
+            case LPHY_MODE_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_DEMODULATE | kWinBit>(A, st);
+            case LPHY_MODE_LORA_DEMODULATE:
+                if constexpr (SF == 12) return -ENOTSUP;  // (wave_fit: the separate launches)
+                else return launch_wave_mode<SF, LPHY_MODE_LORA_DEMODULATE | kWinBit>(A, st);
+            default: return launch_wave_mode<SF, LPHY_MODE_DECHIRP_LORA_DEMODULATE | kWinBit>(A, st);
         }
-    } else {
-        if (A.win) return -ENOTSUP;  // (wave_fit: no SF 12 window)
     }
     switch (A.mode) {
         case LPHY_MODE_DEMODULATE: return launch_wave_mode<SF, LPHY_MODE_DEMODULATE>(A, st);

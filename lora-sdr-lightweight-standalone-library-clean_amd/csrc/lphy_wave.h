@@ -49,7 +49,9 @@
 //
 // LDS: 4 waves x 32 KiB buffers (below 32 lanes per symbol each symbol's
 // rows padded by LPS entries) + the down-chirp (N entries): the whole
-// 160 KiB of a CU at SF 12, one 256-thread workgroup per CU.
+// 160 KiB of a CU at SF 12, one 256-thread workgroup per CU.  SF 12 with
+// the Hann window (round 6, modes 0 / 2): 3 waves (192 threads) x 32 KiB +
+// the down-chirp + the window's N floats, 144 KiB (wave_wpb).
 
 // unroll of the LDS-DMA's run of shifted windows: 4 (the loop's counter,
 // compare and branch per 1 KiB piece were a third of a piece's ~8
@@ -1398,6 +1400,15 @@ struct WFrame {
     int ok;                 // estimate folded, status 0
 };
 
+// waves per workgroup of k_wave<SF, MODE>: 4, but 3 at SF 12 with the
+// window (modes 0 / 2: the window's table does not fit beside four 32 KiB
+// buffers and the down-chirp; SF 12 mode 1 with the window stays on the
+// separate launches, wave_fit: its k_wave spilled 212 B per lane)
+template <int SF, int MODE>
+__host__ __device__ constexpr int wave_wpb() {
+    return (SF == 12 && (MODE & kWinBit) != 0) ? 3 : WGeo<SF>::WPB;
+}
+
 template <int SF, int MODE, bool SPAN = false>
 __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     using W = WGeo<SF>;
@@ -1413,10 +1424,10 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     // WIN (Hann window, SF 7-11): the window's N floats after the down-chirp
     // (west_unit finds them there: wwin_of), the waves' buffers after that
     constexpr bool WIN = (MODE & kWinBit) != 0;
-    static_assert(!WIN || SF <= 11, "k_wave's windowed form: SF 7-11 (SF 12's LDS is full)");
+    constexpr int WPB = wave_wpb<SF, MODE>();  // (SF 12 windowed: 3, the LDS)
     constexpr int WOFS = (DN ? N : 0) + (WIN ? N / 2 : 0);  // (cf32 units)
-    __shared__ cf32 lds_all[WOFS + W::WPB * W::BUF];
-    __shared__ WFrame frings[W::WPB][W::RING];  // (EPU > 1: the frame records)
+    __shared__ cf32 lds_all[WOFS + WPB * W::BUF];
+    __shared__ WFrame frings[WPB][W::RING];  // (EPU > 1: the frame records)
     // SPAN: the rotation tables of the (at most two) frames of a unit, by
     // frame parity: [scale] e^{j rate i}, i < 8 LPS, then e^{j rate 8 LPS a}
     constexpr int RT = 8 * LPS + 8;
@@ -1425,19 +1436,19 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     // dechirp and rotation are one fused product (k_frames' certificate:
     // no charge beyond cert_bound's own, kWaveExtra's two-table share unused)
     constexpr bool M0T = M0 && SPAN && SF <= 8;
-    __shared__ cf32 rtabs[SPAN && !M0T ? W::WPB : 1][2][SPAN && !M0T ? RT : 1];
-    __shared__ cf32 m0tabs[M0T ? W::WPB : 1][2][M0T ? N : 1];
-    __shared__ WSettle settles[SPAN ? W::WPB : 1][SPAN ? W::EPU : 1];  // (SPAN: frames to settle)
+    __shared__ cf32 rtabs[SPAN && !M0T ? WPB : 1][2][SPAN && !M0T ? RT : 1];
+    __shared__ cf32 m0tabs[M0T ? WPB : 1][2][M0T ? N : 1];
+    __shared__ WSettle settles[SPAN ? WPB : 1][SPAN ? W::EPU : 1];  // (SPAN: frames to settle)
     cf32* const dnl = lds_all;
     cf32 (*const sbuf)[W::BUF] = reinterpret_cast<cf32 (*)[W::BUF]>(lds_all + WOFS);
     float* const wtab = reinterpret_cast<float*>(lds_all + (DN ? N : 0));  // (WIN)
 
     const int tid = threadIdx.x;
     if constexpr (DN) {
-        for (int i = tid; i < N; i += 256) dnl[i] = A.down[i];
+        for (int i = tid; i < N; i += 64 * WPB) dnl[i] = A.down[i];
     }
     if constexpr (WIN) {
-        for (int i = tid; i < N; i += 256) wtab[i] = A.win[i];
+        for (int i = tid; i < N; i += 64 * WPB) wtab[i] = A.win[i];
     }
     __syncthreads();  // the only workgroup barrier: waves are independent below
 
@@ -1449,7 +1460,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     const unsigned nframes = (unsigned)A.frames;
     const unsigned S = (unsigned)A.total_syms;
     const unsigned Wn = P.waves;
-    const unsigned w = blockIdx.x * W::WPB + wv;
+    const unsigned w = blockIdx.x * WPB + wv;
     if (w >= nframes) return;
     typename std::conditional<SPAN, WSchedSpan<SF>, WSched<SF>>::type sch;
     if constexpr (SPAN) {

@@ -44,6 +44,7 @@ CASES = [
     (11, 125000, 2, 8, -5.0, 0, False),
     (12, 125000, 2, 8, None, 0, False),
     (12, 500000, 1, 4, -10.0, 0, True),
+    (12, 125000, 3, 16, 0.0, 0, True),
     (5, 125000, 3, 8, None, 0, False),
     (6, 250000, 3, 8, 3.0, 0, False),
 ]
