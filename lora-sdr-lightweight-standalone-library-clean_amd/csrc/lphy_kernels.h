@@ -2798,27 +2798,51 @@ struct ModFastShared {
 
 // f rows read 8 at a time: one LDS round trip per 8 steps of a walk, the
 // loads of a block issued before its adds (and stores)
-// (PF, rows in global memory: the next block's loads are issued before the
-// current block's steps, so a walk waits for a cache round trip once, not
-// once per block)
-template <bool PF = false, class Fn>
+// (PF, rows in global memory, 16-byte aligned: chunks of 16 floats, NB of
+// them in flight - a walk waits for one cache round trip per NB x 16 steps
+// instead of one per 8; round 6: at SF 12 the round trips were most of the
+// split modulator's 390 us per packet)
+template <bool PF = false, int NB = 4, class Fn>
 __device__ __forceinline__ void row_blocks(const float* row, int i0, int i1, Fn fn) {
     int i = i0;
     if constexpr (PF) {
-        if (i + 8 <= i1) {
-            float b[8];
+        for (; i < i1 && (i & 3); ++i) fn(i, row[i]);
+        const int nc = i < i1 ? (i1 - i) >> 4 : 0;
+        if (nc > 0) {
+            const float4* src = reinterpret_cast<const float4*>(row + i);
+            float4 b[NB][4];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) b[k] = row[i + k];
-            for (; i + 8 <= i1; i += 8) {
-                const int nx = i + 16 <= i1 ? i + 8 : i;  // (past the last block: a re-read)
-                float nb[8];
+            for (int k = 0; k < NB; ++k) {
+                const int c = k < nc ? k : nc - 1;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) nb[k] = row[nx + k];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) fn(i + k, b[k]);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) b[k] = nb[k];
+                for (int q = 0; q < 4; ++q) b[k][q] = src[4 * c + q];
             }
+            auto eat = [&](int c, const float4 (&ch)[4]) __attribute__((always_inline)) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int ii = i + 16 * c + 4 * q;
+                    fn(ii, ch[q].x);
+                    fn(ii + 1, ch[q].y);
+                    fn(ii + 2, ch[q].z);
+                    fn(ii + 3, ch[q].w);
+                }
+            };
+            // (whole rounds without branches, so the load counter's waits
+            // stay partial across the loop's back edge; then the rest)
+            int c0 = 0;
+            for (; c0 + NB <= nc; c0 += NB) {
+#pragma unroll
+                for (int k = 0; k < NB; ++k) {
+                    eat(c0 + k, b[k]);
+                    const int cn = c0 + k + NB < nc ? c0 + k + NB : nc - 1;  // (past the end: a harmless re-read)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) b[k][q] = src[4 * cn + q];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NB - 1; ++k)
+                if (c0 + k < nc) eat(c0 + k, b[k]);
+            i += 16 * nc;
         }
     } else {
         for (; i + 8 <= i1; i += 8) {
@@ -3164,31 +3188,8 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
 // reads are wave-uniform (scalar loads) and the 64 walks of a symbol run
 // side by side; each walks its candidate from symbol s's pivot through the
 // symbol-end wrap to symbol s + 1's pivot in the reference's float order and
-// records where it lands (T).  Four symbols per 256-thread workgroup.
-__device__ __forceinline__ float mc_walk(const float* __restrict__ row, int i0, int i1, float p) {
-    int i = i0;
-    for (; i < i1 && (i & 3); ++i) p += row[i];
-    // 16 at a time, the next 16 loaded before the current ones are added
-    if (i + 16 <= i1) {
-        float4 a0 = *reinterpret_cast<const float4*>(row + i), a1 = *reinterpret_cast<const float4*>(row + i + 4),
-               a2 = *reinterpret_cast<const float4*>(row + i + 8), a3 = *reinterpret_cast<const float4*>(row + i + 12);
-        for (; i + 16 <= i1; i += 16) {
-            const int nx = i + 32 <= i1 ? i + 16 : i;  // (past the last block: a harmless re-read)
-            const float4 b0 = *reinterpret_cast<const float4*>(row + nx),
-                         b1 = *reinterpret_cast<const float4*>(row + nx + 4),
-                         b2 = *reinterpret_cast<const float4*>(row + nx + 8),
-                         b3 = *reinterpret_cast<const float4*>(row + nx + 12);
-            p += a0.x; p += a0.y; p += a0.z; p += a0.w;
-            p += a1.x; p += a1.y; p += a1.z; p += a1.w;
-            p += a2.x; p += a2.y; p += a2.z; p += a2.w;
-            p += a3.x; p += a3.y; p += a3.z; p += a3.w;
-            a0 = b0; a1 = b1; a2 = b2; a3 = b3;
-        }
-    }
-    for (; i < i1; ++i) p += row[i];
-    return p;
-}
-
+// records where it lands (T).  Four symbols per 256-thread workgroup; 8
+// chunks of 16 floats in flight per walk (row_blocks).
 __global__ __launch_bounds__(256) void k_mod_cand(ModArgs A) {
     const int ns = (int)(A.nsyms + 2);
     const int per = (ns - 1 + 3) / 4;  // workgroups per frame
@@ -3200,9 +3201,9 @@ __global__ __launch_bounds__(256) void k_mod_cand(ModArgs A) {
     const ModFastG& G = A.mfg[f];
     const float* row = A.phases + (f * (unsigned long long)ns + (unsigned)s) * (unsigned)step;
     float p = f_unord(G.base[s] + j);
-    p = mc_walk(row, G.kp[s] + 1, step, p);
+    row_blocks<true, 8>(row, G.kp[s] + 1, step, [&](int, float x) { p += x; });
     p = wrap_phase(p);
-    p = mc_walk(row + step, 0, G.kp[s + 1] + 1, p);
+    row_blocks<true, 8>(row + step, 0, G.kp[s + 1] + 1, [&](int, float x) { p += x; });
     const int jj = f_ord(p) - G.base[s + 1];
     A.mft[f * (unsigned long long)(kModFastSyms * kModFastWin) + (unsigned)(s * kModFastWin + j)] =
         (jj >= 0 && jj < kModFastWin) ? (unsigned char)jj : (unsigned char)255;
