@@ -2856,6 +2856,54 @@ __device__ __forceinline__ void row_blocks(const float* row, int i0, int i1, Fn 
     for (; i < i1; ++i) fn(i, row[i]);
 }
 
+// The in-place running sum of a global row over [i0, i1) from p (row[i] =
+// p += row[i]), the loads pipelined as row_blocks<true, NB> and each chunk
+// of 16 stored as four 16-byte stores; returns p.
+template <int NB = 4>
+__device__ __forceinline__ float walk_store(float* row, int i0, int i1, float p) {
+    int i = i0;
+    for (; i < i1 && (i & 3); ++i) row[i] = p += row[i];
+    const int nc = i < i1 ? (i1 - i) >> 4 : 0;
+    if (nc > 0) {
+        float4* io = reinterpret_cast<float4*>(row + i);
+        float4 b[NB][4];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            const int c = k < nc ? k : nc - 1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b[k][q] = io[4 * c + q];
+        }
+        auto eat = [&](int c, const float4 (&ch)[4]) __attribute__((always_inline)) {
+            float4 o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                o[q].x = p += ch[q].x;
+                o[q].y = p += ch[q].y;
+                o[q].z = p += ch[q].z;
+                o[q].w = p += ch[q].w;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) io[4 * c + q] = o[q];
+        };
+        int c0 = 0;
+        for (; c0 + NB <= nc; c0 += NB) {
+#pragma unroll
+            for (int k = 0; k < NB; ++k) {
+                eat(c0 + k, b[k]);
+                const int cn = c0 + k + NB < nc ? c0 + k + NB : nc - 1;  // (a chunk not yet stored, or a re-read)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) b[k][q] = io[4 * cn + q];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NB - 1; ++k)
+            if (c0 + k < nc) eat(c0 + k, b[k]);
+        i += 16 * nc;
+    }
+    for (; i < i1; ++i) row[i] = p += row[i];
+    return p;
+}
+
 // sum of row s's samples [0, i1[s]) in double, a wave per row (GROWS: the
 // rows are in global memory and every thread of the workgroup helps; the
 // sums are estimates, exact to far below a float step)
@@ -2960,8 +3008,14 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
                 }
             }
             fr = g[7];
+            if constexpr (GROWS) {  // (global rows, 16-byte aligned: two 16-byte stores)
+                float4* o = reinterpret_cast<float4*>(row + i);
+                o[0] = float4{g[0], g[1], g[2], g[3]};
+                o[1] = float4{g[4], g[5], g[6], g[7]};
+            } else {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) row[i + k] = g[k];
+                for (int k = 0; k < 8; ++k) row[i + k] = g[k];
+            }
             if constexpr (!GROWS)
                 t += (((double)g[0] + (double)g[1]) + ((double)g[2] + (double)g[3])) +
                      (((double)g[4] + (double)g[5]) + ((double)g[6] + (double)g[7]));  // (an estimate)
@@ -3140,20 +3194,28 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
         for (int s = tid; s < ns; s += blockDim.x) {
             float* row = rows + (size_t)s * stride;
             float p = f_unord(M.base[s] + M.J[s]);
-            row_blocks<GROWS>(row, M.kp[s] + 1, step, [&](int i, float x) {
-                p += x;
-                row[i] = p;
-            });
+            if constexpr (GROWS) {
+                p = walk_store(row, M.kp[s] + 1, step, p);
+            } else {
+                row_blocks(row, M.kp[s] + 1, step, [&](int i, float x) {
+                    p += x;
+                    row[i] = p;
+                });
+            }
             M.xs[s + 1 < ns ? s + 1 : 0] = s + 1 < ns ? wrap_phase(p) : 0.0f;
         }
         __syncthreads();
         for (int s = tid; s < ns; s += blockDim.x) {
             float* row = rows + (size_t)s * stride;
             float p = M.xs[s];
-            row_blocks<GROWS>(row, 0, M.kp[s] + 1, [&](int i, float x) {
-                p += x;
-                row[i] = p;
-            });
+            if constexpr (GROWS) {
+                walk_store(row, 0, M.kp[s] + 1, p);
+            } else {
+                row_blocks(row, 0, M.kp[s] + 1, [&](int i, float x) {
+                    p += x;
+                    row[i] = p;
+                });
+            }
         }
     } else if (tid == 0) {
         // the serial walk (k_mod_accumulate's order)
