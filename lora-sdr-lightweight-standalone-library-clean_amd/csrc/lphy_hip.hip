@@ -737,6 +737,7 @@ int modulate_impl(lphy_hip_ctx* c, const uint16_t* d_syms, size_t frames, size_t
         char* g = static_cast<char*>(scratch.p) + align_up(nph * sizeof(float)) + align_up(samples * sizeof(float));
         A.mfg = reinterpret_cast<ModFastG*>(g);
         A.mft = reinterpret_cast<unsigned char*>(g + align_up(frames * sizeof(ModFastG)));
+        A.blk = (int)(nsyms + 2);  // (k_mod_fast<true>'s interleaved rows, read so by k_mod_sincos)
     }
     // ... then the walk by candidate windows and a chain of lookups
     // (k_mod_fast): with the f rows in LDS when they fit there beside the

@@ -2553,6 +2553,8 @@ struct ModArgs {
     int force_serial;          // (test build) k_mod_fast takes its serial walk for every frame
     struct ModFastG* mfg;      // (k_mod_fast GROWS, split) per frame: windows, pivots, chain start
     unsigned char* mft;        // (ditto) per frame: T, kModFastSyms x kModFastWin
+    int blk;                   // 0: phases row after row; else (split form) rows interleaved by
+                               // 16-byte groups, blk = rows per frame (k_mod_fast GROWS)
 };
 
 __device__ __forceinline__ float mod_f0(const ModArgs& A, unsigned long long f, unsigned long long s) {
@@ -2802,20 +2804,25 @@ struct ModFastShared {
 // them in flight - a walk waits for one cache round trip per NB x 16 steps
 // instead of one per 8; round 6: at SF 12 the round trips were most of the
 // split modulator's 390 us per packet)
+// PF: element i of the row at row[(i / 4) bs + i % 4] (bs = 4: contiguous;
+// the split modulator's interleaved rows: 4 x rows per frame)
 template <bool PF = false, int NB = 4, class Fn>
-__device__ __forceinline__ void row_blocks(const float* row, int i0, int i1, Fn fn) {
+__device__ __forceinline__ void row_blocks(const float* row, int bs, int i0, int i1, Fn fn) {
     int i = i0;
     if constexpr (PF) {
-        for (; i < i1 && (i & 3); ++i) fn(i, row[i]);
+        for (; i < i1 && (i & 3); ++i) fn(i, row[(i >> 2) * bs + (i & 3)]);
         const int nc = i < i1 ? (i1 - i) >> 4 : 0;
         if (nc > 0) {
-            const float4* src = reinterpret_cast<const float4*>(row + i);
+            // float4 j of chunk c: group (i / 4) + j
+            auto src = [&](int j) __attribute__((always_inline)) {
+                return reinterpret_cast<const float4*>(row + (size_t)((i >> 2) + j) * (unsigned)bs);
+            };
             float4 b[NB][4];
 #pragma unroll
             for (int k = 0; k < NB; ++k) {
                 const int c = k < nc ? k : nc - 1;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) b[k][q] = src[4 * c + q];
+                for (int q = 0; q < 4; ++q) b[k][q] = *src(4 * c + q);
             }
             auto eat = [&](int c, const float4 (&ch)[4]) __attribute__((always_inline)) {
 #pragma unroll
@@ -2836,7 +2843,7 @@ __device__ __forceinline__ void row_blocks(const float* row, int i0, int i1, Fn 
                     eat(c0 + k, b[k]);
                     const int cn = c0 + k + NB < nc ? c0 + k + NB : nc - 1;  // (past the end: a harmless re-read)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) b[k][q] = src[4 * cn + q];
+                    for (int q = 0; q < 4; ++q) b[k][q] = *src(4 * cn + q);
                 }
             }
 #pragma unroll
@@ -2844,7 +2851,9 @@ __device__ __forceinline__ void row_blocks(const float* row, int i0, int i1, Fn 
                 if (c0 + k < nc) eat(c0 + k, b[k]);
             i += 16 * nc;
         }
+        for (; i < i1; ++i) fn(i, row[(i >> 2) * bs + (i & 3)]);
     } else {
+        (void)bs;  // (rows in LDS: contiguous)
         for (; i + 8 <= i1; i += 8) {
             float b[8];
 #pragma unroll
@@ -2852,26 +2861,29 @@ __device__ __forceinline__ void row_blocks(const float* row, int i0, int i1, Fn 
 #pragma unroll
             for (int k = 0; k < 8; ++k) fn(i + k, b[k]);
         }
+        for (; i < i1; ++i) fn(i, row[i]);
     }
-    for (; i < i1; ++i) fn(i, row[i]);
 }
 
 // The in-place running sum of a global row over [i0, i1) from p (row[i] =
 // p += row[i]), the loads pipelined as row_blocks<true, NB> and each chunk
 // of 16 stored as four 16-byte stores; returns p.
 template <int NB = 4>
-__device__ __forceinline__ float walk_store(float* row, int i0, int i1, float p) {
+__device__ __forceinline__ float walk_store(float* row, int bs, int i0, int i1, float p) {
     int i = i0;
-    for (; i < i1 && (i & 3); ++i) row[i] = p += row[i];
+    auto at = [&](int k) -> float& { return row[(k >> 2) * bs + (k & 3)]; };
+    for (; i < i1 && (i & 3); ++i) at(i) = p += at(i);
     const int nc = i < i1 ? (i1 - i) >> 4 : 0;
     if (nc > 0) {
-        float4* io = reinterpret_cast<float4*>(row + i);
+        auto io = [&](int j) __attribute__((always_inline)) {
+            return reinterpret_cast<float4*>(row + (size_t)((i >> 2) + j) * (unsigned)bs);
+        };
         float4 b[NB][4];
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
             const int c = k < nc ? k : nc - 1;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) b[k][q] = io[4 * c + q];
+            for (int q = 0; q < 4; ++q) b[k][q] = *io(4 * c + q);
         }
         auto eat = [&](int c, const float4 (&ch)[4]) __attribute__((always_inline)) {
             float4 o[4];
@@ -2883,7 +2895,7 @@ __device__ __forceinline__ float walk_store(float* row, int i0, int i1, float p)
                 o[q].w = p += ch[q].w;
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) io[4 * c + q] = o[q];
+            for (int q = 0; q < 4; ++q) *io(4 * c + q) = o[q];
         };
         int c0 = 0;
         for (; c0 + NB <= nc; c0 += NB) {
@@ -2892,7 +2904,7 @@ __device__ __forceinline__ float walk_store(float* row, int i0, int i1, float p)
                 eat(c0 + k, b[k]);
                 const int cn = c0 + k + NB < nc ? c0 + k + NB : nc - 1;  // (a chunk not yet stored, or a re-read)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) b[k][q] = io[4 * cn + q];
+                for (int q = 0; q < 4; ++q) b[k][q] = *io(4 * cn + q);
             }
         }
 #pragma unroll
@@ -2900,21 +2912,33 @@ __device__ __forceinline__ float walk_store(float* row, int i0, int i1, float p)
             if (c0 + k < nc) eat(c0 + k, b[k]);
         i += 16 * nc;
     }
-    for (; i < i1; ++i) row[i] = p += row[i];
+    for (; i < i1; ++i) at(i) = p += at(i);
     return p;
 }
 
 // sum of row s's samples [0, i1[s]) in double, a wave per row (GROWS: the
-// rows are in global memory and every thread of the workgroup helps; the
-// sums are estimates, exact to far below a float step)
+// rows are in global memory, interleaved by 16-byte groups, and every thread
+// of the workgroup helps; the sums are estimates, exact to far below a
+// float step)
 template <class I1>
-__device__ __forceinline__ void mf_row_sums(double* out, const float* rows, int stride, int ns, int tid, I1 i1) {
+__device__ __forceinline__ void mf_row_sums(double* out, const float* rows, int ns, int tid, I1 i1) {
     const int wave = tid >> 6, lane = tid & 63, nw = kModFastThreads / 64;
     for (int s = wave; s < ns; s += nw) {
-        const float* row = rows + (size_t)s * stride;
+        const float* row = rows + 4 * s;
         const int n = i1(s);
+        auto at = [&](int i) { return row[(i >> 2) * 4 * ns + (i & 3)]; };
         double t = 0.0;
-        for (int i = lane; i < n; i += 64) t += (double)row[i];
+        int i = lane;
+        // (16 loads in flight per lane before their adds: one cache round
+        // trip per 1,024 samples, not per 64)
+        for (; i + 64 * 15 < n; i += 64 * 16) {
+            float x[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) x[k] = at(i + 64 * k);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) t += (double)x[k];
+        }
+        for (; i < n; i += 64) t += (double)at(i);
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) t += __shfl_xor(t, off, 64);
         if (lane == 0) out[s] = t;
@@ -2961,6 +2985,13 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     const int ns = (int)(A.nsyms + 2);
     const int tid = threadIdx.x;
     float* rows = GROWS ? A.phases + f * (unsigned long long)ns * step : reinterpret_cast<float*>(mod_lds);
+    // GROWS (round 6): the frame's rows interleaved by 16-byte groups,
+    // element i of row s at ((i / 4) ns + s) 4 + i % 4, so the walks of one
+    // row per lane read and write 1 KiB contiguous per instruction (row
+    // after row, each lane's 16 bytes were a cache line of their own); rowp
+    // and the group stride bs (LDS rows: contiguous, bs = 4)
+    const int bs = GROWS ? 4 * ns : 4;
+    auto rowp = [&](int s) __attribute__((always_inline)) { return GROWS ? rows + 4 * s : rows + (size_t)s * stride; };
     // T[s][j]: where candidate j of symbol s lands among symbol s+1's, 255 outside
     unsigned char* T = PART != 0 ? A.mft + f * (unsigned long long)(kModFastSyms * kModFastWin)
                        : GROWS   ? reinterpret_cast<unsigned char*>(mod_lds)
@@ -2981,13 +3012,16 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
             M.J[0] = G.j0;
             M.ok = G.ok;
         }
+#ifdef LPHY_MODFAST_CLOCKS
+        if (tid == 0) mf_t = wall_clock64();
+#endif
         __syncthreads();
     } else {
     MF_T(0)
     // 1. f rows (ChirpGenerator.hpp:39-40) and their exact sums
     for (int s = tid; s < ns; s += blockDim.x) {
         float fr = W.fmin + mod_f0(A, f, (unsigned long long)s);
-        float* row = rows + (size_t)s * stride;
+        float* row = rowp(s);
         double t = 0.0;
         int i = 0;
         for (; i + 8 <= step; i += 8) {
@@ -3008,10 +3042,9 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
                 }
             }
             fr = g[7];
-            if constexpr (GROWS) {  // (global rows, 16-byte aligned: two 16-byte stores)
-                float4* o = reinterpret_cast<float4*>(row + i);
-                o[0] = float4{g[0], g[1], g[2], g[3]};
-                o[1] = float4{g[4], g[5], g[6], g[7]};
+            if constexpr (GROWS) {  // (two 16-byte groups)
+                *reinterpret_cast<float4*>(row + (size_t)(i >> 2) * bs) = float4{g[0], g[1], g[2], g[3]};
+                *reinterpret_cast<float4*>(row + (size_t)((i >> 2) + 1) * bs) = float4{g[4], g[5], g[6], g[7]};
             } else {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) row[i + k] = g[k];
@@ -3023,14 +3056,14 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
         for (; i < step; ++i) {
             fr += W.fstep;
             if (fr > W.fmax) fr -= (W.fmax - W.fmin);
-            row[i] = fr;
+            row[(i >> 2) * bs + (i & 3)] = fr;
             t += (double)fr;
         }
         if constexpr (!GROWS) M.tot[s] = t;
     }
     __syncthreads();
     if constexpr (GROWS) {  // (the exact sums by the whole workgroup, off the walks' chains)
-        mf_row_sums(M.tot, rows, stride, ns, tid, [&](int) { return step; });
+        mf_row_sums(M.tot, rows, ns, tid, [&](int) { return step; });
         __syncthreads();
     }
     MF_T(1)
@@ -3044,7 +3077,7 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     //    the pivot (largest |phase| among every 8th sample) with the exact
     //    partial sum up to it
     for (int s = tid; s < ns; s += blockDim.x) {
-        const float* row = rows + (size_t)s * stride;
+        const float* row = rowp(s);
         const double e = M.est[s];
         const float x0 = (float)(e - floor(e * (1.0 / two_pi)) * two_pi);
         float p = x0;
@@ -3054,7 +3087,7 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
         int i = 0;
         if constexpr (GROWS) {
             // the walk alone (the pivot's partial sum: mf_row_sums below)
-            row_blocks<true>(row, 0, step, [&](int k, float x) {
+            row_blocks<true>(row, bs, 0, step, [&](int k, float x) {
                 p += x;
                 if ((k & 7) == 7) {
                     const float a = fabsf(p);
@@ -3096,7 +3129,7 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     }
     __syncthreads();
     if constexpr (GROWS) {
-        mf_row_sums(M.piv, rows, stride, ns, tid, [&](int s) { return M.kp[s] + 1; });
+        mf_row_sums(M.piv, rows, ns, tid, [&](int s) { return M.kp[s] + 1; });
         __syncthreads();
     }
     MF_T(3)
@@ -3111,8 +3144,7 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     __syncthreads();
     if (tid == 0) {
         float p = 0.0f;
-        const float* row = rows;
-        row_blocks<GROWS>(row, 0, M.kp[0] + 1, [&](int, float x) { p += x; });
+        row_blocks<GROWS>(rowp(0), bs, 0, M.kp[0] + 1, [&](int, float x) { p += x; });
         const int j = f_ord(p) - M.base[0];
         M.J[0] = j;
         if (j < 0 || j >= kModFastWin) M.ok = 0;
@@ -3137,19 +3169,19 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     constexpr int kPer = GROWS ? 16 : 8, kGroups = kModFastWin / kPer;
     for (int idx = tid; idx < (PART == 0 ? (ns - 1) * kGroups : 0); idx += blockDim.x) {
         const int s = idx / kGroups, g = idx - s * kGroups;
-        const float* row = rows + (size_t)s * stride;
+        const float* row = rowp(s);
         float p[kPer];
 #pragma unroll
         for (int m = 0; m < kPer; ++m) p[m] = f_unord(M.base[s] + g + kGroups * m);
-        row_blocks<GROWS>(row, M.kp[s] + 1, step, [&](int, float x) {
+        row_blocks<GROWS>(row, bs, M.kp[s] + 1, step, [&](int, float x) {
 #pragma unroll
             for (int m = 0; m < kPer; ++m) p[m] += x;
         });
 #pragma unroll
         for (int m = 0; m < kPer; ++m) p[m] = wrap_phase(p[m]);
-        const float* nrow = row + stride;
+        const float* nrow = rowp(s + 1);
         const int kn = M.kp[s + 1];
-        row_blocks<GROWS>(nrow, 0, kn + 1, [&](int, float x) {
+        row_blocks<GROWS>(nrow, bs, 0, kn + 1, [&](int, float x) {
 #pragma unroll
             for (int m = 0; m < kPer; ++m) p[m] += x;
         });
@@ -3192,12 +3224,12 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
         //    pivot) and, from the start that tail's wrap gives the next
         //    symbol, each symbol's head (up to its pivot)
         for (int s = tid; s < ns; s += blockDim.x) {
-            float* row = rows + (size_t)s * stride;
+            float* row = rowp(s);
             float p = f_unord(M.base[s] + M.J[s]);
             if constexpr (GROWS) {
-                p = walk_store(row, M.kp[s] + 1, step, p);
+                p = walk_store(row, bs, M.kp[s] + 1, step, p);
             } else {
-                row_blocks(row, M.kp[s] + 1, step, [&](int i, float x) {
+                row_blocks(row, bs, M.kp[s] + 1, step, [&](int i, float x) {
                     p += x;
                     row[i] = p;
                 });
@@ -3206,12 +3238,12 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
         }
         __syncthreads();
         for (int s = tid; s < ns; s += blockDim.x) {
-            float* row = rows + (size_t)s * stride;
+            float* row = rowp(s);
             float p = M.xs[s];
             if constexpr (GROWS) {
-                walk_store(row, 0, M.kp[s] + 1, p);
+                walk_store(row, bs, 0, M.kp[s] + 1, p);
             } else {
-                row_blocks(row, 0, M.kp[s] + 1, [&](int i, float x) {
+                row_blocks(row, bs, 0, M.kp[s] + 1, [&](int i, float x) {
                     p += x;
                     row[i] = p;
                 });
@@ -3222,10 +3254,11 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
         if (A.slow) atomicAdd(A.slow, 1ull);
         float phase = 0.0f;
         for (int s = 0; s < ns; ++s) {
-            float* row = rows + (size_t)s * stride;
+            float* row = rowp(s);
             for (int i = 0; i < step; ++i) {
-                phase += row[i];
-                row[i] = phase;
+                float& x = row[(i >> 2) * bs + (i & 3)];
+                phase += x;
+                x = phase;
             }
             phase = wrap_phase(phase);
         }
@@ -3234,7 +3267,10 @@ __global__ __launch_bounds__(kModFastThreads) void k_mod_fast(ModArgs A, int str
     // 9. the phases out, row after row (k_mod_sincos, GPU-wide, turns them
     //    into IQ: one CU's sincos would be the longest phase); GROWS: they
     //    are there already
-    if constexpr (GROWS) return;
+    if constexpr (GROWS) {
+        MF_T(7)
+        return;
+    }
     const int count = ns * step;
     float* out = A.phases + f * (unsigned long long)count;
     for (int g = tid; g < count; g += blockDim.x) {
@@ -3261,11 +3297,12 @@ __global__ __launch_bounds__(256) void k_mod_cand(ModArgs A) {
     if (s >= ns - 1) return;  // (wave-uniform)
     const int step = A.N * A.osr;
     const ModFastG& G = A.mfg[f];
-    const float* row = A.phases + (f * (unsigned long long)ns + (unsigned)s) * (unsigned)step;
+    // (the frame's rows interleaved by 16-byte groups, as k_mod_fast<true> writes them)
+    const float* rows = A.phases + f * (unsigned long long)ns * (unsigned)step;
     float p = f_unord(G.base[s] + j);
-    row_blocks<true, 8>(row, G.kp[s] + 1, step, [&](int, float x) { p += x; });
+    row_blocks<true, 8>(rows + 4 * s, 4 * ns, G.kp[s] + 1, step, [&](int, float x) { p += x; });
     p = wrap_phase(p);
-    row_blocks<true, 8>(row + step, 0, G.kp[s + 1] + 1, [&](int, float x) { p += x; });
+    row_blocks<true, 8>(rows + 4 * (s + 1), 4 * ns, 0, G.kp[s + 1] + 1, [&](int, float x) { p += x; });
     const int jj = f_ord(p) - G.base[s + 1];
     A.mft[f * (unsigned long long)(kModFastSyms * kModFastWin) + (unsigned)(s * kModFastWin + j)] =
         (jj >= 0 && jj < kModFastWin) ? (unsigned char)jj : (unsigned char)255;
@@ -3292,8 +3329,14 @@ __global__ void k_mod_samples(ModArgs A) {
 __global__ void k_mod_sincos(ModArgs A, unsigned long long count) {
     const unsigned long long g = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= count) return;
+    unsigned long long src = g;
+    if (A.blk) {  // (the split form's interleaved rows: k_mod_fast<true>)
+        const unsigned long long step = (unsigned long long)A.N * A.osr, fs = step * (unsigned)A.blk;
+        const unsigned long long fb = g / fs * fs, r = g - fb, s = r / step, i = r - s * step;
+        src = fb + ((i >> 2) * (unsigned)A.blk + s) * 4 + (i & 3);
+    }
     float sn, cs;
-    lphy_libm::sincosf_exact(A.phases[g], &sn, &cs);
+    lphy_libm::sincosf_exact(A.phases[src], &sn, &cs);
     A.iq[g] = cf32{A.ampl * cs, A.ampl * sn};
 }
 
