@@ -1421,7 +1421,7 @@ __global__ __launch_bounds__(256, 1) void k_wave(FrameArgs P) {
     const KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
     // one LDS block: the down-chirp at offset 0 (its wrapped index is then
     // the byte address itself), the waves' buffers after it
-    // WIN (Hann window, SF 7-11): the window's N floats after the down-chirp
+    // WIN (Hann window): the window's N floats after the down-chirp
     // (west_unit finds them there: wwin_of), the waves' buffers after that
     constexpr bool WIN = (MODE & kWinBit) != 0;
     constexpr int WPB = wave_wpb<SF, MODE>();  // (SF 12 windowed: 3, the LDS)
