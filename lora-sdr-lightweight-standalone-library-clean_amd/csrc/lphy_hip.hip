@@ -514,7 +514,7 @@ int demod_batch_impl(lphy_hip_ctx* c, const float* d_iq, size_t frames, size_t f
     // two streams, prologue of chunk c+1 beside the symbol kernel of chunk
     // c: the co-running kernels slowed each other ~2x, 1.1x slower overall.)
     // (LPHY_F_FRAMES_KERNEL, test build: k_frames where k_wave would run -
-    // SF 7-10; the matrix-core tests)
+    // SF 7-10; the certificate tests on k_frames)
     const bool wfit = wave_fit(c->sf, c->osr, A.est_units, total, mode, A) &&
                       !(flags & LPHY_F_FRAMES_KERNEL);
     const bool fused = (all || (stages & both) == both) && !(flags & LPHY_F_UNFUSED) &&

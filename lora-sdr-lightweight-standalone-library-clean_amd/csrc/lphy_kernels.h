@@ -48,7 +48,6 @@
 
 
 using namespace lphy;
-#include "lphy_mfma.h"
 
 namespace lphy {
 // ---------------------------------------------------------------------------
@@ -1267,15 +1266,8 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     // rotation tables: per-wave LDS ring of two frames up to SF 8, per-lane
     // registers (built when a team reaches a new frame) for SF 9-10
     constexpr bool RLDS = SF <= 8;
-    // symbol-only tiles of modes 1/2 on the matrix cores (lphy_mfma.h)
-#ifdef LPHY_NO_MFMA  // A/B timing only: the KISS-order transform everywhere
-    constexpr bool MF = SF < 0;  // (dependent: the discarded branches stay unchecked)
-#else
-    constexpr bool MF = MfmaUse<SF>::value && (MODE & 3) != LPHY_MODE_DEMODULATE;
-#endif
     const DemodArgs& A = P.A;
     __shared__ cf32 lds[G::T * G::SSTRIDE];
-    __shared__ typename std::conditional<MF, MfmaTable, char>::type mfk[1];
     __shared__ cf32 twl[N];
     // down-chirp twice over (entry i = down[i mod N]): a symbol window's
     // chirp indices t0 + i, i < N, need no wrap
@@ -1290,9 +1282,6 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
     __shared__ cf32 rtab2[RLDS ? 1 : WPB][RLDS ? 1 : NSLOT][RLDS ? 1 : 64 + N / 64];
 
     const int tid = threadIdx.x;
-    if constexpr (MF) {
-        if (tid < 64) mfk[0].put(tid, mfma_lane_consts<SF>(A.tw, tid));
-    }
     for (int i = tid; i < N; i += kTile) {
         twl[i] = A.tw[i];
         if constexpr (TAB) {
@@ -1615,7 +1604,6 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         __builtin_amdgcn_s_setprio(1);
 #endif
         if (emask) fft_tile<SF, false, false, true>(v, lds, slot, lam, twl);
-        else if constexpr (MF) mfma_symbols<SF>(v, lds, wv * WT, mfk[0], lane);
         else fft_tile<SF, true, false, true>(v, lds, slot, lam, twl);
 
         // (SF <= 8: reduced toward lane lam == 0 by DPP, the only lane that
@@ -1656,9 +1644,7 @@ __global__ __launch_bounds__(kTile, OCC) void k_frames(FrameArgs P) {
         // symbols the certificate does not cover: exact per-sample rotation
         // certificate (fast_certified, written out so that the speculation
         // below reuses its lead and bound): B is linear in amax
-        // (the matrix-core transform charges its f16 roundings, kMfmaExtra)
-        const float cb1 = cert_bound<SF>(c.rate, c.start, 1.0f,
-                                         (RLDS ? 0.0f : 6.0f) + ((MF && !emask) ? kMfmaExtra : 0.0f));
+        const float cb1 = cert_bound<SF>(c.rate, c.start, 1.0f, RLDS ? 0.0f : 6.0f);
         const float cgap = cert_gap(b2);
         const bool cert = cgap > 4.0f * (cb1 * amax) && (float)N * 1.41421366f * amax * 1.0001f < 1e18f &&
                           amax >= 1e-20f && b2.v >= 1e-30f && b2.v < 1e30f;

@@ -283,3 +283,45 @@ def test_awgn_mixed_paths(oracle, lphy, sf, nf, mode):
             assert out[2]["sync_word"][f] == osync, (who, ctx)
             assert _bits(out[2]["cfo"][f]) == _bits(omet[0]), (who, ctx)
             assert _bits(out[2]["time_offset"][f]) == _bits(omet[1]), (who, ctx)
+
+
+@pytest.mark.parametrize("sf,nf", [(11, 24), (12, 12)])
+def test_hann_frames_take_the_wave_kernel(oracle, lphy, sf, nf):
+    """Hann-windowed frames at SF 11-12 run on k_wave (round 6; SF 12 with
+    three waves per workgroup, wave_wpb): the Parseval counter, which only
+    k_wave's certificate moves, proves clean windowed symbols there, and
+    every output bit equals the oracle's windowed lora_demodulate
+    (LoRaDemod.cpp:16-24, 97-98) and the separate launches'."""
+    rng = np.random.default_rng(4400 + sf)
+    N = 1 << sf
+    iq = []
+    for f in range(nf):
+        p = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+        x = oracle.modulate(oracle.encode(p), sf).astype(np.complex128)
+        n = np.arange(x.size)
+        x = x * np.exp(2j * np.pi * rng.uniform(-0.3, 0.3) / N * n) * [0.6, 1.0, 1.7][f % 3]
+        iq.append(x.astype(np.complex64))
+    iq = np.stack(iq)
+    d = lphy.Demodulator(sf, window=lphy.WINDOW_HANN, test_build=True)
+    d.parseval_count(reset=True)
+    got = d.demod_host(iq, nf, iq.shape[1], 2, lphy.F_DECODE)
+    n_pv = d.parseval_count(reset=True)
+    prod = lphy.Demodulator(sf, window=lphy.WINDOW_HANN).demod_host(iq, nf, iq.shape[1], 2, lphy.F_DECODE)
+    ref = lphy.Demodulator(sf, window=lphy.WINDOW_HANN).demod_host(iq, nf, iq.shape[1], 2,
+                                                                   lphy.F_DECODE | lphy.F_UNFUSED)
+    for out in (got, prod):
+        np.testing.assert_array_equal(out[0], ref[0])
+        np.testing.assert_array_equal(out[1], ref[1])
+        np.testing.assert_array_equal(out[2].view(np.uint8), ref[2].view(np.uint8))
+    # (a windowed tone keeps 2/3 of its energy in its bin, less the chirp's
+    # wrap-around leak: a part of the units pass, SF 11 ~28 %; any means
+    # k_wave ran)
+    assert n_pv > 0, n_pv
+    for f in range(0, nf, 4):
+        r, osyms, osync, omet = oracle.lora_demodulate(oracle.dechirp(iq[f], sf), sf, hann=True)
+        ctx = f"sf {sf} hann frame {f}"
+        assert got[2]["status"][f] == 0, ctx
+        np.testing.assert_array_equal(got[0][f], osyms, err_msg=ctx)
+        assert got[2]["sync_word"][f] == osync, ctx
+        assert _bits(got[2]["cfo"][f]) == _bits(omet[0]), ctx
+        assert _bits(got[2]["time_offset"][f]) == _bits(omet[1]), ctx
