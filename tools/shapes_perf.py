@@ -19,7 +19,7 @@ symbol + the 32 B frame record).  Shapes:
 Writes a CSV (shape,sf,osr,mode,frames,symbols_per_frame,ms,symbols_per_s,
 hbm_gbps,roofline_frac) and prints it.  Timing aid; the numbers are the
 product library's (lib/liblphy_hip.so).
-  python tools/shapes_perf.py out.csv [sf ...]      (GPU box)"""
+  python tools/shapes_perf.py out.csv [sf ...] [--shapes mode_A,hann,...]   (GPU box)"""
 import csv
 import sys
 from pathlib import Path
@@ -86,12 +86,20 @@ def run_shape(dev, sf, name, osr, window, mode, nsyms, reps=20, warmup=10):
 
 
 def main():
-    dst = sys.argv[1] if len(sys.argv) > 1 else "shapes.csv"
-    sfs = [int(a) for a in sys.argv[2:]] or [7, 8, 9, 10, 11, 12]
+    args = sys.argv[1:]
+    only = None
+    if "--shapes" in args:
+        i = args.index("--shapes")
+        only = set(args[i + 1].split(","))
+        args = args[:i] + args[i + 2:]
+    dst = args[0] if args else "shapes.csv"
+    sfs = [int(a) for a in args[1:]] or [7, 8, 9, 10, 11, 12]
     dev = torch.device("cuda", 0)
     rows = []
     for sf in sfs:
         for name, osr, window, mode, nsyms in SHAPES:
+            if only is not None and name not in only:
+                continue
             if name.startswith("short") and not ((name == "short16" and sf == 7) or (name == "short8" and sf == 8)):
                 continue
             r = run_shape(dev, sf, name, osr, window, mode, nsyms)
