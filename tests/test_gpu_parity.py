@@ -112,11 +112,12 @@ def test_modulate_bit_exact(oracle, lphy):
 
 @pytest.mark.parametrize("sf,osr,nf,nsyms", [(7, 1, 1, 64), (7, 1, 5, 64), (8, 1, 3, 64), (9, 1, 2, 64),
                                               (5, 3, 4, 21), (7, 2, 2, 30), (3, 3, 3, 7), (2, 1, 2, 5),
-                                              (10, 1, 2, 64), (7, 1, 70, 64)])
+                                              (10, 1, 2, 64), (7, 1, 70, 64), (11, 2, 2, 30), (12, 1, 3, 20)])
 def test_modulate_batch_frames(oracle, lphy, sf, osr, nf, nsyms):
     """lphy_hip_modulate_batch, frame by frame == the oracle: k_mod_fast (f
-    rows in LDS: up to SF 9 at 66 symbols, few frames, osr 2-3 too), the
-    three-kernel few-symbol form (SF 10) and the batch form (70 frames)."""
+    rows in LDS: up to SF 9 at 66 symbols, few frames, osr 2-3 too), its
+    split form with the rows interleaved in the phase buffer (SF 10-12,
+    several frames, osr 2 at SF 11) and the batch form (70 frames)."""
     rng = np.random.default_rng(sf * 100 + nf)
     syms = rng.integers(0, 1 << min(sf, 8), (nf, nsyms), dtype=np.uint16)
     d = lphy.Demodulator(sf, 125000, osr)
