@@ -176,7 +176,7 @@ inline bool frames_fit(unsigned sf, unsigned osr, int est_units, size_t total) {
 #define LPHY_WAVE_MIN_SF 7
 #endif
 inline bool wave_fit(unsigned sf, unsigned osr, int est_units, size_t total, int mode, const DemodArgs& A) {
-    return sf >= LPHY_WAVE_MIN_SF && sf <= 12 && (sf >= 9 || LPHY_SHORT_WAVE || total >= (size_t)(4096u >> sf)) && osr == 1 &&
+    return sf >= LPHY_WAVE_MIN_SF && sf <= 12 && (sf >= 9 || total >= (size_t)(4096u >> sf)) && osr == 1 &&
            !(sf == 12 && A.win && mode == LPHY_MODE_LORA_DEMODULATE) && est_units == 2 && total >= 2 &&
            !A.exact_rotation &&
            (mode == LPHY_MODE_DEMODULATE || A.spec);

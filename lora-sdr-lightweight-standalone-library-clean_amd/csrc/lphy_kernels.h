@@ -3499,9 +3499,6 @@ int launch_demod_sf(const DemodArgs& A, hipStream_t st, bool prologue, bool symb
 // shared exchange buffers, were removed in round 5: with the Parseval
 // certificate and the grouped estimate units k_wave was faster at every SF,
 // DESIGN §4.9.)
-#ifndef LPHY_SHORT_WAVE  // frames shorter than a unit at SF 7-8 on k_wave, one frame per unit (A/B)
-#define LPHY_SHORT_WAVE 0
-#endif
 #ifndef LPHY_SPAN_MIN_SPW  // (-D for timing experiments only)
 #define LPHY_SPAN_MIN_SPW 4
 #endif
@@ -3523,7 +3520,7 @@ int launch_wave_mode(const DemodArgs& A, hipStream_t st) {
             return 0;
         }
     }
-    if constexpr (SF >= 9 || LPHY_SHORT_WAVE) {
+    if constexpr (SF >= 9) {
         hipLaunchKernelGGL((k_wave<SF, MODE, false>), dim3((unsigned)blocks), dim3(64 * WPB), 0, st, P);
         HIP_OK(hipGetLastError());
         return 0;
